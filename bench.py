@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""Benchmark: consensus slots decided/sec on the batched Rabia phase evaluator.
+
+Workload (BASELINE.json configs[1], "C2"): 5 replicas, windows of 2^20 slots,
+90%-agreement synthetic vote trace, REF single phase sweep. One bench "step" is
+one launch over `--windows` consecutive 2^20-slot windows (default 64: the
+steady-state streaming batch; --windows 1 is the single-sweep latency case and is
+also reported as `sweep_1m_us`). Inputs are generated on the device before the
+timed region and rotate over 3 buffer sets (> 2x the 256 MiB Infinity Cache) so
+every step reads from HBM.
+
+Multi-GPU (torchrun, one rank per GPU): every rank is one slot shard with its own
+engine context (weak scaling); after each step the per-shard step results
+(commit watermark, last_committed, counts) are exchanged with an RCCL all_gather
+that overlaps the next step.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (imported before the native library: shared HIP runtime)
+
+from rabia_amd import _native as N  # noqa: E402
+from rabia_amd.engine import PhaseEvaluator  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+WINDOW = 1 << 20
+
+
+def bytes_per_slot_ref(n: int) -> float:
+    """Algorithmic bytes per slot per REF phase evaluation:
+    read R1 + R2 codes (4n bits), write 8 output bits."""
+    return (4 * n + 8) / 8.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--windows", type=int, default=64)
+    ap.add_argument("--replicas", type=int, default=5)
+    ap.add_argument("--sets", type=int, default=3)
+    ap.add_argument("--cpu-sample-windows", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_c2.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(n: int, windows: int):
+    """Structure-faithful REF path (oracle/rabia_oracle.c:or_ref_structured: per-slot
+    NodeId->StateValue maps, one handler call per vote, PhaseData clone per read),
+    single thread, on `windows` x 2^20 slots of the same trace kind."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    S = windows * WINDOW
+    r1, r2, _ = O.trace(1, n, 42, 1, S)
+    t0 = time.perf_counter()
+    _, res = O.ref_structured(n, n // 2 + 1, n - 1, 42, 0, 1, r1, r2)
+    dt = time.perf_counter() - t0
+    return {"value": res["n_decided"] / dt, "unit": "slots decided/s", "cores": 1, "kind": "port",
+            "sample": f"{S} slots ({windows} x 2^20 windows, agree90 trace, n={n}) through the "
+                      f"structure-faithful REF restatement (oracle/rabia_oracle.c:or_ref_structured), "
+                      f"1 thread, {dt:.2f} s"}
+
+
+def load_pmc(path: str, n: int, slots: int):
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("replicas") == n and d.get("slots_per_launch") == slots:
+            return d.get("hbm_bytes_per_launch")
+    except Exception:
+        pass
+    return None
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    n, G = a.replicas, a.windows
+    S = G * WINDOW
+    stride = ((S + 127) // 128) * 4
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+
+    ev = PhaseEvaluator(n, self_lane=n - 1, mode="ref", seed=42 + rank, device=local)
+    sets = []
+    for i in range(a.sets):
+        votes = torch.empty((4 * n + 1) * stride, dtype=torch.int32, device="cuda")
+        out = torch.empty(8 * stride, dtype=torch.int32, device="cuda")
+        ev.trace_generate_async(N.RG_TRACE_AGREE90, 1000 * rank + i, 1 + i * S, S, stride,
+                                votes.data_ptr(), sp)
+        sets.append((votes, out))
+    n_total = a.warmup + a.steps
+    res_dev = torch.zeros((n_total, 10), dtype=torch.int64, device="cuda")
+    gathered = torch.zeros((n_total, world, 10), dtype=torch.int64, device="cuda") if world > 1 else None
+    torch.cuda.synchronize()
+
+    rank_base = 1 + rank * (1 << 40)  # disjoint slot-id range per shard
+    works = []
+
+    def step(t, evs=None):
+        votes, out = sets[t % a.sets]
+        if evs is not None:
+            evs[0].record(stream)
+        ev.phase_step_async(votes.data_ptr(), out.data_ptr(), S, stride,
+                            slot_base=rank_base + t * S, result_ptr=res_dev[t].data_ptr(), stream=sp)
+        if evs is not None:
+            evs[1].record(stream)
+        if dist is not None:  # global commit exchange, overlapped with the next step
+            works.append(dist.all_gather_into_tensor(gathered[t], res_dev[t], async_op=True))
+
+    for t in range(a.warmup):
+        step(t)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(a.steps)]
+    t_begin = torch.cuda.Event(enable_timing=True)
+    t_end = torch.cuda.Event(enable_timing=True)
+    t_begin.record(stream)
+    for k in range(a.steps):
+        step(a.warmup + k, evs[k])
+    for w in works:
+        w.wait()
+    t_end.record(stream)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    total_ms = t_begin.elapsed_time(t_end)
+    kern_ms = [b.elapsed_time(e) for b, e in evs]
+    res = res_dev.cpu().numpy().view(np.uint64)
+    if int(res[:, 9].max()) != 0:
+        raise RuntimeError("device-side protocol fault flagged in a step result")
+    timed = res[a.warmup:]
+    assert (timed[:, 0] == S).all(), "a timed step did not complete"
+    decided_total = int(timed[:, 1].sum())
+    if dist is not None:  # every shard's step results arrived through the exchange
+        g = gathered.cpu().numpy().view(np.uint64)
+        assert (g[a.warmup:, :, 0] == S).all()
+
+    tmax = torch.tensor([total_ms, float(np.mean(kern_ms)), float(decided_total)], dtype=torch.float64,
+                        device="cuda")
+    if dist is not None:
+        t_all = tmax.clone()
+        dist.all_reduce(t_all[:2], op=dist.ReduceOp.MAX)
+        dec_all = tmax[2:].clone()
+        dist.all_reduce(dec_all, op=dist.ReduceOp.SUM)
+        total_ms, kavg_ms, decided_all = float(t_all[0]), float(t_all[1]), float(dec_all[0])
+    else:
+        kavg_ms, decided_all = float(np.mean(kern_ms)), float(decided_total)
+
+    # single-window (C2 one sweep) latency, untimed w.r.t. the headline
+    sweep_us = None
+    if rank == 0:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 20
+        e0.record(stream)
+        for i in range(reps):
+            ev.phase_step_async(sets[i % a.sets][0].data_ptr(), sets[i % a.sets][1].data_ptr(), WINDOW,
+                                stride, slot_base=1, stream=sp)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        sweep_us = e0.elapsed_time(e1) * 1000.0 / reps
+
+    if rank == 0:
+        value = decided_all / (total_ms / 1000.0)
+        alg_bytes = S * bytes_per_slot_ref(n)
+        achieved = alg_bytes / (kavg_ms / 1000.0) / 1e9
+        cpu = None if a.no_cpu_baseline else cpu_baseline(n, a.cpu_sample_windows)
+        line = {
+            "metric": "consensus slots decided/sec (5 replicas, 1M slots) + HBM GB/s as % of peak",
+            "value": value,
+            "unit": "slots decided/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": total_ms / a.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32 bit-sliced 2-bit vote codes (integer only)",
+            "data": "synthetic (seeded agree90 vote trace generated on device)",
+            "config": {"workload": f"C2: {n} replicas x 2^20-slot windows, agree90 trace, REF single phase "
+                                   f"sweep; {G} windows per step per GPU",
+                       "replicas": n, "slots_per_window": WINDOW, "windows_per_step": G,
+                       "slots_per_step_per_gpu": S, "mode": "ref", "parallelism": f"slot-shard x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": load_pmc(a.pmc_file, n, S),
+                         "alg_bytes_per_launch": alg_bytes, "kernel_avg_us": kavg_ms * 1000.0},
+            "cpu_baseline": cpu,
+            "sweep_1m_us": sweep_us,
+        }
+        print(json.dumps(line), flush=True)
+    ev.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

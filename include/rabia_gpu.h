@@ -1,0 +1,175 @@
+/*
+ * rabia_gpu.h — C ABI of the MI355X batched Rabia phase evaluator.
+ *
+ * Drop-in boundary for the phase-evaluation step of rabia-rs's RabiaEngine
+ * (reference @ /root/reference). One call evaluates, for every slot (PhaseId)
+ * of a window, what the reference's handlers compute for that slot one
+ * message at a time:
+ *
+ *   handle_vote_round1 / has_round1_majority  rabia-engine/src/engine.rs:483-509,
+ *                                              rabia-core/src/messages.rs:177-211
+ *   proceed_to_round2 + randomized round-2     engine.rs:511-611
+ *   handle_vote_round2 / make_decision         engine.rs:613-682
+ *   PhaseData::set_decision                    messages.rs:217-222
+ *   EngineState::commit_phase (watermark)      rabia-engine/src/state.rs:65-103
+ *   Weak-MVC rounds + common coin (WMVC mode)  docs/weak_mvc.ivy:109-191
+ *
+ * Plain C types only (no HIP/torch types): streams are passed as `void*`
+ * (a hipStream_t; NULL = the context's own stream). Every entry point returns
+ * RG_OK (0) or a negative rg_status; rg_last_error() gives the text. No entry
+ * point throws, retains a caller pointer past return, or falls back to the CPU:
+ * without a usable gfx950 device rg_create fails with RG_ENODEV.
+ *
+ * Vote codes (StateValue serde variant order, rabia-core/src/types.rs:286-294):
+ *   V0 = 0, V1 = 1, VQuestion = 2, 3 = absent voter / None / pending.
+ *
+ * Layout: bit-sliced planes of 32-bit words; slot s of a
+ * window is bit (s % 32) of word (s / 32). A "plane stride" is the distance in
+ * words between planes; it must be a multiple of 4 and >= ceil(n_slots/32)
+ * (rg_plane_stride() gives the minimum). Plane pointers must be 16-B aligned.
+ *   votes  = (4n + 1) planes: [0, 2n)   round-1 received votes, lane j at 2j (bit0), 2j+1 (bit1)
+ *                             [2n, 4n)  round-2 received votes, same order
+ *                             4n        WMVC own state bit (unused in REF mode)
+ *   output = 8 planes: 0-1 round-1 result code, 2-3 own round-2 vote code,
+ *            4-5 decision code, 6 committed (decision in {V0,V1}),
+ *            7 value (REF: decision == V1, i.e. batch applied; WMVC: next state).
+ * Replica lane j = position of the voter's NodeId in the sorted cluster membership.
+ */
+#ifndef RABIA_GPU_H
+#define RABIA_GPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RG_ABI_VERSION 1
+#define RG_MAX_REPLICAS 16
+#define RG_OUT_PLANES 8
+
+typedef struct rg_ctx rg_ctx;
+
+typedef enum rg_status {
+  RG_OK = 0,
+  RG_EINVAL = -1,  /* bad argument (maps to RabiaError::Internal)               */
+  RG_EHIP = -2,    /* HIP runtime error                                         */
+  RG_ENOMEM = -3,  /* device allocation failed                                  */
+  RG_ENODEV = -4,  /* no gfx950 device                                          */
+  RG_ESTATE = -5,  /* device-side protocol fault (e.g. look-back timeout)       */
+} rg_status;
+
+typedef enum rg_mode {
+  RG_MODE_REF = 0,  /* what engine.rs computes (majority quorum, biased StdRng draw) */
+  RG_MODE_WMVC = 1, /* Weak-MVC of the paper / weak_mvc.ivy (f+1 decide, common coin) */
+} rg_mode;
+
+typedef enum rg_trace_kind {
+  RG_TRACE_UNIFORM = 0, /* every code uniform over {V0,V1,VQ,absent}              */
+  RG_TRACE_AGREE90 = 1, /* per-slot majority value, each vote agrees w.p. 0.9       */
+  RG_TRACE_SPLIT = 2,   /* adversarial split round 1, all-VQ round 2                */
+} rg_trace_kind;
+
+/* Mirrors RabiaConfig (rabia-engine/src/config.rs:4-37) + ClusterConfig
+ * (rabia-core/src/network.rs:7-21) fields the path reads. */
+typedef struct rg_config {
+  uint32_t n_replicas;       /* ClusterConfig.all_nodes.len(), 1..16               */
+  uint32_t quorum;           /* 0 => n/2 + 1 (network.rs:15)                       */
+  uint32_t decide_threshold; /* WMVC f+1; 0 => (n-1)/2 + 1                         */
+  int32_t self_lane;         /* this node's lane, -1 = none                        */
+  uint32_t mode;             /* rg_mode                                            */
+  int32_t device;            /* HIP device ordinal                                 */
+  uint64_t seed;             /* RabiaConfig.randomization_seed (StdRng)            */
+  uint64_t coin_seed;        /* WMVC cluster-wide common-coin seed                 */
+  uint64_t epoch;            /* WMVC configuration epoch (coin stream)             */
+} rg_config;
+
+/* Per-step result (host or device memory). */
+typedef struct rg_step_result {
+  uint64_t n_slots;
+  uint64_t n_decided;          /* PhaseData.is_committed slots                      */
+  uint64_t n_v1;               /* decision V1 (batch applied via apply_commands)    */
+  uint64_t n_pending_r1;       /* round-1 result not yet available                  */
+  uint64_t n_draws;            /* REF StdRng draws / WMVC coin flips consumed       */
+  uint64_t last_committed_max; /* EngineState.last_committed_phase after the step   */
+  uint64_t first_undecided;    /* min slot id not committed (or slot_base+n_slots)  */
+  uint64_t rng_next;           /* REF draw index after the step                     */
+  uint64_t commit_watermark;   /* contiguous total-order watermark after the step   */
+  uint64_t flags;              /* nonzero = device-side fault (RG_ESTATE)           */
+} rg_step_result;
+
+/* Device-resident engine state carried across steps (EngineState mirror,
+ * rabia-engine/src/state.rs:13-29): next StdRng draw index,
+ * last_committed_phase, contiguous commit watermark (first slot id not yet
+ * known decided; PhaseIds start at 1). */
+typedef struct rg_engine_state {
+  uint64_t rng_next;
+  uint64_t last_committed;
+  uint64_t commit_watermark;
+  uint64_t steps;
+} rg_engine_state;
+
+int rg_abi_version(void);
+int rg_device_count(int* out);
+uint64_t rg_plane_stride(uint64_t n_slots);
+
+int rg_create(rg_ctx** out, const rg_config* cfg);
+int rg_destroy(rg_ctx* ctx);
+const char* rg_last_error(const rg_ctx* ctx);
+int rg_get_config(const rg_ctx* ctx, rg_config* out);
+
+/* Engine state (synchronous w.r.t. the context's stream). */
+int rg_set_state(rg_ctx* ctx, const rg_engine_state* st);
+int rg_get_state(rg_ctx* ctx, rg_engine_state* st);
+
+/* Phase step over one slot window [slot_base, slot_base + n_slots).
+ * `phase` is the WMVC phase number (>= 1; ignored in REF). `max_phase` is
+ * EngineState.current_phase for commit_phase's ordering check (state.rs:70-75);
+ * 0 disables it. Calls on one context must be stream-ordered.
+ *  _async: device pointers, enqueued on `stream`; result_dev may be NULL
+ *          (then fetch it with rg_last_result).
+ *  plain : host pointers; copies in, runs, copies out, synchronises. */
+int rg_phase_step_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev,
+                        uint64_t n_slots, uint64_t stride_words, uint64_t slot_base,
+                        uint64_t phase, uint64_t max_phase, rg_step_result* result_dev,
+                        void* stream);
+int rg_phase_step(rg_ctx* ctx, const uint32_t* votes_host, uint32_t* out_host,
+                  uint64_t n_slots, uint64_t stride_words, uint64_t slot_base,
+                  uint64_t phase, uint64_t max_phase, rg_step_result* result_host);
+int rg_last_result(rg_ctx* ctx, rg_step_result* out_host);
+
+/* Exchange stage: state bit = 1 iff some proposal digest is held by >= quorum
+ * replicas (weak_mvc.ivy:109-128). digests_dev = [n][digest_stride] u64 (0 = no
+ * proposal received), state_dev = one plane of stride_words. */
+int rg_digest_majority_async(rg_ctx* ctx, const uint64_t* digests_dev,
+                             uint64_t digest_stride, uint32_t* state_dev,
+                             uint64_t n_slots, void* stream);
+
+/* Common coin bits for slots [slot_base, slot_base+n_slots) at `phase` (>=1). */
+int rg_coin_async(rg_ctx* ctx, uint64_t slot_base, uint64_t n_slots, uint64_t phase,
+                  uint32_t* out_dev, void* stream);
+
+/* StdRng::seed_from_u64(seed).next_u64() draws first..first+count-1 (random access;
+ * the stream the REF mode consumes, engine.rs:461-604). */
+int rg_ref_draws_async(rg_ctx* ctx, uint64_t first, uint64_t count, uint64_t* out_dev,
+                       void* stream);
+
+/* Synthetic traces (seeded, counter-based) straight into device planes. */
+int rg_trace_generate_async(rg_ctx* ctx, int kind, uint64_t seed, uint64_t slot_base,
+                            uint64_t n_slots, uint64_t stride_words, uint32_t* votes_dev,
+                            void* stream);
+int rg_digest_trace_async(rg_ctx* ctx, uint64_t seed, uint64_t slot_base, uint64_t n_slots,
+                          uint64_t digest_stride, uint64_t* digests_dev, void* stream);
+
+int rg_stream_sync(rg_ctx* ctx, void* stream);
+
+/* Host-side packing helpers (no device work): slot-major codes [S][n] <-> planes. */
+int rg_pack_codes(const uint8_t* codes, uint32_t n, uint64_t n_slots, uint64_t stride_words,
+                  uint32_t* planes);
+int rg_unpack_planes(const uint32_t* planes, uint32_t n, uint64_t n_slots,
+                     uint64_t stride_words, uint8_t* codes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RABIA_GPU_H */

@@ -1,0 +1,118 @@
+"""ctypes binding of the C ABI in include/rabia_gpu.h (rabia_amd/lib/librabia_gpu.so).
+
+There is no fallback: if the library cannot be loaded, or no gfx950 device is
+present, the calls raise. torch (when importable) is imported BEFORE the library
+so both share one HIP runtime: torch's wheel bundles libamdhip64.so.7 and the
+loader then resolves our NEEDED entry to that already-loaded copy, which lets
+torch tensors / streams be handed to the library directly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+LIB_PATH = os.path.join(PKG, "lib", "librabia_gpu.so")
+HEADER = os.path.join(ROOT, "include", "rabia_gpu.h")
+
+u32, u64, i32, vp = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32, ctypes.c_void_p
+
+RG_OK, RG_EINVAL, RG_EHIP, RG_ENOMEM, RG_ENODEV, RG_ESTATE = 0, -1, -2, -3, -4, -5
+RG_MODE_REF, RG_MODE_WMVC = 0, 1
+RG_TRACE_UNIFORM, RG_TRACE_AGREE90, RG_TRACE_SPLIT = 0, 1, 2
+OUT_PLANES = 8
+
+
+class RgConfig(ctypes.Structure):
+    _fields_ = [("n_replicas", u32), ("quorum", u32), ("decide_threshold", u32),
+                ("self_lane", i32), ("mode", u32), ("device", i32), ("seed", u64),
+                ("coin_seed", u64), ("epoch", u64)]
+
+
+RESULT_FIELDS = ["n_slots", "n_decided", "n_v1", "n_pending_r1", "n_draws",
+                 "last_committed_max", "first_undecided", "rng_next", "commit_watermark", "flags"]
+
+
+class RgStepResult(ctypes.Structure):
+    _fields_ = [(f, u64) for f in RESULT_FIELDS]
+
+    def as_dict(self):
+        return {f: int(getattr(self, f)) for f in RESULT_FIELDS}
+
+
+class RgEngineState(ctypes.Structure):
+    _fields_ = [("rng_next", u64), ("last_committed", u64), ("commit_watermark", u64),
+                ("steps", u64)]
+
+
+_SIGS = {
+    "rg_abi_version": (ctypes.c_int, []),
+    "rg_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "rg_plane_stride": (u64, [u64]),
+    "rg_create": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.POINTER(RgConfig)]),
+    "rg_destroy": (ctypes.c_int, [vp]),
+    "rg_last_error": (ctypes.c_char_p, [vp]),
+    "rg_get_config": (ctypes.c_int, [vp, ctypes.POINTER(RgConfig)]),
+    "rg_set_state": (ctypes.c_int, [vp, ctypes.POINTER(RgEngineState)]),
+    "rg_get_state": (ctypes.c_int, [vp, ctypes.POINTER(RgEngineState)]),
+    "rg_phase_step_async": (ctypes.c_int, [vp, vp, vp, u64, u64, u64, u64, u64, vp, vp]),
+    "rg_phase_step": (ctypes.c_int, [vp, vp, vp, u64, u64, u64, u64, u64, ctypes.POINTER(RgStepResult)]),
+    "rg_last_result": (ctypes.c_int, [vp, ctypes.POINTER(RgStepResult)]),
+    "rg_digest_majority_async": (ctypes.c_int, [vp, vp, u64, vp, u64, vp]),
+    "rg_coin_async": (ctypes.c_int, [vp, u64, u64, u64, vp, vp]),
+    "rg_ref_draws_async": (ctypes.c_int, [vp, u64, u64, vp, vp]),
+    "rg_trace_generate_async": (ctypes.c_int, [vp, ctypes.c_int, u64, u64, u64, u64, vp, vp]),
+    "rg_digest_trace_async": (ctypes.c_int, [vp, u64, u64, u64, u64, vp, vp]),
+    "rg_stream_sync": (ctypes.c_int, [vp, vp]),
+    "rg_pack_codes": (ctypes.c_int, [vp, u32, u64, u64, vp]),
+    "rg_unpack_planes": (ctypes.c_int, [vp, u32, u64, u64, vp]),
+}
+
+_lib = None
+
+
+def header_symbols() -> list[str]:
+    """Every function declared in include/rabia_gpu.h."""
+    with open(HEADER) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"^\s*(?:[\w\s\*]+?)\b(rg_\w+)\s*\(", text, re.M)))
+
+
+def load():
+    """Load librabia_gpu.so (building it first if the sources are newer)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    try:  # share torch's HIP runtime when torch is present (see module doc)
+        import torch  # noqa: F401
+    except Exception:  # pragma: no cover - torch is optional for the binding itself
+        pass
+    if not os.path.exists(LIB_PATH):
+        from . import build as _build
+        _build.build()
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+class RabiaGpuError(RuntimeError):
+    """Error returned by the C ABI (maps onto the reference's RabiaError variants:
+    RG_EINVAL/RG_EHIP/RG_ENOMEM/RG_ENODEV -> Internal, RG_ESTATE -> Consensus)."""
+
+    def __init__(self, code: int, message: str):
+        super().__init__(f"[{code}] {message}")
+        self.code = code
+        self.message = message
+
+
+def check(rc: int, ctx=None):
+    if rc != RG_OK:
+        msg = load().rg_last_error(ctx)
+        raise RabiaGpuError(rc, msg.decode() if msg else "")
+    return rc

@@ -1,0 +1,84 @@
+"""Build the in-tree native library rabia_amd/lib/librabia_gpu.so for gfx950.
+
+Explicit hipcc (no JIT cache): the .so lives in-tree so it travels to the GPU box
+with the repo snapshot. `python -m rabia_amd.build [--resource-usage]`.
+"""
+from __future__ import annotations
+
+import os
+import re
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB_DIR = os.path.join(PKG, "lib")
+LIB = os.path.join(LIB_DIR, "librabia_gpu.so")
+SOURCES = [os.path.join(CSRC, "rabia_gpu.hip")]
+DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("rg_common.h", "rg_kernels.h")] + [
+    os.path.join(ROOT, "include", "rabia_gpu.h")]
+ARCH = "gfx950"
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if cand and (os.path.isabs(cand) and os.path.exists(cand) or not os.path.isabs(cand)):
+            return cand
+    return "hipcc"
+
+
+def needs_build() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    return any(os.path.getmtime(d) > t for d in DEPS)
+
+
+def build(force: bool = False, resource_usage: bool = False, verbose: bool = False) -> str:
+    if not force and not needs_build() and not resource_usage:
+        return LIB
+    os.makedirs(LIB_DIR, exist_ok=True)
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wall", "-Wno-unused-result", "-I", os.path.join(ROOT, "include"), "-o", LIB + ".tmp",
+           *SOURCES]
+    if resource_usage:
+        cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
+    proc = subprocess.run(cmd, capture_output=True, text=True)
+    if proc.returncode != 0:
+        sys.stderr.write(proc.stdout + proc.stderr)
+        raise RuntimeError(f"hipcc failed ({proc.returncode}): {' '.join(cmd)}")
+    os.replace(LIB + ".tmp", LIB)
+    if verbose and proc.stderr:
+        sys.stderr.write(proc.stderr)
+    if resource_usage:
+        print_resource_usage(proc.stderr)
+    return LIB
+
+
+def print_resource_usage(text: str) -> None:
+    rows, cur = [], None
+    for line in text.splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            cur = {"name": m.group(1)}
+            rows.append(cur)
+            continue
+        if cur is None:
+            continue
+        for key, pat in (("vgpr", r" VGPRs: (\d+)"), ("sgpr", r"TotalSGPRs: (\d+)"),
+                         ("scratch", r"ScratchSize \[bytes/lane\]: (\d+)"),
+                         ("occ", r"Occupancy \[waves/SIMD\]: (\d+)"), ("lds", r"LDS Size \[bytes/block\]: (\d+)")):
+            m = re.search(pat, line)
+            if m:
+                cur[key] = m.group(1)
+    names = subprocess.run(["c++filt"], input="\n".join(r["name"] for r in rows),
+                           capture_output=True, text=True).stdout.split("\n")
+    for r, n in zip(rows, names):
+        print(f"{n.split('(')[0][:48]:48s} vgpr={r.get('vgpr', '?'):>4} sgpr={r.get('sgpr', '?'):>4} "
+              f"scratch={r.get('scratch', '?'):>4} lds={r.get('lds', '?'):>5} occ={r.get('occ', '?')}")
+
+
+if __name__ == "__main__":
+    build(force=True, resource_usage="--resource-usage" in sys.argv, verbose="-v" in sys.argv)
+    print(LIB)

@@ -1,0 +1,432 @@
+// rabia_gpu.hip — C ABI (include/rabia_gpu.h) over the gfx950 kernels.
+//
+// The context is the GPU-side twin of the reference's per-engine state: the
+// StdRng position, last_committed_phase and the commit watermark live in device
+// memory and are advanced by the last workgroup of every step, so consecutive
+// steps on one stream never round-trip through the host.
+#include "rabia_gpu.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "rg_kernels.h"
+
+using namespace rg;
+
+struct rg_ctx {
+  rg_config cfg{};
+  uint32_t q = 0, fp1 = 0;
+  Key ref_key{}, coin_key{};
+  uint64_t coin_stream = 0;
+  hipStream_t stream = nullptr;
+  Record* rec = nullptr;
+  DevState* state = nullptr;
+  DevResult* result = nullptr;
+  unsigned long long* lookback = nullptr;
+  uint64_t lookback_cap = 0;
+  uint32_t seq = 0;
+  uint32_t* d_votes = nullptr;
+  uint32_t* d_out = nullptr;
+  DevResult* d_user_result = nullptr;
+  uint64_t stage_votes_words = 0, stage_out_words = 0;
+  std::string err;
+};
+
+namespace {
+
+thread_local std::string g_err;  // errors before a context exists
+
+int fail(rg_ctx* ctx, int code, const std::string& msg) {
+  if (ctx) ctx->err = msg;
+  else g_err = msg;
+  return code;
+}
+
+int hip_fail(rg_ctx* ctx, hipError_t e, const char* what) {
+  std::string m = std::string(what) + ": " + hipGetErrorString(e);
+  return fail(ctx, RG_EHIP, m);
+}
+
+#define RG_HIP(ctx, call)                                   \
+  do {                                                      \
+    hipError_t e_ = (call);                                 \
+    if (e_ != hipSuccess) return hip_fail(ctx, e_, #call);  \
+  } while (0)
+
+constexpr int wmax_for(int n) { return n <= 6 ? 4 : (n <= 10 ? 2 : 1); }
+
+using StepLaunch = void (*)(int, uint32_t, hipStream_t, const StepParams&);
+
+template <int N>
+struct Disp {
+  static constexpr int WM = wmax_for(N);
+  static void ref(int w, uint32_t grid, hipStream_t s, const StepParams& p) {
+    if (w == WM) hipLaunchKernelGGL((ref_step_kernel<N, WM>), dim3(grid), dim3(kBlock), 0, s, p);
+    else hipLaunchKernelGGL((ref_step_kernel<N, 1>), dim3(grid), dim3(kBlock), 0, s, p);
+  }
+  static void wmvc(int w, uint32_t grid, hipStream_t s, const StepParams& p) {
+    if (w == WM) hipLaunchKernelGGL((wmvc_step_kernel<N, WM>), dim3(grid), dim3(kBlock), 0, s, p);
+    else hipLaunchKernelGGL((wmvc_step_kernel<N, 1>), dim3(grid), dim3(kBlock), 0, s, p);
+  }
+  static void digest(uint32_t grid, hipStream_t s, const uint64_t* dg, uint64_t ds, uint32_t* out,
+                     uint64_t n, uint32_t q) {
+    hipLaunchKernelGGL((digest_kernel<N>), dim3(grid), dim3(kBlock), 0, s, dg, ds, out, n, q);
+  }
+};
+
+using DigestLaunch = void (*)(uint32_t, hipStream_t, const uint64_t*, uint64_t, uint32_t*, uint64_t,
+                              uint32_t);
+
+#define RG_TABLE(fn)                                                                          \
+  {nullptr, &Disp<1>::fn, &Disp<2>::fn, &Disp<3>::fn, &Disp<4>::fn, &Disp<5>::fn,             \
+   &Disp<6>::fn, &Disp<7>::fn, &Disp<8>::fn, &Disp<9>::fn, &Disp<10>::fn, &Disp<11>::fn,     \
+   &Disp<12>::fn, &Disp<13>::fn, &Disp<14>::fn, &Disp<15>::fn, &Disp<16>::fn}
+
+const StepLaunch kRefLaunch[17] = RG_TABLE(ref);
+const StepLaunch kWmvcLaunch[17] = RG_TABLE(wmvc);
+const DigestLaunch kDigestLaunch[17] = RG_TABLE(digest);
+
+hipStream_t pick_stream(rg_ctx* ctx, void* stream) {
+  return stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
+}
+
+Record fresh_record() {
+  Record r;
+  std::memset(&r, 0, sizeof r);
+  r.min_und.v = ~0ull;
+  return r;
+}
+
+// Lookback granules for the largest legal call (n_slots < 2^32 at W = 1).
+constexpr uint64_t kLookbackCap = ((1ull << 32) / 32 + kBlock - 1) / kBlock + 1;
+
+}  // namespace
+
+extern "C" {
+
+int rg_abi_version(void) { return RG_ABI_VERSION; }
+
+int rg_device_count(int* out) {
+  if (!out) return fail(nullptr, RG_EINVAL, "rg_device_count: null out");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    *out = 0;
+    return hip_fail(nullptr, e, "hipGetDeviceCount");
+  }
+  *out = n;
+  return RG_OK;
+}
+
+uint64_t rg_plane_stride(uint64_t n_slots) { return ((n_slots + 127) / 128) * 4; }
+
+const char* rg_last_error(const rg_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
+
+int rg_create(rg_ctx** out, const rg_config* cfg) {
+  if (!out || !cfg) return fail(nullptr, RG_EINVAL, "rg_create: null argument");
+  *out = nullptr;
+  const uint32_t n = cfg->n_replicas;
+  if (n < 1 || n > RG_MAX_REPLICAS) return fail(nullptr, RG_EINVAL, "rg_create: n_replicas must be 1..16");
+  const uint32_t q = cfg->quorum ? cfg->quorum : n / 2 + 1;
+  const uint32_t fp1 = cfg->decide_threshold ? cfg->decide_threshold : (n - 1) / 2 + 1;
+  if (q < 1 || q > n) return fail(nullptr, RG_EINVAL, "rg_create: quorum must be 1..n");
+  if (fp1 < 1 || fp1 > n) return fail(nullptr, RG_EINVAL, "rg_create: decide_threshold must be 1..n");
+  if (cfg->mode != RG_MODE_REF && cfg->mode != RG_MODE_WMVC)
+    return fail(nullptr, RG_EINVAL, "rg_create: unknown mode");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return fail(nullptr, RG_ENODEV, "rg_create: no HIP device (the evaluator has no CPU fallback)");
+  if (cfg->device < 0 || cfg->device >= ndev) return fail(nullptr, RG_EINVAL, "rg_create: bad device ordinal");
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, cfg->device) != hipSuccess)
+    return fail(nullptr, RG_ENODEV, "rg_create: hipGetDeviceProperties failed");
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(nullptr, RG_ENODEV, std::string("rg_create: device is ") + prop.gcnArchName +
+                                        ", this build targets gfx950 only");
+  rg_ctx* ctx = new (std::nothrow) rg_ctx();
+  if (!ctx) return fail(nullptr, RG_ENOMEM, "rg_create: host allocation failed");
+  ctx->cfg = *cfg;
+  ctx->cfg.quorum = q;
+  ctx->cfg.decide_threshold = fp1;
+  ctx->q = q;
+  ctx->fp1 = fp1;
+  seed_from_u64(cfg->seed, ctx->ref_key.k);
+  seed_from_u64(cfg->coin_seed, ctx->coin_key.k);
+  ctx->coin_stream = cfg->epoch | kCoinStreamBit;
+  auto bail = [&](hipError_t e, const char* what) {
+    int rc = hip_fail(nullptr, e, what);
+    rg_destroy(ctx);
+    return rc;
+  };
+  hipError_t e;
+  if ((e = hipSetDevice(cfg->device)) != hipSuccess) return bail(e, "hipSetDevice");
+  if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess)
+    return bail(e, "hipStreamCreate");
+  if ((e = hipMalloc(&ctx->rec, 2 * sizeof(Record))) != hipSuccess) return bail(e, "hipMalloc(rec)");
+  if ((e = hipMalloc(&ctx->state, sizeof(DevState))) != hipSuccess) return bail(e, "hipMalloc(state)");
+  if ((e = hipMalloc(&ctx->result, sizeof(DevResult))) != hipSuccess) return bail(e, "hipMalloc(result)");
+  ctx->lookback_cap = kLookbackCap;
+  if ((e = hipMalloc(&ctx->lookback, ctx->lookback_cap * 8)) != hipSuccess) return bail(e, "hipMalloc(lookback)");
+  Record recs[2] = {fresh_record(), fresh_record()};
+  DevState st{0, 0, 1, 0};  // PhaseIds start at 1 (state.rs:59-63)
+  DevResult res;
+  std::memset(&res, 0, sizeof res);
+  if ((e = hipMemcpy(ctx->rec, recs, sizeof recs, hipMemcpyHostToDevice)) != hipSuccess) return bail(e, "init rec");
+  if ((e = hipMemcpy(ctx->state, &st, sizeof st, hipMemcpyHostToDevice)) != hipSuccess) return bail(e, "init state");
+  if ((e = hipMemcpy(ctx->result, &res, sizeof res, hipMemcpyHostToDevice)) != hipSuccess) return bail(e, "init result");
+  if ((e = hipMemset(ctx->lookback, 0, ctx->lookback_cap * 8)) != hipSuccess) return bail(e, "init lookback");
+  if ((e = hipDeviceSynchronize()) != hipSuccess) return bail(e, "init sync");
+  *out = ctx;
+  return RG_OK;
+}
+
+int rg_destroy(rg_ctx* ctx) {
+  if (!ctx) return RG_OK;
+  (void)hipSetDevice(ctx->cfg.device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  (void)hipFree(ctx->rec);
+  (void)hipFree(ctx->state);
+  (void)hipFree(ctx->result);
+  (void)hipFree(ctx->lookback);
+  (void)hipFree(ctx->d_votes);
+  (void)hipFree(ctx->d_out);
+  (void)hipFree(ctx->d_user_result);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return RG_OK;
+}
+
+int rg_get_config(const rg_ctx* ctx, rg_config* out) {
+  if (!ctx || !out) return fail(nullptr, RG_EINVAL, "rg_get_config: null argument");
+  *out = ctx->cfg;
+  return RG_OK;
+}
+
+int rg_set_state(rg_ctx* ctx, const rg_engine_state* st) {
+  if (!ctx || !st) return fail(ctx, RG_EINVAL, "rg_set_state: null argument");
+  RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
+  RG_HIP(ctx, hipDeviceSynchronize());
+  DevState s{st->rng_next, st->last_committed, st->commit_watermark, st->steps};
+  RG_HIP(ctx, hipMemcpy(ctx->state, &s, sizeof s, hipMemcpyHostToDevice));
+  return RG_OK;
+}
+
+int rg_get_state(rg_ctx* ctx, rg_engine_state* st) {
+  if (!ctx || !st) return fail(ctx, RG_EINVAL, "rg_get_state: null argument");
+  RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
+  RG_HIP(ctx, hipDeviceSynchronize());
+  DevState s;
+  RG_HIP(ctx, hipMemcpy(&s, ctx->state, sizeof s, hipMemcpyDeviceToHost));
+  st->rng_next = s.rng_next;
+  st->last_committed = s.last_committed;
+  st->commit_watermark = s.commit_watermark;
+  st->steps = s.steps;
+  return RG_OK;
+}
+
+int rg_phase_step_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, uint64_t n_slots,
+                        uint64_t stride_words, uint64_t slot_base, uint64_t phase, uint64_t max_phase,
+                        rg_step_result* result_dev, void* stream) {
+  if (!ctx) return fail(nullptr, RG_EINVAL, "rg_phase_step: null context");
+  if (n_slots == 0) return fail(ctx, RG_EINVAL, "rg_phase_step: n_slots must be > 0");
+  if (n_slots >= (1ull << 32)) return fail(ctx, RG_EINVAL, "rg_phase_step: n_slots must be < 2^32 per call");
+  if (!votes_dev || !out_dev) return fail(ctx, RG_EINVAL, "rg_phase_step: null plane pointer");
+  if ((reinterpret_cast<uintptr_t>(votes_dev) | reinterpret_cast<uintptr_t>(out_dev)) & 15u)
+    return fail(ctx, RG_EINVAL, "rg_phase_step: plane pointers must be 16-byte aligned");
+  if (stride_words % 4 || stride_words < (n_slots + 31) / 32)
+    return fail(ctx, RG_EINVAL, "rg_phase_step: stride_words must be a multiple of 4 and >= ceil(n_slots/32)");
+  const bool wmvc = ctx->cfg.mode == RG_MODE_WMVC;
+  if (wmvc && (phase < 1 || phase > (1ull << 24)))
+    return fail(ctx, RG_EINVAL, "rg_phase_step: WMVC phase must be 1..2^24");
+  if (wmvc && slot_base + n_slots > (1ull << 49))
+    return fail(ctx, RG_EINVAL, "rg_phase_step: WMVC slot ids must be < 2^49 (coin counter layout)");
+  RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
+  const int n = (int)ctx->cfg.n_replicas;
+  const uint64_t n_words = (n_slots + 31) / 32;
+  const int wm = wmax_for(n);
+  const int w = (n_words / ((uint64_t)kBlock * wm) >= 512) ? wm : 1;
+  const uint64_t n_tiles = (n_words + (uint64_t)kBlock * w - 1) / ((uint64_t)kBlock * w);
+  if (n_tiles > ctx->lookback_cap) return fail(ctx, RG_EINVAL, "rg_phase_step: window too large");
+  if (++ctx->seq >= (1u << 31)) {  // look-back tags wrap: start a fresh epoch
+    RG_HIP(ctx, hipDeviceSynchronize());
+    RG_HIP(ctx, hipMemset(ctx->lookback, 0, ctx->lookback_cap * 8));
+    // keep the record parity: seq restarts at 1 or 2 with the same low bit
+    ctx->seq = 2 - (ctx->seq & 1u);
+  }
+  StepParams p;
+  p.votes = votes_dev;
+  p.out = out_dev;
+  p.lookback = ctx->lookback;
+  p.rec = ctx->rec;
+  p.state = ctx->state;
+  p.result = ctx->result;
+  p.result_user = reinterpret_cast<DevResult*>(result_dev);
+  p.stride = stride_words;
+  p.n_slots = n_slots;
+  p.n_words = n_words;
+  p.slot_base = slot_base;
+  p.max_phase = max_phase;
+  p.phase = phase;
+  p.coin_stream = ctx->coin_stream;
+  p.key = wmvc ? ctx->coin_key : ctx->ref_key;
+  p.q = ctx->q;
+  p.fp1 = ctx->fp1;
+  p.self_lane = ctx->cfg.self_lane;
+  p.seq = ctx->seq;
+  p.n_tiles = (uint32_t)n_tiles;
+  hipStream_t s = pick_stream(ctx, stream);
+  (wmvc ? kWmvcLaunch : kRefLaunch)[n](w, (uint32_t)n_tiles, s, p);
+  RG_HIP(ctx, hipGetLastError());
+  return RG_OK;
+}
+
+int rg_last_result(rg_ctx* ctx, rg_step_result* out_host) {
+  if (!ctx || !out_host) return fail(ctx, RG_EINVAL, "rg_last_result: null argument");
+  RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
+  RG_HIP(ctx, hipDeviceSynchronize());
+  RG_HIP(ctx, hipMemcpy(out_host, ctx->result, sizeof(DevResult), hipMemcpyDeviceToHost));
+  if (out_host->flags) return fail(ctx, RG_ESTATE, "device-side protocol fault (look-back timeout)");
+  return RG_OK;
+}
+
+int rg_phase_step(rg_ctx* ctx, const uint32_t* votes_host, uint32_t* out_host, uint64_t n_slots,
+                  uint64_t stride_words, uint64_t slot_base, uint64_t phase, uint64_t max_phase,
+                  rg_step_result* result_host) {
+  if (!ctx || !votes_host || !out_host) return fail(ctx, RG_EINVAL, "rg_phase_step: null argument");
+  if (stride_words % 4 || stride_words < (n_slots + 31) / 32)
+    return fail(ctx, RG_EINVAL, "rg_phase_step: stride_words must be a multiple of 4 and >= ceil(n_slots/32)");
+  RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
+  const uint64_t n = ctx->cfg.n_replicas;
+  const uint64_t vw = (4 * n + 1) * stride_words, ow = (uint64_t)kOutPlanes * stride_words;
+  if (vw > ctx->stage_votes_words) {
+    RG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    (void)hipFree(ctx->d_votes);
+    ctx->d_votes = nullptr;
+    RG_HIP(ctx, hipMalloc(&ctx->d_votes, vw * 4));
+    ctx->stage_votes_words = vw;
+  }
+  if (ow > ctx->stage_out_words) {
+    RG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    (void)hipFree(ctx->d_out);
+    ctx->d_out = nullptr;
+    RG_HIP(ctx, hipMalloc(&ctx->d_out, ow * 4));
+    ctx->stage_out_words = ow;
+  }
+  RG_HIP(ctx, hipMemcpyAsync(ctx->d_votes, votes_host, vw * 4, hipMemcpyHostToDevice, ctx->stream));
+  int rc = rg_phase_step_async(ctx, ctx->d_votes, ctx->d_out, n_slots, stride_words, slot_base, phase,
+                               max_phase, nullptr, ctx->stream);
+  if (rc) return rc;
+  RG_HIP(ctx, hipMemcpyAsync(out_host, ctx->d_out, ow * 4, hipMemcpyDeviceToHost, ctx->stream));
+  rg_step_result tmp;
+  RG_HIP(ctx, hipMemcpyAsync(&tmp, ctx->result, sizeof tmp, hipMemcpyDeviceToHost, ctx->stream));
+  RG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (result_host) *result_host = tmp;
+  if (tmp.flags) return fail(ctx, RG_ESTATE, "device-side protocol fault (look-back timeout)");
+  return RG_OK;
+}
+
+int rg_digest_majority_async(rg_ctx* ctx, const uint64_t* digests_dev, uint64_t digest_stride,
+                             uint32_t* state_dev, uint64_t n_slots, void* stream) {
+  if (!ctx || !digests_dev || !state_dev) return fail(ctx, RG_EINVAL, "rg_digest_majority: null argument");
+  if (n_slots == 0 || digest_stride < n_slots) return fail(ctx, RG_EINVAL, "rg_digest_majority: bad sizes");
+  if (reinterpret_cast<uintptr_t>(state_dev) & 15u)
+    return fail(ctx, RG_EINVAL, "rg_digest_majority: state plane must be 16-byte aligned");
+  RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
+  const uint64_t waves = (n_slots + 127) / 128;
+  const uint64_t grid = (waves + kWaves - 1) / kWaves;
+  kDigestLaunch[ctx->cfg.n_replicas]((uint32_t)grid, pick_stream(ctx, stream), digests_dev, digest_stride,
+                                     state_dev, n_slots, ctx->q);
+  RG_HIP(ctx, hipGetLastError());
+  return RG_OK;
+}
+
+int rg_coin_async(rg_ctx* ctx, uint64_t slot_base, uint64_t n_slots, uint64_t phase, uint32_t* out_dev,
+                  void* stream) {
+  if (!ctx || !out_dev || n_slots == 0) return fail(ctx, RG_EINVAL, "rg_coin: bad argument");
+  if (phase < 1 || phase > (1ull << 24)) return fail(ctx, RG_EINVAL, "rg_coin: phase must be 1..2^24");
+  RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
+  const uint64_t n_words = (n_slots + 31) / 32;
+  hipLaunchKernelGGL(coin_kernel, dim3((uint32_t)((n_words + 255) / 256)), dim3(256), 0,
+                     pick_stream(ctx, stream), ctx->coin_key, ctx->coin_stream, phase, slot_base, n_slots,
+                     out_dev);
+  RG_HIP(ctx, hipGetLastError());
+  return RG_OK;
+}
+
+int rg_ref_draws_async(rg_ctx* ctx, uint64_t first, uint64_t count, uint64_t* out_dev, void* stream) {
+  if (!ctx || !out_dev || count == 0) return fail(ctx, RG_EINVAL, "rg_ref_draws: bad argument");
+  RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
+  hipLaunchKernelGGL(draws_kernel, dim3((uint32_t)((count + 255) / 256)), dim3(256), 0,
+                     pick_stream(ctx, stream), ctx->ref_key, first, count,
+                     reinterpret_cast<unsigned long long*>(out_dev));
+  RG_HIP(ctx, hipGetLastError());
+  return RG_OK;
+}
+
+int rg_trace_generate_async(rg_ctx* ctx, int kind, uint64_t seed, uint64_t slot_base, uint64_t n_slots,
+                            uint64_t stride_words, uint32_t* votes_dev, void* stream) {
+  if (!ctx || !votes_dev || n_slots == 0) return fail(ctx, RG_EINVAL, "rg_trace_generate: bad argument");
+  if (kind < 0 || kind > 2) return fail(ctx, RG_EINVAL, "rg_trace_generate: unknown kind");
+  if (stride_words < (n_slots + 31) / 32) return fail(ctx, RG_EINVAL, "rg_trace_generate: stride too small");
+  RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
+  const uint64_t n_words = (n_slots + 31) / 32;
+  hipLaunchKernelGGL(trace_kernel, dim3((uint32_t)((n_words + 127) / 128)), dim3(128), 0,
+                     pick_stream(ctx, stream), kind, (int)ctx->cfg.n_replicas, seed, slot_base, n_slots,
+                     stride_words, votes_dev);
+  RG_HIP(ctx, hipGetLastError());
+  return RG_OK;
+}
+
+int rg_digest_trace_async(rg_ctx* ctx, uint64_t seed, uint64_t slot_base, uint64_t n_slots,
+                          uint64_t digest_stride, uint64_t* digests_dev, void* stream) {
+  if (!ctx || !digests_dev || n_slots == 0 || digest_stride < n_slots)
+    return fail(ctx, RG_EINVAL, "rg_digest_trace: bad argument");
+  RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
+  hipLaunchKernelGGL(digest_trace_kernel, dim3((uint32_t)((n_slots + 255) / 256)), dim3(256), 0,
+                     pick_stream(ctx, stream), (int)ctx->cfg.n_replicas, seed, slot_base, n_slots,
+                     digest_stride, reinterpret_cast<unsigned long long*>(digests_dev));
+  RG_HIP(ctx, hipGetLastError());
+  return RG_OK;
+}
+
+int rg_stream_sync(rg_ctx* ctx, void* stream) {
+  if (!ctx) return fail(nullptr, RG_EINVAL, "rg_stream_sync: null context");
+  RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
+  RG_HIP(ctx, hipStreamSynchronize(pick_stream(ctx, stream)));
+  return RG_OK;
+}
+
+int rg_pack_codes(const uint8_t* codes, uint32_t n, uint64_t n_slots, uint64_t stride, uint32_t* planes) {
+  if (!codes || !planes || n < 1 || n > RG_MAX_REPLICAS || stride < (n_slots + 31) / 32)
+    return fail(nullptr, RG_EINVAL, "rg_pack_codes: bad argument");
+  std::memset(planes, 0, sizeof(uint32_t) * stride * 2 * n);
+  for (uint64_t s = 0; s < n_slots; s++) {
+    const uint8_t* c = codes + s * n;
+    const uint32_t bit = 1u << (s & 31);
+    for (uint32_t j = 0; j < n; j++) {
+      if (c[j] & 1u) planes[(uint64_t)(2 * j) * stride + s / 32] |= bit;
+      if (c[j] & 2u) planes[(uint64_t)(2 * j + 1) * stride + s / 32] |= bit;
+    }
+  }
+  return RG_OK;
+}
+
+int rg_unpack_planes(const uint32_t* planes, uint32_t n, uint64_t n_slots, uint64_t stride, uint8_t* codes) {
+  if (!codes || !planes || n < 1 || n > RG_MAX_REPLICAS || stride < (n_slots + 31) / 32)
+    return fail(nullptr, RG_EINVAL, "rg_unpack_planes: bad argument");
+  for (uint64_t s = 0; s < n_slots; s++) {
+    const uint32_t sh = (uint32_t)(s & 31);
+    for (uint32_t j = 0; j < n; j++) {
+      const uint32_t lo = (planes[(uint64_t)(2 * j) * stride + s / 32] >> sh) & 1u;
+      const uint32_t hi = (planes[(uint64_t)(2 * j + 1) * stride + s / 32] >> sh) & 1u;
+      codes[s * n + j] = (uint8_t)(lo | (hi << 1));
+    }
+  }
+  return RG_OK;
+}
+
+}  // extern "C"

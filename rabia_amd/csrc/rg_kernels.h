@@ -1,0 +1,736 @@
+// rg_kernels.h — gfx950 kernels of the batched Rabia phase evaluator.
+//
+// Layout: bit-sliced planes (one bit per slot, 32 slots per word), so one VALU
+// op evaluates a boolean over 32 slots. Each thread owns W consecutive words
+// (W*32 slots) of every plane and loads them as one 16/8/4-B vector per plane:
+// coalesced, read exactly once, no LDS staging needed (no reuse exists).
+// Counts over the n replica lanes are bit-sliced ripple counters.
+//
+// REF mode needs, per VQ slot, the index of its StdRng draw = number of VQ slots
+// before it in ascending slot order (engine.rs:567-611 consumes the engine's one
+// RNG stream). That is an exclusive prefix sum across the launch, done in the
+// same pass by a decoupled look-back over dynamically ticketed tiles.
+#pragma once
+
+#include "rg_common.h"
+
+namespace rg {
+
+struct StepParams {
+  const uint32_t* votes;          // [4N+1][stride]
+  uint32_t* out;                  // [8][stride]
+  unsigned long long* lookback;   // [n_tiles] {tag:32 | value:32} granules
+  Record* rec;                    // ring of 2
+  DevState* state;
+  DevResult* result;              // ctx-internal, always written
+  DevResult* result_user;         // optional copy
+  uint64_t stride;
+  uint64_t n_slots;
+  uint64_t n_words;
+  uint64_t slot_base;
+  uint64_t max_phase;
+  uint64_t phase;
+  uint64_t coin_stream;
+  Key key;                        // REF: StdRng key; WMVC: coin key
+  uint32_t q, fp1;
+  int32_t self_lane;
+  uint32_t seq;
+  uint32_t n_tiles;
+};
+
+constexpr int ctr_bits(int n) { return n < 2 ? 1 : n < 4 ? 2 : n < 8 ? 3 : n < 16 ? 4 : 5; }
+
+// ---- bit-sliced counters --------------------------------------------------
+template <int B>
+struct Ctr {
+  uint32_t b[B];
+};
+
+template <int B>
+RG_HD void ctr_zero(Ctr<B>& c) {
+#pragma unroll
+  for (int i = 0; i < B; i++) c.b[i] = 0;
+}
+
+template <int B>
+RG_HD void ctr_add(Ctr<B>& c, uint32_t m) {
+#pragma unroll
+  for (int i = 0; i < B; i++) {
+    uint32_t t = c.b[i] & m;
+    c.b[i] ^= m;
+    m = t;
+  }
+}
+
+// Per-slot mask of (count >= q) for a wave-uniform q < 2^B.
+template <int B>
+RG_HD uint32_t ctr_ge(const Ctr<B>& c, uint32_t q) {
+  uint32_t gt = 0, eq = ~0u;
+#pragma unroll
+  for (int i = B - 1; i >= 0; i--) {
+    uint32_t qb = ((q >> i) & 1u) ? ~0u : 0u;
+    gt |= eq & c.b[i] & ~qb;
+    eq &= ~(c.b[i] ^ qb);
+  }
+  return gt | eq;
+}
+
+template <int B>
+RG_HD uint32_t ctr_nz(const Ctr<B>& c) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int i = 0; i < B; i++) r |= c.b[i];
+  return r;
+}
+
+template <int B>
+RG_HD uint32_t ctr_at(const Ctr<B>& c, int bit) {
+  uint32_t v = 0;
+#pragma unroll
+  for (int i = 0; i < B; i++) v |= ((c.b[i] >> bit) & 1u) << i;
+  return v;
+}
+
+// ---- vector plane access ----------------------------------------------------
+template <int W>
+__device__ __forceinline__ void load_words(const uint32_t* p, uint32_t (&v)[W]) {
+  if constexpr (W == 4) {
+    uint4 x = *reinterpret_cast<const uint4*>(p);
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+  } else if constexpr (W == 2) {
+    uint2 x = *reinterpret_cast<const uint2*>(p);
+    v[0] = x.x; v[1] = x.y;
+  } else {
+    v[0] = *p;
+  }
+}
+
+template <int W>
+__device__ __forceinline__ void store_words(uint32_t* p, const uint32_t (&v)[W]) {
+  if constexpr (W == 4) {
+    *reinterpret_cast<uint4*>(p) = make_uint4(v[0], v[1], v[2], v[3]);
+  } else if constexpr (W == 2) {
+    *reinterpret_cast<uint2*>(p) = make_uint2(v[0], v[1]);
+  } else {
+    *p = v[0];
+  }
+}
+
+__device__ __forceinline__ uint32_t valid_mask(uint64_t w, uint64_t n_words, uint64_t n_slots) {
+  if (w >= n_words) return 0u;
+  if (w == n_words - 1 && (n_slots & 31u)) return (1u << (n_slots & 31u)) - 1u;
+  return ~0u;
+}
+
+// Mask of local bits b with slot_base + 32w + b <= max_phase (max_phase 0 = no limit).
+__device__ __forceinline__ uint32_t phase_limit_mask(uint64_t slot_base, uint64_t w,
+                                                     uint64_t max_phase) {
+  if (max_phase == 0) return ~0u;
+  uint64_t first = slot_base + 32 * w;
+  if (first > max_phase) return 0u;
+  uint64_t lim = max_phase - first;
+  return lim >= 31 ? ~0u : ((2u << lim) - 1u);
+}
+
+// ---- wave / block reductions -------------------------------------------------
+__device__ __forceinline__ unsigned long long wave_sum64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ unsigned long long wave_max64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    unsigned long long t = __shfl_xor(v, o, 64);
+    v = t > v ? t : v;
+  }
+  return v;
+}
+__device__ __forceinline__ unsigned long long wave_min64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    unsigned long long t = __shfl_xor(v, o, 64);
+    v = t < v ? t : v;
+  }
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+__device__ __forceinline__ unsigned long long atomic_load_agent(unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void atomic_store_agent(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---- decoupled look-back (run by all 64 lanes of wave 0) ----------------------
+// Granule = {tag:32 | value:32}, tag = seq<<1 | inclusive, written by ONE 8-B
+// agent-scope store and read by agent-scope loads (MI355X_MICROARCH.md,
+// visibility: "R2" granules need no separate flag or fence). seq changes every
+// launch, so the array is never re-zeroed. Tickets are handed out in dispatch
+// order, so every predecessor is already resident: the spin terminates. It is
+// still bounded; a timeout raises Record.error and the step reports RG_ESTATE.
+__device__ __forceinline__ uint32_t lookback_exclusive(unsigned long long* status, uint32_t tile,
+                                                       uint32_t seq, uint32_t agg, int lane,
+                                                       unsigned long long* err) {
+  const uint32_t tag_agg = seq << 1, tag_inc = (seq << 1) | 1u;
+  if (tile == 0) {
+    if (lane == 0) atomic_store_agent(status, ((unsigned long long)tag_inc << 32) | agg);
+    return 0;
+  }
+  if (lane == 0) atomic_store_agent(status + tile, ((unsigned long long)tag_agg << 32) | agg);
+  uint32_t excl = 0;
+  int64_t pos = (int64_t)tile - 1;
+  uint32_t spins = 0;
+  for (;;) {
+    const int64_t pidx = pos - lane;
+    unsigned long long g = pidx >= 0 ? atomic_load_agent(status + pidx)
+                                     : ((unsigned long long)tag_inc << 32);
+    const uint32_t tag = (uint32_t)(g >> 32);
+    const bool ready = (tag >> 1) == seq;
+    const bool incl = ready && (tag & 1u);
+    const unsigned long long incl_mask = __ballot(incl);
+    const unsigned long long notready = __ballot(!ready);
+    const int first = incl_mask ? __builtin_ctzll(incl_mask) : 64;
+    const unsigned long long need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);
+    if (notready & need) {
+      if (++spins > (1u << 22)) {  // ~seconds: a protocol fault, not a wait
+        if (lane == 0) atomicOr(err, 1ull);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    const uint32_t v = (lane <= first) ? (uint32_t)g : 0u;
+    excl += (uint32_t)wave_sum64(v);
+    if (first < 64) break;
+    pos -= 64;
+  }
+  if (lane == 0)
+    atomic_store_agent(status + tile, ((unsigned long long)tag_inc << 32) | (agg + excl));
+  return excl;
+}
+
+// ---- per-block statistics -> record; last arrival finalises the step ----------
+struct BlockStats {
+  unsigned long long dec_v1, pend_vq, max_v1p1, min_und;
+};
+
+template <bool IS_REF>
+__device__ __forceinline__ void finish_block(const StepParams& p, Record* rec, BlockStats st,
+                                             int tid, int lane, int wave) {
+  __shared__ unsigned long long s_red[kWaves][4];
+  st.dec_v1 = wave_sum64(st.dec_v1);
+  st.pend_vq = wave_sum64(st.pend_vq);
+  st.max_v1p1 = wave_max64(st.max_v1p1);
+  st.min_und = wave_min64(st.min_und);
+  if (lane == 0) {
+    s_red[wave][0] = st.dec_v1; s_red[wave][1] = st.pend_vq;
+    s_red[wave][2] = st.max_v1p1; s_red[wave][3] = st.min_und;
+  }
+  __syncthreads();
+  if (tid != 0) return;
+  unsigned long long a = 0, b = 0, mx = 0, mn = ~0ull;
+#pragma unroll
+  for (int w = 0; w < kWaves; w++) {
+    a += s_red[w][0]; b += s_red[w][1];
+    mx = s_red[w][2] > mx ? s_red[w][2] : mx;
+    mn = s_red[w][3] < mn ? s_red[w][3] : mn;
+  }
+  if (a) atomicAdd(&rec->dec_v1.v, a);
+  if (b) atomicAdd(&rec->pend_vq.v, b);
+  if (mx) atomicMax(&rec->max_v1p1.v, mx);
+  if (mn != ~0ull) atomicMin(&rec->min_und.v, mn);
+  // The statistics atomics must be performed before our arrival is counted.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const unsigned long long old = atomicAdd(&rec->done.v, 1ull);
+  if (old != (unsigned long long)p.n_tiles - 1) return;
+
+  // Last arrival: every other block's atomics are complete. Read totals with
+  // atomic RMWs (performed where the adds were), update the engine state.
+  const unsigned long long dv = atomicAdd(&rec->dec_v1.v, 0ull);
+  const unsigned long long pv = atomicAdd(&rec->pend_vq.v, 0ull);
+  const unsigned long long mxv = atomicAdd(&rec->max_v1p1.v, 0ull);
+  const unsigned long long mnv = atomicAdd(&rec->min_und.v, 0ull);
+  const unsigned long long err = atomicAdd(&rec->error.v, 0ull);
+  DevState s = *p.state;
+  DevResult r;
+  r.n_slots = p.n_slots;
+  r.n_decided = dv & 0xffffffffull;
+  r.n_v1 = dv >> 32;
+  r.n_pending_r1 = pv & 0xffffffffull;
+  r.n_draws = pv >> 32;
+  unsigned long long lc = s.last_committed;          // commit_phase: monotonic max,
+  if (mxv && mxv - 1 > lc) lc = mxv - 1;             // state.rs:77-99
+  const unsigned long long end = p.slot_base + p.n_slots;
+  const unsigned long long fu = mnv < end ? mnv : end;
+  unsigned long long wm = s.commit_watermark;
+  if (p.slot_base <= wm && wm < fu) wm = fu;
+  r.last_committed_max = lc;
+  r.first_undecided = fu;
+  r.rng_next = IS_REF ? s.rng_next + r.n_draws : s.rng_next;
+  r.commit_watermark = wm;
+  r.flags = err;
+  s.rng_next = r.rng_next;
+  s.last_committed = lc;
+  s.commit_watermark = wm;
+  s.steps += 1;
+  *p.state = s;
+  *p.result = r;
+  if (p.result_user) *p.result_user = r;
+  Record* nxt = p.rec + ((p.seq + 1) & 1u);
+  atomic_store_agent(&nxt->ticket.v, 0ull);
+  atomic_store_agent(&nxt->done.v, 0ull);
+  atomic_store_agent(&nxt->dec_v1.v, 0ull);
+  atomic_store_agent(&nxt->pend_vq.v, 0ull);
+  atomic_store_agent(&nxt->max_v1p1.v, 0ull);
+  atomic_store_agent(&nxt->min_und.v, ~0ull);
+  atomic_store_agent(&nxt->error.v, 0ull);
+}
+
+template <int W>
+__device__ __forceinline__ void thread_extrema(const uint32_t (&committed)[W],
+                                               const uint32_t (&v1)[W], const uint32_t (&vm)[W],
+                                               uint64_t w0, const StepParams& p,
+                                               unsigned long long& max_v1p1,
+                                               unsigned long long& min_und) {
+  max_v1p1 = 0;
+  min_und = ~0ull;
+#pragma unroll
+  for (int i = W - 1; i >= 0; i--) {
+    const uint32_t m = v1[i] & phase_limit_mask(p.slot_base, w0 + i, p.max_phase);
+    if (m && !max_v1p1) max_v1p1 = p.slot_base + 32 * (w0 + i) + (31 - __builtin_clz(m)) + 1;
+  }
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    const uint32_t m = ~committed[i] & vm[i];
+    if (m && min_und == ~0ull) min_und = p.slot_base + 32 * (w0 + i) + __builtin_ctz(m);
+  }
+}
+
+// ============================================================================
+// REF phase step: engine.rs:483-682 on the final vote sets of every slot.
+// ============================================================================
+template <int N, int W>
+__global__ __launch_bounds__(kBlock) void ref_step_kernel(StepParams p) {
+  constexpr int B = ctr_bits(N);
+  __shared__ uint32_t s_ticket;
+  __shared__ uint32_t s_wave[kWaves];
+  __shared__ uint32_t s_excl;
+  Record* rec = p.rec + (p.seq & 1u);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) s_ticket = (uint32_t)atomicAdd(&rec->ticket.v, 1ull);
+  __syncthreads();
+  const uint32_t tile = s_ticket;
+  const uint64_t w0 = ((uint64_t)tile * kBlock + tid) * W;
+  const bool active = w0 < p.n_words;
+
+  // Issue every plane load up front (R2 stays in flight across the look-back).
+  uint32_t r1lo[N][W], r1hi[N][W], r2lo[N][W], r2hi[N][W];
+  if (active) {
+    const uint32_t* base = p.votes + w0;
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      load_words<W>(base + (uint64_t)(2 * j) * p.stride, r1lo[j]);
+      load_words<W>(base + (uint64_t)(2 * j + 1) * p.stride, r1hi[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      load_words<W>(base + (uint64_t)(2 * N + 2 * j) * p.stride, r2lo[j]);
+      load_words<W>(base + (uint64_t)(2 * N + 2 * j + 1) * p.stride, r2hi[j]);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < N; j++)
+#pragma unroll
+      for (int i = 0; i < W; i++) r1lo[j][i] = r1hi[j][i] = r2lo[j][i] = r2hi[j][i] = ~0u;
+  }
+  uint32_t vm[W];
+#pragma unroll
+  for (int i = 0; i < W; i++) vm[i] = valid_mask(w0 + i, p.n_words, p.n_slots);
+
+  // ---- round 1: count_votes + |votes| >= quorum fallback (engine.rs:495-505)
+  uint32_t r1v1[W], r1vq[W], pend[W];
+  Ctr<B> c0s[W], c1s[W];
+  uint32_t vq_count = 0;
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    Ctr<B> cp;
+    ctr_zero(c0s[i]); ctr_zero(c1s[i]); ctr_zero(cp);
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      const uint32_t lo = r1lo[j][i], hi = r1hi[j][i];
+      ctr_add(c0s[i], ~lo & ~hi);
+      ctr_add(c1s[i], lo & ~hi);
+      ctr_add(cp, ~(lo & hi));
+    }
+    const uint32_t g0 = ctr_ge(c0s[i], p.q), g1 = ctr_ge(c1s[i], p.q), gp = ctr_ge(cp, p.q);
+    const uint32_t v0 = g0 & vm[i];
+    r1v1[i] = ~g0 & g1 & vm[i];
+    r1vq[i] = ~g0 & ~g1 & gp & vm[i];  // cq >= q implies present >= q
+    pend[i] = ~(v0 | r1v1[i] | r1vq[i]) & vm[i];
+    vq_count += __builtin_popcount(r1vq[i]);
+  }
+
+  // ---- exclusive prefix of VQ slots: block scan + cross-tile look-back
+  const uint32_t incl = wave_incl_scan32(vq_count, lane);
+  if (lane == 63) s_wave[wave] = incl;
+  __syncthreads();
+  uint32_t wave_off = 0, tile_total = 0;
+#pragma unroll
+  for (int w = 0; w < kWaves; w++) {
+    wave_off += (w < wave) ? s_wave[w] : 0u;
+    tile_total += s_wave[w];
+  }
+  if (wave == 0) {
+    const uint32_t e = lookback_exclusive(p.lookback, tile, p.seq, tile_total, lane, &rec->error.v);
+    if (lane == 0) s_excl = e;
+  }
+  __syncthreads();
+  unsigned long long k = p.state->rng_next + s_excl + wave_off + incl - vq_count;
+
+  // ---- own round-2 vote (engine.rs:523-537; VQ -> one StdRng draw, 567-611)
+  uint32_t own_lo[W];
+  unsigned long long cur_blk = ~0ull;
+  uint32_t blk[16];
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    uint32_t m = r1vq[i], dv1 = 0;
+    while (m) {
+      const int b = __builtin_ctz(m);
+      m &= m - 1;
+      const unsigned long long bi = k >> 3;
+      if (bi != cur_blk) {
+        chacha_block<12>(p.key, bi, 0, blk);
+        cur_blk = bi;
+      }
+      const uint32_t ws = (uint32_t)(k & 7u) * 2u;
+      const unsigned long long u =
+          (unsigned long long)select16(blk, ws) | ((unsigned long long)select16(blk, ws + 1) << 32);
+      const uint32_t c0 = ctr_at(c0s[i], b), c1 = ctr_at(c1s[i], b);
+      const bool v1 = c1 > c0 ? (u < kP90) : (c1 < c0 ? (u >= kP90) : (u < kP80));
+      dv1 |= (uint32_t)v1 << b;
+      k++;
+    }
+    own_lo[i] = r1v1[i] | dv1;
+  }
+
+  // ---- own vote joins round2_votes (engine.rs:540-542); decision (613-628)
+#pragma unroll
+  for (int j = 0; j < N; j++) {
+    if (j == p.self_lane) {
+#pragma unroll
+      for (int i = 0; i < W; i++) {
+        r2lo[j][i] = (r2lo[j][i] & pend[i]) | (own_lo[i] & ~pend[i]);
+        r2hi[j][i] &= pend[i];
+      }
+    }
+  }
+  uint32_t o[kOutPlanes][W];
+  unsigned long long n_dec = 0, n_v1 = 0, n_pend = 0;
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    Ctr<B> c0, c1, cq;
+    ctr_zero(c0); ctr_zero(c1); ctr_zero(cq);
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      const uint32_t lo = r2lo[j][i], hi = r2hi[j][i];
+      ctr_add(c0, ~lo & ~hi);
+      ctr_add(c1, lo & ~hi);
+      ctr_add(cq, ~lo & hi);
+    }
+    const uint32_t d0 = ctr_ge(c0, p.q);
+    const uint32_t d1 = ~d0 & ctr_ge(c1, p.q);
+    const uint32_t dq = ~d0 & ~d1 & ctr_ge(cq, p.q);
+    const uint32_t dn = ~(d0 | d1 | dq);
+    o[0][i] = (r1v1[i] | pend[i]) & vm[i];
+    o[1][i] = (r1vq[i] | pend[i]) & vm[i];
+    o[2][i] = (own_lo[i] | pend[i]) & vm[i];
+    o[3][i] = pend[i];
+    o[4][i] = (d1 | dn) & vm[i];
+    o[5][i] = (dq | dn) & vm[i];
+    o[6][i] = (d0 | d1) & vm[i];   // set_decision: committed iff not VQuestion
+    o[7][i] = d1 & vm[i];          // V1: apply_batch + commit_phase
+    n_dec += __builtin_popcount(o[6][i]);
+    n_v1 += __builtin_popcount(o[7][i]);
+    n_pend += __builtin_popcount(pend[i]);
+  }
+  if (active) {
+    uint32_t* ob = p.out + w0;
+#pragma unroll
+    for (int pl = 0; pl < kOutPlanes; pl++) store_words<W>(ob + (uint64_t)pl * p.stride, o[pl]);
+  }
+  BlockStats st;
+  st.dec_v1 = n_dec | (n_v1 << 32);
+  st.pend_vq = n_pend | ((unsigned long long)vq_count << 32);
+  thread_extrema<W>(o[6], o[7], vm, w0, p, st.max_v1p1, st.min_und);
+  finish_block<true>(p, rec, st, tid, lane, wave);
+}
+
+// ============================================================================
+// WMVC phase step, one replica's view (weak_mvc.ivy:129-191).
+// ============================================================================
+__device__ __forceinline__ uint32_t coin_word(const Key& key, uint64_t stream, uint64_t phase,
+                                              uint64_t g0, unsigned long long& cur,
+                                              uint32_t (&blk)[16]) {
+  uint32_t words[2];
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const uint64_t id = g0 + 32u * h;
+    const unsigned long long bi = ((phase - 1) << 40) | (id >> 9);
+    if (bi != cur) {
+      chacha_block<12>(key, bi, stream, blk);
+      cur = bi;
+    }
+    words[h] = select16(blk, (uint32_t)(id >> 5) & 15u);
+    if (h == 0 && (g0 & 31u) == 0) return words[0];
+  }
+  const uint32_t sh = (uint32_t)(g0 & 31u);
+  return (words[0] >> sh) | (words[1] << (32u - sh));
+}
+
+template <int N, int W>
+__global__ __launch_bounds__(kBlock) void wmvc_step_kernel(StepParams p) {
+  constexpr int B = ctr_bits(N);
+  Record* rec = p.rec + (p.seq & 1u);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint64_t w0 = ((uint64_t)blockIdx.x * kBlock + tid) * W;
+  const bool active = w0 < p.n_words;
+  uint32_t r1lo[N][W], r1hi[N][W], r2lo[N][W], r2hi[N][W], st_in[W];
+  if (active) {
+    const uint32_t* base = p.votes + w0;
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      load_words<W>(base + (uint64_t)(2 * j) * p.stride, r1lo[j]);
+      load_words<W>(base + (uint64_t)(2 * j + 1) * p.stride, r1hi[j]);
+      load_words<W>(base + (uint64_t)(2 * N + 2 * j) * p.stride, r2lo[j]);
+      load_words<W>(base + (uint64_t)(2 * N + 2 * j + 1) * p.stride, r2hi[j]);
+    }
+    load_words<W>(base + (uint64_t)(4 * N) * p.stride, st_in);
+  } else {
+#pragma unroll
+    for (int i = 0; i < W; i++) {
+      st_in[i] = 0;
+#pragma unroll
+      for (int j = 0; j < N; j++) r1lo[j][i] = r1hi[j][i] = r2lo[j][i] = r2hi[j][i] = ~0u;
+    }
+  }
+  uint32_t o[kOutPlanes][W];
+  unsigned long long n_dec = 0, n_v1 = 0, n_pend = 0, n_coin = 0;
+  unsigned long long cur_blk = ~0ull;
+  uint32_t blk[16];
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    const uint32_t vm = valid_mask(w0 + i, p.n_words, p.n_slots);
+    // round 1 (phase_rnd1): >= q messages, vote v if #v >= q else ?
+    Ctr<B> c0, c1, cp;
+    ctr_zero(c0); ctr_zero(c1); ctr_zero(cp);
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      const uint32_t lo = r1lo[j][i], hi = r1hi[j][i];
+      ctr_add(c0, ~lo & ~hi);
+      ctr_add(c1, lo & ~hi);
+      ctr_add(cp, ~(lo & hi));
+    }
+    const uint32_t gp = ctr_ge(cp, p.q), g0 = ctr_ge(c0, p.q), g1 = ctr_ge(c1, p.q);
+    const uint32_t pend1 = ~gp;
+    const uint32_t v1 = gp & ~g0 & g1, vq = gp & ~g0 & ~g1;
+    // round 2 (phase_rnd2): own vote at self lane
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      if (j == p.self_lane) {
+        r2lo[j][i] = (r2lo[j][i] & pend1) | (v1 & ~pend1);
+        r2hi[j][i] = (r2hi[j][i] & pend1) | (vq & ~pend1);
+      }
+    }
+    Ctr<B> e0, e1, ep;
+    ctr_zero(e0); ctr_zero(e1); ctr_zero(ep);
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      const uint32_t lo = r2lo[j][i], hi = r2hi[j][i];
+      ctr_add(e0, ~lo & ~hi);
+      ctr_add(e1, lo & ~hi);
+      ctr_add(ep, ~(lo & hi));
+    }
+    const uint32_t live = ~pend1 & ctr_ge(ep, p.q);
+    const uint32_t f0 = ctr_ge(e0, p.fp1), f1 = ctr_ge(e1, p.fp1);
+    const uint32_t nz0 = ctr_nz(e0), nz1 = ctr_nz(e1);
+    const uint32_t d0 = live & f0, d1 = live & ~f0 & f1;
+    const uint32_t open = live & ~f0 & ~f1;
+    const uint32_t a1 = open & ~nz0 & nz1;
+    const uint32_t cm = open & ~nz0 & ~nz1 & vm;  // all round-2 votes '?': common coin
+    uint32_t coin = 0;
+    if (cm) coin = coin_word(p.key, p.coin_stream, p.phase, p.slot_base + 32 * (w0 + i), cur_blk, blk);
+    const uint32_t next = d1 | a1 | (cm & coin) | (~live & st_in[i]);
+    o[0][i] = (v1 | pend1) & vm;
+    o[1][i] = (vq | pend1) & vm;
+    o[2][i] = o[0][i];
+    o[3][i] = o[1][i];
+    o[4][i] = ~d0 & vm;
+    o[5][i] = ~(d0 | d1) & vm;
+    o[6][i] = (d0 | d1) & vm;
+    o[7][i] = next & vm;
+    n_dec += __builtin_popcount(o[6][i]);
+    n_v1 += __builtin_popcount(d1 & vm);
+    n_pend += __builtin_popcount(pend1 & vm);
+    n_coin += __builtin_popcount(cm);
+  }
+  if (active) {
+    uint32_t* ob = p.out + w0;
+#pragma unroll
+    for (int pl = 0; pl < kOutPlanes; pl++) store_words<W>(ob + (uint64_t)pl * p.stride, o[pl]);
+  }
+  uint32_t vm_all[W], dv1[W];
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    vm_all[i] = valid_mask(w0 + i, p.n_words, p.n_slots);
+    dv1[i] = o[6][i] & o[4][i];  // committed with decision code lo bit set = V1
+  }
+  BlockStats st;
+  st.dec_v1 = n_dec | (n_v1 << 32);
+  st.pend_vq = n_pend | (n_coin << 32);
+  thread_extrema<W>(o[6], dv1, vm_all, w0, p, st.max_v1p1, st.min_und);
+  finish_block<false>(p, rec, st, tid, lane, wave);
+}
+
+// ============================================================================
+// Exchange stage: digest majority (weak_mvc.ivy:109-128). One wave = 128 slots:
+// lane l owns slots l and 64+l, so each u64 load instruction is 512 contiguous B.
+// ============================================================================
+template <int N>
+__global__ __launch_bounds__(kBlock) void digest_kernel(const uint64_t* __restrict__ dg,
+                                                        uint64_t dstride, uint32_t* out,
+                                                        uint64_t n_slots, uint32_t q) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t s0 = ((uint64_t)blockIdx.x * kWaves + wave) * 128;
+  if (s0 >= n_slots) return;
+  unsigned long long masks[2];
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const uint64_t s = s0 + 64 * h + lane;
+    const bool valid = s < n_slots;
+    uint64_t d[N];
+#pragma unroll
+    for (int j = 0; j < N; j++) d[j] = valid ? dg[(uint64_t)j * dstride + s] : 0ull;
+    bool st = false;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      uint32_t c = 0;
+#pragma unroll
+      for (int j = 0; j < N; j++) c += (d[j] == d[i]) ? 1u : 0u;
+      st |= (d[i] != 0) && (c >= q);
+    }
+    masks[h] = __ballot(st && valid);
+  }
+  if (lane == 0) {
+    *reinterpret_cast<uint4*>(out + s0 / 32) =
+        make_uint4((uint32_t)masks[0], (uint32_t)(masks[0] >> 32), (uint32_t)masks[1],
+                   (uint32_t)(masks[1] >> 32));
+  }
+}
+
+__global__ void coin_kernel(Key key, uint64_t stream, uint64_t phase, uint64_t slot_base,
+                            uint64_t n_slots, uint32_t* out) {
+  const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t n_words = (n_slots + 31) / 32;
+  if (w >= n_words) return;
+  unsigned long long cur = ~0ull;
+  uint32_t blk[16];
+  out[w] = coin_word(key, stream, phase, slot_base + 32 * w, cur, blk) & valid_mask(w, n_words, n_slots);
+}
+
+__global__ void draws_kernel(Key key, uint64_t first, uint64_t count, unsigned long long* out) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= count) return;
+  const uint64_t k = first + t;
+  uint32_t blk[16];
+  chacha_block<12>(key, k >> 3, 0, blk);
+  const uint32_t ws = (uint32_t)(k & 7u) * 2u;
+  out[t] = (unsigned long long)select16(blk, ws) | ((unsigned long long)select16(blk, ws + 1) << 32);
+}
+
+// Synthetic traces, one thread per 32-slot word (restated in oracle/rabia_oracle.c:or_trace).
+__global__ void trace_kernel(int kind, int n, uint64_t seed, uint64_t slot_base, uint64_t n_slots,
+                             uint64_t stride, uint32_t* planes) {
+  const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t n_words = (n_slots + 31) / 32;
+  if (w >= n_words) return;
+  const uint64_t kmaj = trace_key(seed, 0), kst = trace_key(seed, 1), krot = trace_key(seed, 2);
+  uint32_t lo[2][kMaxReplicas], hi[2][kMaxReplicas];
+#pragma unroll
+  for (int r = 0; r < 2; r++)
+#pragma unroll
+    for (int j = 0; j < kMaxReplicas; j++) lo[r][j] = hi[r][j] = 0;
+  uint32_t stw = 0;
+  const int nv0 = (n - 1) / 2;
+  const uint32_t vm = valid_mask(w, n_words, n_slots);
+  for (int b = 0; b < 32; b++) {
+    if (!((vm >> b) & 1u)) break;
+    const uint64_t id = slot_base + 32 * w + b;
+    const uint32_t m = (uint32_t)(mix64(kmaj + id) & 1u);
+    stw |= (uint32_t)(mix64(kst + id) & 1u) << b;
+    const uint32_t rot = (uint32_t)(mix64(krot + id) % (uint64_t)n);
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+#pragma unroll
+      for (int j = 0; j < kMaxReplicas; j++) {
+        if (j >= n) continue;
+        const uint64_t u = mix64(trace_key(seed, 16u + (uint32_t)r * 16u + (uint32_t)j) + id);
+        uint32_t c;
+        if (kind == 0) {
+          c = (uint32_t)(u & 3u);
+        } else if (kind == 1) {
+          if (u < kTraceP90) {
+            c = m;
+          } else {
+            const uint32_t pick = (uint32_t)u % 3u;
+            c = pick == 0 ? 1u - m : (pick == 1 ? kCodeVQ : kCodeNone);
+          }
+        } else {
+          if (r) {
+            c = kCodeVQ;
+          } else {
+            const int l = (int)((j + rot) % (uint32_t)n);
+            c = l < nv0 ? kCodeV0 : (l < n - 1 ? kCodeV1 : kCodeVQ);
+          }
+        }
+        lo[r][j] |= (c & 1u) << b;
+        hi[r][j] |= ((c >> 1) & 1u) << b;
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 2; r++)
+#pragma unroll
+    for (int j = 0; j < kMaxReplicas; j++) {
+      if (j >= n) continue;
+      planes[(uint64_t)(2 * n * r + 2 * j) * stride + w] = lo[r][j];
+      planes[(uint64_t)(2 * n * r + 2 * j + 1) * stride + w] = hi[r][j];
+    }
+  planes[(uint64_t)(4 * n) * stride + w] = stw;
+}
+
+__global__ void digest_trace_kernel(int n, uint64_t seed, uint64_t slot_base, uint64_t n_slots,
+                                    uint64_t dstride, unsigned long long* dg) {
+  const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_slots) return;
+  const uint64_t id = slot_base + s;
+  const uint64_t maj = mix64(trace_key(seed, 3) + id) | 1u;
+  for (int j = 0; j < n; j++) {
+    const uint64_t u = mix64(trace_key(seed, 64u + (uint32_t)j) + id);
+    uint64_t d;
+    if (u < kTraceP90) d = maj;
+    else if ((u & 15u) == 0) d = 0;
+    else d = mix64(u) | 1u;
+    dg[(uint64_t)j * dstride + s] = d;
+  }
+}
+
+}  // namespace rg

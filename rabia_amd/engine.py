@@ -1,0 +1,248 @@
+"""Host-side mirror of the reference's phase-evaluation interface, over the C ABI.
+
+Names follow rabia-rs so a maintainer finds the same concepts:
+  StateValue (rabia-core/src/types.rs:286-294), NodeId::from(u32) (types.rs:49-75),
+  ClusterConfig.quorum_size (rabia-core/src/network.rs:13-21),
+  PhaseData::add_round{1,2}_vote / has_round{1,2}_majority (rabia-core/src/messages.rs:169-183)
+  -> PhaseWindow (a window of PhaseData as SoA bit planes),
+  EngineState.last_committed_phase / commit_phase (rabia-engine/src/state.rs:55-103)
+  -> PhaseEvaluator.state.
+
+Every evaluation runs on the GPU through librabia_gpu.so; there is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from enum import IntEnum
+
+import numpy as np
+
+from . import _native as N
+
+
+class StateValue(IntEnum):
+    V0 = 0
+    V1 = 1
+    VQuestion = 2
+
+
+ABSENT = 3  # voter not in the HashMap / None / pending
+
+
+def node_id_from_u32(value: int) -> bytes:
+    """NodeId::from(u32): the 4 big-endian bytes repeated 4 times (types.rs:49-75)."""
+    return bytes([(value >> 24) & 255, (value >> 16) & 255, (value >> 8) & 255, value & 255] * 4)
+
+
+@dataclass
+class ClusterConfig:
+    """rabia-core/src/network.rs:7-21. Lane j = j-th NodeId in sorted order."""
+    node_id: bytes
+    all_nodes: list
+
+    @property
+    def quorum_size(self) -> int:
+        return len(self.all_nodes) // 2 + 1
+
+    def lane_of(self, node: bytes) -> int:
+        return sorted(self.all_nodes).index(node)
+
+    def total_nodes(self) -> int:
+        return len(self.all_nodes)
+
+
+def plane_stride(n_slots: int) -> int:
+    return ((n_slots + 127) // 128) * 4
+
+
+def unpack_bits(plane: np.ndarray, n_slots: int) -> np.ndarray:
+    """One bit plane (uint32 words) -> uint8 per slot."""
+    return np.unpackbits(np.ascontiguousarray(plane).view(np.uint8), bitorder="little")[:n_slots]
+
+
+def decode_outputs(out: np.ndarray, n_slots: int) -> dict:
+    """8 output planes -> per-slot arrays (codes: V0=0, V1=1, VQ=2, none=3)."""
+    b = [unpack_bits(out[i], n_slots) for i in range(N.OUT_PLANES)]
+    return {
+        "r1": b[0] | (b[1] << 1),
+        "r2own": b[2] | (b[3] << 1),
+        "dec": b[4] | (b[5] << 1),
+        "committed": b[6],
+        "value": b[7],
+    }
+
+
+class PhaseWindow:
+    """A window of `n_slots` consecutive phases' vote sets, packed as the device
+    layout: (4n+1) planes of uint32 words (R1 lanes, R2 lanes, own state)."""
+
+    def __init__(self, n_replicas: int, n_slots: int, slot_base: int = 1):
+        self.n = int(n_replicas)
+        self.n_slots = int(n_slots)
+        self.slot_base = int(slot_base)
+        self.stride = plane_stride(n_slots)
+        self.planes = np.zeros((4 * self.n + 1, self.stride), np.uint32)
+        # every voter starts absent (empty HashMaps, messages.rs:152-166)
+        self.planes[: 4 * self.n] = 0xFFFFFFFF
+        self._mask_tail()
+
+    def _mask_tail(self):
+        if self.n_slots % 32:
+            w = self.n_slots // 32
+            self.planes[:, w] &= np.uint32((1 << (self.n_slots % 32)) - 1)
+            self.planes[:, w + 1:] = 0
+        else:
+            self.planes[:, self.n_slots // 32:] = 0
+
+    @classmethod
+    def from_codes(cls, r1: np.ndarray, r2: np.ndarray, state=None, slot_base: int = 1):
+        r1 = np.ascontiguousarray(r1, np.uint8)
+        r2 = np.ascontiguousarray(r2, np.uint8)
+        S, n = r1.shape
+        w = cls(n, S, slot_base)
+        lib = N.load()
+        N.check(lib.rg_pack_codes(r1.ctypes.data, n, S, w.stride, w.planes[: 2 * n].ctypes.data))
+        N.check(lib.rg_pack_codes(r2.ctypes.data, n, S, w.stride, w.planes[2 * n: 4 * n].ctypes.data))
+        w.planes[4 * n] = 0
+        if state is not None:
+            st = np.ascontiguousarray(state, np.uint8) & 1
+            packed = np.packbits(st, bitorder="little")
+            buf = np.zeros(w.stride * 4, np.uint8)
+            buf[: packed.size] = packed
+            w.planes[4 * n] = buf.view(np.uint32)
+        return w
+
+    def _set(self, base_plane: int, phase_id: int, lane: int, vote: int):
+        s = phase_id - self.slot_base
+        if not (0 <= s < self.n_slots) or not (0 <= lane < self.n):
+            raise IndexError(f"phase {phase_id} / lane {lane} outside window")
+        wd, bit = s // 32, np.uint32(1 << (s % 32))
+        for b in range(2):
+            p = self.planes[base_plane + 2 * lane + b]
+            if (int(vote) >> b) & 1:
+                p[wd] |= bit
+            else:
+                p[wd] &= ~bit
+
+    def add_round1_vote(self, phase_id: int, lane: int, vote: StateValue):
+        """PhaseData::add_round1_vote (messages.rs:169-171): last write wins."""
+        self._set(0, phase_id, lane, int(vote))
+
+    def add_round2_vote(self, phase_id: int, lane: int, vote: StateValue):
+        """PhaseData::add_round2_vote (messages.rs:173-175)."""
+        self._set(2 * self.n, phase_id, lane, int(vote))
+
+    def set_state(self, phase_id: int, bit: int):
+        s = phase_id - self.slot_base
+        wd, m = s // 32, np.uint32(1 << (s % 32))
+        if bit:
+            self.planes[4 * self.n, wd] |= m
+        else:
+            self.planes[4 * self.n, wd] &= ~m
+
+
+class PhaseEvaluator:
+    """Owns one rg_ctx (device state: StdRng position, last_committed_phase,
+    commit watermark). Not thread-safe, like the single &mut engine task
+    (engine.rs:184)."""
+
+    def __init__(self, n_replicas: int, *, quorum: int = 0, decide_threshold: int = 0,
+                 self_lane: int = -1, mode: str = "ref", seed: int = 0, coin_seed=None,
+                 epoch: int = 0, device: int = 0):
+        self.lib = N.load()
+        self.n = int(n_replicas)
+        self.mode = mode
+        cfg = N.RgConfig(n_replicas=self.n, quorum=quorum, decide_threshold=decide_threshold,
+                         self_lane=self_lane, mode=N.RG_MODE_WMVC if mode == "wmvc" else N.RG_MODE_REF,
+                         device=device, seed=seed & (2 ** 64 - 1),
+                         coin_seed=(seed if coin_seed is None else coin_seed) & (2 ** 64 - 1),
+                         epoch=epoch)
+        ctx = ctypes.c_void_p()
+        N.check(self.lib.rg_create(ctypes.byref(ctx), ctypes.byref(cfg)))
+        self.ctx = ctx
+        got = N.RgConfig()
+        N.check(self.lib.rg_get_config(self.ctx, ctypes.byref(got)), self.ctx)
+        self.quorum = got.quorum
+        self.decide_threshold = got.decide_threshold
+
+    @classmethod
+    def from_configs(cls, cluster: ClusterConfig, seed: int, mode: str = "ref", **kw):
+        return cls(cluster.total_nodes(), quorum=cluster.quorum_size,
+                   self_lane=cluster.lane_of(cluster.node_id), mode=mode, seed=seed, **kw)
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.rg_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- engine state -----------------------------------------------------
+    def get_state(self) -> dict:
+        st = N.RgEngineState()
+        N.check(self.lib.rg_get_state(self.ctx, ctypes.byref(st)), self.ctx)
+        return {"rng_next": st.rng_next, "last_committed": st.last_committed,
+                "commit_watermark": st.commit_watermark, "steps": st.steps}
+
+    def set_state(self, rng_next=0, last_committed=0, commit_watermark=1, steps=0):
+        st = N.RgEngineState(rng_next, last_committed, commit_watermark, steps)
+        N.check(self.lib.rg_set_state(self.ctx, ctypes.byref(st)), self.ctx)
+
+    def last_result(self) -> dict:
+        r = N.RgStepResult()
+        N.check(self.lib.rg_last_result(self.ctx, ctypes.byref(r)), self.ctx)
+        return r.as_dict()
+
+    # -- steps ---------------------------------------------------------------
+    def phase_step_host(self, window: PhaseWindow, phase: int = 1, max_phase: int = 0):
+        """Synchronous step over host planes: returns (out planes, result dict)."""
+        if window.n != self.n:
+            raise ValueError("window replica count does not match the evaluator")
+        out = np.zeros((N.OUT_PLANES, window.stride), np.uint32)
+        votes = np.ascontiguousarray(window.planes)
+        r = N.RgStepResult()
+        N.check(self.lib.rg_phase_step(self.ctx, votes.ctypes.data, out.ctypes.data, window.n_slots,
+                                       window.stride, window.slot_base, phase, max_phase,
+                                       ctypes.byref(r)), self.ctx)
+        return out, r.as_dict()
+
+    def phase_step_async(self, votes_ptr: int, out_ptr: int, n_slots: int, stride: int,
+                         slot_base: int = 1, phase: int = 1, max_phase: int = 0,
+                         result_ptr: int = 0, stream: int = 0):
+        """Device-pointer step enqueued on `stream` (a hipStream_t handle, 0 = own)."""
+        N.check(self.lib.rg_phase_step_async(self.ctx, votes_ptr, out_ptr, n_slots, stride, slot_base,
+                                             phase, max_phase, result_ptr or None, stream or None),
+                self.ctx)
+
+    def digest_majority_async(self, digests_ptr, digest_stride, state_ptr, n_slots, stream=0):
+        N.check(self.lib.rg_digest_majority_async(self.ctx, digests_ptr, digest_stride, state_ptr,
+                                                  n_slots, stream or None), self.ctx)
+
+    def coin_async(self, slot_base, n_slots, phase, out_ptr, stream=0):
+        N.check(self.lib.rg_coin_async(self.ctx, slot_base, n_slots, phase, out_ptr, stream or None),
+                self.ctx)
+
+    def ref_draws_async(self, first, count, out_ptr, stream=0):
+        N.check(self.lib.rg_ref_draws_async(self.ctx, first, count, out_ptr, stream or None), self.ctx)
+
+    def trace_generate_async(self, kind, seed, slot_base, n_slots, stride, votes_ptr, stream=0):
+        N.check(self.lib.rg_trace_generate_async(self.ctx, kind, seed, slot_base, n_slots, stride,
+                                                 votes_ptr, stream or None), self.ctx)
+
+    def digest_trace_async(self, seed, slot_base, n_slots, digest_stride, digests_ptr, stream=0):
+        N.check(self.lib.rg_digest_trace_async(self.ctx, seed, slot_base, n_slots, digest_stride,
+                                               digests_ptr, stream or None), self.ctx)
+
+    def sync(self, stream=0):
+        N.check(self.lib.rg_stream_sync(self.ctx, stream or None), self.ctx)

@@ -1,0 +1,182 @@
+"""ctypes loader for the CPU oracle (oracle/rabia_oracle.c). Test infrastructure:
+used by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg only."""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "build", "librabia_oracle.so")
+
+u8p = ctypes.POINTER(ctypes.c_uint8)
+u32p = ctypes.POINTER(ctypes.c_uint32)
+u64p = ctypes.POINTER(ctypes.c_uint64)
+i, u64 = ctypes.c_int, ctypes.c_uint64
+
+RES_KEYS = ["n_slots", "n_decided", "n_v1", "n_pending_r1", "n_draws",
+            "last_committed_max", "first_undecided", "rng_next", "commit_watermark"]
+
+
+class OrResult(ctypes.Structure):
+    _fields_ = [(k, u64) for k in RES_KEYS]
+
+    def as_dict(self):
+        return {k: int(getattr(self, k)) for k in RES_KEYS}
+
+
+_lib = None
+
+
+def build():
+    src = [os.path.join(ORACLE_DIR, f) for f in ("rabia_oracle.c", "rabia_oracle.h")]
+    if not os.path.exists(ORACLE_SO) or any(os.path.getmtime(s) > os.path.getmtime(ORACLE_SO) for s in src):
+        subprocess.run(["make", "-C", ORACLE_DIR, "build/librabia_oracle.so"], check=True,
+                       capture_output=True)
+    return ORACLE_SO
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    build()
+    lib = ctypes.CDLL(ORACLE_SO)
+    lib.or_count_votes.argtypes = [u8p, i, i]
+    lib.or_ref_round1.argtypes = [u8p, i, i]
+    lib.or_seed_from_u64.argtypes = [u64, u32p]
+    lib.or_chacha_block.argtypes = [u32p, u64, u64, i, u32p]
+    lib.or_ref_draw.argtypes = [u32p, u64]
+    lib.or_ref_draw.restype = u64
+    lib.or_coin.argtypes = [u32p, u64, u64, u64]
+    lib.or_ref_step.argtypes = [i, i, i, u64, u64, u64, u64, u64, u64, u8p, u8p, u64,
+                                u8p, u8p, u8p, u8p, u8p, ctypes.POINTER(OrResult)]
+    lib.or_wmvc_step.argtypes = [i, i, i, i, u64, u64, u64, u64, u64, u64, u8p, u8p, u8p, u64,
+                                 u8p, u8p, u8p, u8p, u8p, ctypes.POINTER(OrResult)]
+    lib.or_digest_majority.argtypes = [i, i, u64p, u64, u8p]
+    lib.or_coin_range.argtypes = [u64, u64, u64, u64, u64, u8p]
+    lib.or_ref_structured.argtypes = [i, i, i, u64, u64, u64, u8p, u8p, u64, u8p,
+                                      ctypes.POINTER(OrResult)]
+    lib.or_trace.argtypes = [i, i, u64, u64, u64, u8p, u8p, u8p]
+    lib.or_digest_trace.argtypes = [i, u64, u64, u64, u64p]
+    lib.or_pack_planes.argtypes = [u8p, i, u64, u64, u32p]
+    lib.or_unpack_planes.argtypes = [u32p, i, u64, u64, u8p]
+    _lib = lib
+    return lib
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+def trace(kind, n, seed, slot_base, S):
+    lib = load()
+    r1 = np.zeros((S, n), np.uint8)
+    r2 = np.zeros((S, n), np.uint8)
+    st = np.zeros(S, np.uint8)
+    lib.or_trace(kind, n, seed, slot_base, S, _p(r1, u8p), _p(r2, u8p), _p(st, u8p))
+    return r1, r2, st
+
+
+def ref_step(n, q, self_lane, seed, rng_base, slot_base, r1, r2, max_phase=0, lc_in=0, wm_in=1):
+    lib = load()
+    S = r1.shape[0]
+    outs = [np.zeros(S, np.uint8) for _ in range(5)]
+    res = OrResult()
+    rc = lib.or_ref_step(n, q, self_lane, seed, rng_base, slot_base, max_phase, lc_in, wm_in,
+                         _p(np.ascontiguousarray(r1), u8p), _p(np.ascontiguousarray(r2), u8p), S,
+                         *[_p(o, u8p) for o in outs], ctypes.byref(res))
+    assert rc == 0
+    return dict(zip(["r1", "r2own", "dec", "committed", "value"], outs)), res.as_dict()
+
+
+def wmvc_step(n, q, fp1, self_lane, coin_seed, epoch, phase, slot_base, r1, r2, state,
+              lc_in=0, wm_in=1):
+    lib = load()
+    S = r1.shape[0]
+    outs = [np.zeros(S, np.uint8) for _ in range(5)]
+    res = OrResult()
+    rc = lib.or_wmvc_step(n, q, fp1, self_lane, coin_seed, epoch, phase, slot_base, lc_in, wm_in,
+                          _p(np.ascontiguousarray(r1), u8p), _p(np.ascontiguousarray(r2), u8p),
+                          _p(np.ascontiguousarray(state, np.uint8), u8p), S,
+                          *[_p(o, u8p) for o in outs], ctypes.byref(res))
+    assert rc == 0
+    return dict(zip(["r1", "r2own", "dec", "committed", "value"], outs)), res.as_dict()
+
+
+def ref_structured(n, q, self_lane, seed, rng_base, slot_base, r1, r2):
+    lib = load()
+    S = r1.shape[0]
+    dec = np.zeros(S, np.uint8)
+    res = OrResult()
+    rc = lib.or_ref_structured(n, q, self_lane, seed, rng_base, slot_base,
+                               _p(np.ascontiguousarray(r1), u8p), _p(np.ascontiguousarray(r2), u8p),
+                               S, _p(dec, u8p), ctypes.byref(res))
+    assert rc == 0
+    return dec, res.as_dict()
+
+
+def digest_majority(digests, q):
+    lib = load()
+    n, S = digests.shape
+    out = np.zeros(S, np.uint8)
+    lib.or_digest_majority(n, q, _p(np.ascontiguousarray(digests, np.uint64), u64p), S, _p(out, u8p))
+    return out
+
+
+def digest_trace(n, seed, slot_base, S):
+    lib = load()
+    d = np.zeros((n, S), np.uint64)
+    lib.or_digest_trace(n, seed, slot_base, S, _p(d, u64p))
+    return d
+
+
+def coin_range(coin_seed, epoch, phase, slot_base, S):
+    lib = load()
+    out = np.zeros(S, np.uint8)
+    lib.or_coin_range(coin_seed, epoch, phase, slot_base, S, _p(out, u8p))
+    return out
+
+
+def ref_draws(seed, first, count):
+    lib = load()
+    key = np.zeros(8, np.uint32)
+    lib.or_seed_from_u64(seed, _p(key, u32p))
+    return np.array([lib.or_ref_draw(_p(key, u32p), first + k) for k in range(count)], np.uint64)
+
+
+def chacha_block(key_words, counter, stream, rounds):
+    lib = load()
+    key = np.array(key_words, np.uint32)
+    out = np.zeros(16, np.uint32)
+    lib.or_chacha_block(_p(key, u32p), counter, stream, rounds, _p(out, u32p))
+    return out
+
+
+def seed_from_u64(seed):
+    lib = load()
+    key = np.zeros(8, np.uint32)
+    lib.or_seed_from_u64(seed, _p(key, u32p))
+    return key
+
+
+def pack_planes(codes, stride):
+    lib = load()
+    S, n = codes.shape
+    planes = np.zeros((2 * n, stride), np.uint32)
+    lib.or_pack_planes(_p(np.ascontiguousarray(codes), u8p), n, S, stride, _p(planes, u32p))
+    return planes
+
+
+def count_votes_table(n, q):
+    """All 4^n vectors (lane j = base-4 digit j) through or_count_votes / or_ref_round1."""
+    lib = load()
+    N = 4 ** n
+    idx = np.arange(N, dtype=np.int64)
+    codes = np.stack([(idx >> (2 * j)) & 3 for j in range(n)], axis=1).astype(np.uint8)
+    cv = np.array([lib.or_count_votes(_p(codes[k], u8p), n, q) for k in range(N)], np.uint8)
+    r1 = np.array([lib.or_ref_round1(_p(codes[k], u8p), n, q) for k in range(N)], np.uint8)
+    return codes, cv, r1
