@@ -98,8 +98,12 @@ def main():
     n, G = a.replicas, a.windows
     S = G * WINDOW
     stride = ((S + 127) // 128) * 4
-    stream = torch.cuda.current_stream()
+    # A dedicated stream: the legacy default stream has handle 0, which the C ABI
+    # reads as "the context's own stream"; events must sit on the launch stream.
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
+    assert sp != 0
 
     ev = PhaseEvaluator(n, self_lane=n - 1, mode="ref", seed=42 + rank, device=local)
     sets = []

@@ -27,7 +27,8 @@ struct rg_ctx {
   DevState* state = nullptr;
   DevResult* result = nullptr;
   unsigned long long* lookback = nullptr;
-  uint64_t lookback_cap = 0;
+  unsigned long long* stats = nullptr;
+  uint64_t tile_cap = 0;
   uint32_t seq = 0;
   uint32_t* d_votes = nullptr;
   uint32_t* d_out = nullptr;
@@ -59,18 +60,34 @@ int hip_fail(rg_ctx* ctx, hipError_t e, const char* what) {
 
 constexpr int wmax_for(int n) { return n <= 6 ? 4 : (n <= 10 ? 2 : 1); }
 
+// Tile shapes: {threads, words per thread}. Big tiles keep the per-launch count
+// of tile tickets and look-back hand-offs low on large windows; small tiles fill
+// the 256 CUs on single 2^20-slot windows.
+enum TileCfg { kCfgBig = 0, kCfgMid = 1, kCfgSmall = 2 };
+constexpr int cfg_block(int c) { return c == kCfgBig ? 512 : (c == kCfgMid ? 256 : 128); }
+inline int cfg_words(int c, int n) { return c == kCfgSmall ? 1 : wmax_for(n); }
+
+int pick_cfg(int n, uint64_t n_words) {
+  const uint64_t wm = (uint64_t)wmax_for(n);
+  if (n_words / (512 * wm) >= 256) return kCfgBig;
+  if (n_words / (256 * wm) >= 128) return kCfgMid;
+  return kCfgSmall;
+}
+
 using StepLaunch = void (*)(int, uint32_t, hipStream_t, const StepParams&);
 
 template <int N>
 struct Disp {
   static constexpr int WM = wmax_for(N);
-  static void ref(int w, uint32_t grid, hipStream_t s, const StepParams& p) {
-    if (w == WM) hipLaunchKernelGGL((ref_step_kernel<N, WM>), dim3(grid), dim3(kBlock), 0, s, p);
-    else hipLaunchKernelGGL((ref_step_kernel<N, 1>), dim3(grid), dim3(kBlock), 0, s, p);
+  static void ref(int c, uint32_t grid, hipStream_t s, const StepParams& p) {
+    if (c == kCfgBig) hipLaunchKernelGGL((ref_step_kernel<N, WM, 512>), dim3(grid), dim3(512), 0, s, p);
+    else if (c == kCfgMid) hipLaunchKernelGGL((ref_step_kernel<N, WM, 256>), dim3(grid), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((ref_step_kernel<N, 1, 128>), dim3(grid), dim3(128), 0, s, p);
   }
-  static void wmvc(int w, uint32_t grid, hipStream_t s, const StepParams& p) {
-    if (w == WM) hipLaunchKernelGGL((wmvc_step_kernel<N, WM>), dim3(grid), dim3(kBlock), 0, s, p);
-    else hipLaunchKernelGGL((wmvc_step_kernel<N, 1>), dim3(grid), dim3(kBlock), 0, s, p);
+  static void wmvc(int c, uint32_t grid, hipStream_t s, const StepParams& p) {
+    if (c == kCfgBig) hipLaunchKernelGGL((wmvc_step_kernel<N, WM, 512>), dim3(grid), dim3(512), 0, s, p);
+    else if (c == kCfgMid) hipLaunchKernelGGL((wmvc_step_kernel<N, WM, 256>), dim3(grid), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((wmvc_step_kernel<N, 1, 128>), dim3(grid), dim3(128), 0, s, p);
   }
   static void digest(uint32_t grid, hipStream_t s, const uint64_t* dg, uint64_t ds, uint32_t* out,
                      uint64_t n, uint32_t q) {
@@ -97,12 +114,31 @@ hipStream_t pick_stream(rg_ctx* ctx, void* stream) {
 Record fresh_record() {
   Record r;
   std::memset(&r, 0, sizeof r);
-  r.min_und.v = ~0ull;
   return r;
 }
 
-// Lookback granules for the largest legal call (n_slots < 2^32 at W = 1).
-constexpr uint64_t kLookbackCap = ((1ull << 32) / 32 + kBlock - 1) / kBlock + 1;
+// (Re)allocate the per-tile look-back and statistics granules, zeroed so no
+// stale tag can match a live launch sequence number.
+int ensure_tiles(rg_ctx* ctx, uint64_t n_tiles, bool force_zero) {
+  if (n_tiles <= ctx->tile_cap && !force_zero) return RG_OK;
+  RG_HIP(ctx, hipDeviceSynchronize());
+  if (n_tiles > ctx->tile_cap) {
+    uint64_t cap = ctx->tile_cap ? ctx->tile_cap : 4096;
+    while (cap < n_tiles) cap *= 2;
+    (void)hipFree(ctx->lookback);
+    (void)hipFree(ctx->stats);
+    ctx->lookback = nullptr;
+    ctx->stats = nullptr;
+    ctx->tile_cap = 0;
+    RG_HIP(ctx, hipMalloc(&ctx->lookback, cap * 8));
+    RG_HIP(ctx, hipMalloc(&ctx->stats, cap * kStatGranules * 8));
+    ctx->tile_cap = cap;
+  }
+  RG_HIP(ctx, hipMemset(ctx->lookback, 0, ctx->tile_cap * 8));
+  RG_HIP(ctx, hipMemset(ctx->stats, 0, ctx->tile_cap * kStatGranules * 8));
+  RG_HIP(ctx, hipDeviceSynchronize());
+  return RG_OK;
+}
 
 }  // namespace
 
@@ -169,8 +205,6 @@ int rg_create(rg_ctx** out, const rg_config* cfg) {
   if ((e = hipMalloc(&ctx->rec, 2 * sizeof(Record))) != hipSuccess) return bail(e, "hipMalloc(rec)");
   if ((e = hipMalloc(&ctx->state, sizeof(DevState))) != hipSuccess) return bail(e, "hipMalloc(state)");
   if ((e = hipMalloc(&ctx->result, sizeof(DevResult))) != hipSuccess) return bail(e, "hipMalloc(result)");
-  ctx->lookback_cap = kLookbackCap;
-  if ((e = hipMalloc(&ctx->lookback, ctx->lookback_cap * 8)) != hipSuccess) return bail(e, "hipMalloc(lookback)");
   Record recs[2] = {fresh_record(), fresh_record()};
   DevState st{0, 0, 1, 0};  // PhaseIds start at 1 (state.rs:59-63)
   DevResult res;
@@ -178,8 +212,12 @@ int rg_create(rg_ctx** out, const rg_config* cfg) {
   if ((e = hipMemcpy(ctx->rec, recs, sizeof recs, hipMemcpyHostToDevice)) != hipSuccess) return bail(e, "init rec");
   if ((e = hipMemcpy(ctx->state, &st, sizeof st, hipMemcpyHostToDevice)) != hipSuccess) return bail(e, "init state");
   if ((e = hipMemcpy(ctx->result, &res, sizeof res, hipMemcpyHostToDevice)) != hipSuccess) return bail(e, "init result");
-  if ((e = hipMemset(ctx->lookback, 0, ctx->lookback_cap * 8)) != hipSuccess) return bail(e, "init lookback");
   if ((e = hipDeviceSynchronize()) != hipSuccess) return bail(e, "init sync");
+  if (ensure_tiles(ctx, 4096, true) != RG_OK) {
+    g_err = ctx->err;
+    rg_destroy(ctx);
+    return RG_EHIP;
+  }
   *out = ctx;
   return RG_OK;
 }
@@ -192,6 +230,7 @@ int rg_destroy(rg_ctx* ctx) {
   (void)hipFree(ctx->state);
   (void)hipFree(ctx->result);
   (void)hipFree(ctx->lookback);
+  (void)hipFree(ctx->stats);
   (void)hipFree(ctx->d_votes);
   (void)hipFree(ctx->d_out);
   (void)hipFree(ctx->d_user_result);
@@ -247,20 +286,19 @@ int rg_phase_step_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_de
   RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
   const int n = (int)ctx->cfg.n_replicas;
   const uint64_t n_words = (n_slots + 31) / 32;
-  const int wm = wmax_for(n);
-  const int w = (n_words / ((uint64_t)kBlock * wm) >= 512) ? wm : 1;
-  const uint64_t n_tiles = (n_words + (uint64_t)kBlock * w - 1) / ((uint64_t)kBlock * w);
-  if (n_tiles > ctx->lookback_cap) return fail(ctx, RG_EINVAL, "rg_phase_step: window too large");
-  if (++ctx->seq >= (1u << 31)) {  // look-back tags wrap: start a fresh epoch
-    RG_HIP(ctx, hipDeviceSynchronize());
-    RG_HIP(ctx, hipMemset(ctx->lookback, 0, ctx->lookback_cap * 8));
-    // keep the record parity: seq restarts at 1 or 2 with the same low bit
-    ctx->seq = 2 - (ctx->seq & 1u);
+  const int cfg = pick_cfg(n, n_words);
+  const uint64_t tile_words = (uint64_t)cfg_block(cfg) * cfg_words(cfg, n);
+  const uint64_t n_tiles = (n_words + tile_words - 1) / tile_words;
+  if (int rc = ensure_tiles(ctx, n_tiles, false)) return rc;
+  if (++ctx->seq >= (1u << 31)) {  // tags wrap: start a fresh epoch on zeroed granules
+    if (int rc = ensure_tiles(ctx, n_tiles, true)) return rc;
+    ctx->seq = 2 - (ctx->seq & 1u);  // keep the record-ring parity
   }
   StepParams p;
   p.votes = votes_dev;
   p.out = out_dev;
   p.lookback = ctx->lookback;
+  p.stats = ctx->stats;
   p.rec = ctx->rec;
   p.state = ctx->state;
   p.result = ctx->result;
@@ -279,7 +317,7 @@ int rg_phase_step_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_de
   p.seq = ctx->seq;
   p.n_tiles = (uint32_t)n_tiles;
   hipStream_t s = pick_stream(ctx, stream);
-  (wmvc ? kWmvcLaunch : kRefLaunch)[n](w, (uint32_t)n_tiles, s, p);
+  (wmvc ? kWmvcLaunch : kRefLaunch)[n](cfg, (uint32_t)n_tiles, s, p);
   RG_HIP(ctx, hipGetLastError());
   return RG_OK;
 }

@@ -99,15 +99,10 @@ struct alignas(128) Line {
   unsigned long long pad[15];
 };
 
-// One per launch parity (seq & 1). The finaliser of launch e resets record
+// One per launch parity (seq & 1). The last tile of launch e resets record
 // (e+1)&1 for the next launch, so no host memset sits between steps.
 struct Record {
   Line ticket;     // dynamic tile ticket (decoupled look-back needs dispatch order)
-  Line done;       // arrivals; the arrival that sees n_tiles-1 finalises
-  Line dec_v1;     // n_decided | n_v1 << 32
-  Line pend_vq;    // n_pending_r1 | n_draws << 32
-  Line max_v1p1;   // max(id + 1) over V1 decisions that commit_phase accepts
-  Line min_und;    // min undecided slot id (init ~0)
   Line error;      // device protocol fault bits
 };
 

@@ -18,6 +18,7 @@ namespace rg {
 
 struct StepParams {
   const uint32_t* votes;          // [4N+1][stride]
+  unsigned long long* stats;      // [n_tiles][kStatGranules] tagged granules
   uint32_t* out;                  // [8][stride]
   unsigned long long* lookback;   // [n_tiles] {tag:32 | value:32} granules
   Record* rec;                    // ring of 2
@@ -202,7 +203,10 @@ __device__ __forceinline__ uint32_t lookback_exclusive(unsigned long long* statu
     const unsigned long long need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);
     if (notready & need) {
       if (++spins > (1u << 22)) {  // ~seconds: a protocol fault, not a wait
-        if (lane == 0) atomicOr(err, 1ull);
+        if (lane == 0) {
+          atomicOr(err, 1ull);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -218,59 +222,141 @@ __device__ __forceinline__ uint32_t lookback_exclusive(unsigned long long* statu
   return excl;
 }
 
-// ---- per-block statistics -> record; last arrival finalises the step ----------
-struct BlockStats {
-  unsigned long long dec_v1, pend_vq, max_v1p1, min_und;
+// ---- per-tile statistics -> granules; the last tile reduces them ------------
+// Per tile, kStatGranules 8-B granules {tag = seq : 32 | value : 32}:
+//   0 n_decided, 1 n_v1, 2 n_pending_r1, 3 n_draws,
+//   4 (largest V1 slot offset in the tile that commit_phase accepts) + 1, 0 = none,
+//   5 smallest undecided slot offset in the tile, ~0 = none.
+// One lane writes them with 8-B agent-scope stores; the tile with the last
+// ticket polls and folds them. No per-tile atomics on shared words: thousands of
+// same-address atomics per launch serialise at the memory side.
+constexpr int kStatGranules = 8;
+constexpr uint32_t kSpinLimit = 1u << 24;
+
+struct TileStats {
+  uint32_t dec, v1, pend, draws, max_off1, min_off;
 };
 
-template <bool IS_REF>
-__device__ __forceinline__ void finish_block(const StepParams& p, Record* rec, BlockStats st,
-                                             int tid, int lane, int wave) {
-  __shared__ unsigned long long s_red[kWaves][4];
-  st.dec_v1 = wave_sum64(st.dec_v1);
-  st.pend_vq = wave_sum64(st.pend_vq);
-  st.max_v1p1 = wave_max64(st.max_v1p1);
-  st.min_und = wave_min64(st.min_und);
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_max32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) { uint32_t t = __shfl_xor(v, o, 64); v = t > v ? t : v; }
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_min32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) { uint32_t t = __shfl_xor(v, o, 64); v = t < v ? t : v; }
+  return v;
+}
+
+template <int BLOCK>
+__device__ __forceinline__ TileStats block_reduce_stats(TileStats s, int lane, int wave) {
+  constexpr int WAVES = BLOCK / 64;
+  __shared__ uint32_t red[WAVES][6];
+  s.dec = wave_sum32(s.dec);
+  s.v1 = wave_sum32(s.v1);
+  s.pend = wave_sum32(s.pend);
+  s.draws = wave_sum32(s.draws);
+  s.max_off1 = wave_max32(s.max_off1);
+  s.min_off = wave_min32(s.min_off);
   if (lane == 0) {
-    s_red[wave][0] = st.dec_v1; s_red[wave][1] = st.pend_vq;
-    s_red[wave][2] = st.max_v1p1; s_red[wave][3] = st.min_und;
+    red[wave][0] = s.dec; red[wave][1] = s.v1; red[wave][2] = s.pend;
+    red[wave][3] = s.draws; red[wave][4] = s.max_off1; red[wave][5] = s.min_off;
   }
   __syncthreads();
-  if (tid != 0) return;
-  unsigned long long a = 0, b = 0, mx = 0, mn = ~0ull;
+  TileStats r{0, 0, 0, 0, 0, ~0u};
 #pragma unroll
-  for (int w = 0; w < kWaves; w++) {
-    a += s_red[w][0]; b += s_red[w][1];
-    mx = s_red[w][2] > mx ? s_red[w][2] : mx;
-    mn = s_red[w][3] < mn ? s_red[w][3] : mn;
+  for (int w = 0; w < WAVES; w++) {
+    r.dec += red[w][0]; r.v1 += red[w][1]; r.pend += red[w][2]; r.draws += red[w][3];
+    r.max_off1 = red[w][4] > r.max_off1 ? red[w][4] : r.max_off1;
+    r.min_off = red[w][5] < r.min_off ? red[w][5] : r.min_off;
   }
-  if (a) atomicAdd(&rec->dec_v1.v, a);
-  if (b) atomicAdd(&rec->pend_vq.v, b);
-  if (mx) atomicMax(&rec->max_v1p1.v, mx);
-  if (mn != ~0ull) atomicMin(&rec->min_und.v, mn);
-  // The statistics atomics must be performed before our arrival is counted.
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const unsigned long long old = atomicAdd(&rec->done.v, 1ull);
-  if (old != (unsigned long long)p.n_tiles - 1) return;
+  return r;
+}
 
-  // Last arrival: every other block's atomics are complete. Read totals with
-  // atomic RMWs (performed where the adds were), update the engine state.
-  const unsigned long long dv = atomicAdd(&rec->dec_v1.v, 0ull);
-  const unsigned long long pv = atomicAdd(&rec->pend_vq.v, 0ull);
-  const unsigned long long mxv = atomicAdd(&rec->max_v1p1.v, 0ull);
-  const unsigned long long mnv = atomicAdd(&rec->min_und.v, 0ull);
-  const unsigned long long err = atomicAdd(&rec->error.v, 0ull);
+template <int BLOCK>
+__device__ __forceinline__ void block_reduce_totals(unsigned long long (&v)[7], int lane, int wave) {
+  constexpr int WAVES = BLOCK / 64;
+  __shared__ unsigned long long red[WAVES][7];
+#pragma unroll
+  for (int k = 0; k < 4; k++) v[k] = wave_sum64(v[k]);
+  v[4] = wave_max64(v[4]);
+  v[5] = wave_min64(v[5]);
+  v[6] = wave_max64(v[6]);
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < 7; k++) red[wave][k] = v[k];
+  __syncthreads();
+  unsigned long long r[7] = {0, 0, 0, 0, 0, ~0ull, 0};
+#pragma unroll
+  for (int w = 0; w < WAVES; w++) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) r[k] += red[w][k];
+    r[4] = red[w][4] > r[4] ? red[w][4] : r[4];
+    r[5] = red[w][5] < r[5] ? red[w][5] : r[5];
+    r[6] = red[w][6] > r[6] ? red[w][6] : r[6];
+  }
+#pragma unroll
+  for (int k = 0; k < 7; k++) v[k] = r[k];
+}
+
+// Publish this tile's statistics; the tile holding the last ticket folds every
+// tile's granules, advances the device engine state and writes the step result.
+template <bool IS_REF, int BLOCK, int W>
+__device__ __forceinline__ void finish_tile(const StepParams& p, Record* rec, TileStats ts,
+                                            uint32_t tile, int tid, int lane, int wave) {
+  constexpr uint64_t kTileSlots = (uint64_t)BLOCK * W * 32;
+  const TileStats b = block_reduce_stats<BLOCK>(ts, lane, wave);
+  const unsigned long long tag = (unsigned long long)p.seq << 32;
+  if (tid == 0) {
+    unsigned long long* g = p.stats + (uint64_t)tile * kStatGranules;
+    atomic_store_agent(g + 0, tag | b.dec);
+    atomic_store_agent(g + 1, tag | b.v1);
+    atomic_store_agent(g + 2, tag | b.pend);
+    atomic_store_agent(g + 3, tag | b.draws);
+    atomic_store_agent(g + 4, tag | b.max_off1);
+    atomic_store_agent(g + 5, tag | b.min_off);
+  }
+  if (tile != p.n_tiles - 1) return;
+
+  unsigned long long v[7] = {0, 0, 0, 0, 0, ~0ull, 0};  // dec v1 pend draws max(id+1) min(id) fault
+  for (uint32_t i = tid; i < p.n_tiles; i += BLOCK) {
+    unsigned long long* g = p.stats + (uint64_t)i * kStatGranules;
+    uint32_t x[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      unsigned long long gv = atomic_load_agent(g + k);
+      uint32_t spins = 0;
+      while ((uint32_t)(gv >> 32) != p.seq) {
+        if (++spins > kSpinLimit) { v[6] = 2; break; }
+        __builtin_amdgcn_s_sleep(2);
+        gv = atomic_load_agent(g + k);
+      }
+      x[k] = (uint32_t)gv;
+    }
+    const unsigned long long tb = p.slot_base + (unsigned long long)i * kTileSlots;
+    v[0] += x[0]; v[1] += x[1]; v[2] += x[2]; v[3] += x[3];
+    if (x[4] && tb + x[4] > v[4]) v[4] = tb + x[4];
+    if (x[5] != ~0u && tb + x[5] < v[5]) v[5] = tb + x[5];
+  }
+  block_reduce_totals<BLOCK>(v, lane, wave);
+  if (tid != 0) return;
+  const unsigned long long err = atomicAdd(&rec->error.v, 0ull) | v[6];
   DevState s = *p.state;
   DevResult r;
   r.n_slots = p.n_slots;
-  r.n_decided = dv & 0xffffffffull;
-  r.n_v1 = dv >> 32;
-  r.n_pending_r1 = pv & 0xffffffffull;
-  r.n_draws = pv >> 32;
+  r.n_decided = v[0];
+  r.n_v1 = v[1];
+  r.n_pending_r1 = v[2];
+  r.n_draws = v[3];
   unsigned long long lc = s.last_committed;          // commit_phase: monotonic max,
-  if (mxv && mxv - 1 > lc) lc = mxv - 1;             // state.rs:77-99
+  if (v[4] && v[4] - 1 > lc) lc = v[4] - 1;          // state.rs:77-99
   const unsigned long long end = p.slot_base + p.n_slots;
-  const unsigned long long fu = mnv < end ? mnv : end;
+  const unsigned long long fu = v[5] < end ? v[5] : end;
   unsigned long long wm = s.commit_watermark;
   if (p.slot_base <= wm && wm < fu) wm = fu;
   r.last_committed_max = lc;
@@ -287,49 +373,52 @@ __device__ __forceinline__ void finish_block(const StepParams& p, Record* rec, B
   if (p.result_user) *p.result_user = r;
   Record* nxt = p.rec + ((p.seq + 1) & 1u);
   atomic_store_agent(&nxt->ticket.v, 0ull);
-  atomic_store_agent(&nxt->done.v, 0ull);
-  atomic_store_agent(&nxt->dec_v1.v, 0ull);
-  atomic_store_agent(&nxt->pend_vq.v, 0ull);
-  atomic_store_agent(&nxt->max_v1p1.v, 0ull);
-  atomic_store_agent(&nxt->min_und.v, ~0ull);
   atomic_store_agent(&nxt->error.v, 0ull);
 }
 
+// Per-thread statistics; offsets are relative to the tile's first slot.
 template <int W>
-__device__ __forceinline__ void thread_extrema(const uint32_t (&committed)[W],
-                                               const uint32_t (&v1)[W], const uint32_t (&vm)[W],
-                                               uint64_t w0, const StepParams& p,
-                                               unsigned long long& max_v1p1,
-                                               unsigned long long& min_und) {
-  max_v1p1 = 0;
-  min_und = ~0ull;
+__device__ __forceinline__ TileStats thread_stats(const uint32_t (&committed)[W], const uint32_t (&v1)[W],
+                                                  const uint32_t (&pend)[W], const uint32_t (&vm)[W],
+                                                  uint32_t draws, uint64_t w0, uint32_t tw0,
+                                                  const StepParams& p) {
+  TileStats t{0, 0, 0, draws, 0, ~0u};
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    t.dec += __builtin_popcount(committed[i]);
+    t.v1 += __builtin_popcount(v1[i]);
+    t.pend += __builtin_popcount(pend[i]);
+  }
 #pragma unroll
   for (int i = W - 1; i >= 0; i--) {
     const uint32_t m = v1[i] & phase_limit_mask(p.slot_base, w0 + i, p.max_phase);
-    if (m && !max_v1p1) max_v1p1 = p.slot_base + 32 * (w0 + i) + (31 - __builtin_clz(m)) + 1;
+    if (m && !t.max_off1) t.max_off1 = 32u * (tw0 + i) + (31u - __builtin_clz(m)) + 1u;
   }
 #pragma unroll
   for (int i = 0; i < W; i++) {
     const uint32_t m = ~committed[i] & vm[i];
-    if (m && min_und == ~0ull) min_und = p.slot_base + 32 * (w0 + i) + __builtin_ctz(m);
+    if (m && t.min_off == ~0u) t.min_off = 32u * (tw0 + i) + __builtin_ctz(m);
   }
+  return t;
 }
 
 // ============================================================================
 // REF phase step: engine.rs:483-682 on the final vote sets of every slot.
 // ============================================================================
-template <int N, int W>
-__global__ __launch_bounds__(kBlock) void ref_step_kernel(StepParams p) {
+template <int N, int W, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void ref_step_kernel(StepParams p) {
   constexpr int B = ctr_bits(N);
+  constexpr int WAVES = BLOCK / 64;
   __shared__ uint32_t s_ticket;
-  __shared__ uint32_t s_wave[kWaves];
+  __shared__ uint32_t s_wave[WAVES];
   __shared__ uint32_t s_excl;
   Record* rec = p.rec + (p.seq & 1u);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (tid == 0) s_ticket = (uint32_t)atomicAdd(&rec->ticket.v, 1ull);
   __syncthreads();
   const uint32_t tile = s_ticket;
-  const uint64_t w0 = ((uint64_t)tile * kBlock + tid) * W;
+  const uint32_t tw0 = (uint32_t)tid * W;  // word offset inside the tile
+  const uint64_t w0 = (uint64_t)tile * BLOCK * W + tw0;
   const bool active = w0 < p.n_words;
 
   // Issue every plane load up front (R2 stays in flight across the look-back).
@@ -385,7 +474,7 @@ __global__ __launch_bounds__(kBlock) void ref_step_kernel(StepParams p) {
   __syncthreads();
   uint32_t wave_off = 0, tile_total = 0;
 #pragma unroll
-  for (int w = 0; w < kWaves; w++) {
+  for (int w = 0; w < WAVES; w++) {
     wave_off += (w < wave) ? s_wave[w] : 0u;
     tile_total += s_wave[w];
   }
@@ -434,7 +523,6 @@ __global__ __launch_bounds__(kBlock) void ref_step_kernel(StepParams p) {
     }
   }
   uint32_t o[kOutPlanes][W];
-  unsigned long long n_dec = 0, n_v1 = 0, n_pend = 0;
 #pragma unroll
   for (int i = 0; i < W; i++) {
     Ctr<B> c0, c1, cq;
@@ -458,20 +546,14 @@ __global__ __launch_bounds__(kBlock) void ref_step_kernel(StepParams p) {
     o[5][i] = (dq | dn) & vm[i];
     o[6][i] = (d0 | d1) & vm[i];   // set_decision: committed iff not VQuestion
     o[7][i] = d1 & vm[i];          // V1: apply_batch + commit_phase
-    n_dec += __builtin_popcount(o[6][i]);
-    n_v1 += __builtin_popcount(o[7][i]);
-    n_pend += __builtin_popcount(pend[i]);
   }
   if (active) {
     uint32_t* ob = p.out + w0;
 #pragma unroll
     for (int pl = 0; pl < kOutPlanes; pl++) store_words<W>(ob + (uint64_t)pl * p.stride, o[pl]);
   }
-  BlockStats st;
-  st.dec_v1 = n_dec | (n_v1 << 32);
-  st.pend_vq = n_pend | ((unsigned long long)vq_count << 32);
-  thread_extrema<W>(o[6], o[7], vm, w0, p, st.max_v1p1, st.min_und);
-  finish_block<true>(p, rec, st, tid, lane, wave);
+  const TileStats ts = thread_stats<W>(o[6], o[7], pend, vm, vq_count, w0, tw0, p);
+  finish_tile<true, BLOCK, W>(p, rec, ts, tile, tid, lane, wave);
 }
 
 // ============================================================================
@@ -496,12 +578,14 @@ __device__ __forceinline__ uint32_t coin_word(const Key& key, uint64_t stream, u
   return (words[0] >> sh) | (words[1] << (32u - sh));
 }
 
-template <int N, int W>
-__global__ __launch_bounds__(kBlock) void wmvc_step_kernel(StepParams p) {
+template <int N, int W, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void wmvc_step_kernel(StepParams p) {
   constexpr int B = ctr_bits(N);
   Record* rec = p.rec + (p.seq & 1u);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint64_t w0 = ((uint64_t)blockIdx.x * kBlock + tid) * W;
+  const uint32_t tile = blockIdx.x;  // no cross-tile dependency: no ticket needed
+  const uint32_t tw0 = (uint32_t)tid * W;
+  const uint64_t w0 = (uint64_t)tile * BLOCK * W + tw0;
   const bool active = w0 < p.n_words;
   uint32_t r1lo[N][W], r1hi[N][W], r2lo[N][W], r2hi[N][W], st_in[W];
   if (active) {
@@ -523,7 +607,7 @@ __global__ __launch_bounds__(kBlock) void wmvc_step_kernel(StepParams p) {
     }
   }
   uint32_t o[kOutPlanes][W];
-  unsigned long long n_dec = 0, n_v1 = 0, n_pend = 0, n_coin = 0;
+  uint32_t pend_w[W], n_coin = 0;
   unsigned long long cur_blk = ~0ull;
   uint32_t blk[16];
 #pragma unroll
@@ -577,9 +661,7 @@ __global__ __launch_bounds__(kBlock) void wmvc_step_kernel(StepParams p) {
     o[5][i] = ~(d0 | d1) & vm;
     o[6][i] = (d0 | d1) & vm;
     o[7][i] = next & vm;
-    n_dec += __builtin_popcount(o[6][i]);
-    n_v1 += __builtin_popcount(d1 & vm);
-    n_pend += __builtin_popcount(pend1 & vm);
+    pend_w[i] = pend1 & vm;
     n_coin += __builtin_popcount(cm);
   }
   if (active) {
@@ -593,11 +675,8 @@ __global__ __launch_bounds__(kBlock) void wmvc_step_kernel(StepParams p) {
     vm_all[i] = valid_mask(w0 + i, p.n_words, p.n_slots);
     dv1[i] = o[6][i] & o[4][i];  // committed with decision code lo bit set = V1
   }
-  BlockStats st;
-  st.dec_v1 = n_dec | (n_v1 << 32);
-  st.pend_vq = n_pend | (n_coin << 32);
-  thread_extrema<W>(o[6], dv1, vm_all, w0, p, st.max_v1p1, st.min_und);
-  finish_block<false>(p, rec, st, tid, lane, wave);
+  const TileStats ts = thread_stats<W>(o[6], dv1, pend_w, vm_all, n_coin, w0, tw0, p);
+  finish_tile<false, BLOCK, W>(p, rec, ts, tile, tid, lane, wave);
 }
 
 // ============================================================================

@@ -1,0 +1,100 @@
+"""N>1 path on CPU: world_size-2 gloo ranks each evaluate their slot shard (with the
+oracle standing in for the device step on this GPU-less host), exchange results
+and decided bitmaps with all_gather, and the folded global commit must equal one
+evaluator over the whole window."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from rabia_amd import shard
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def test_shard_range_partitions():
+    for total in (1, 127, 128, 1000, 1 << 20):
+        for world in (1, 2, 3, 8):
+            parts = [shard.shard_range(total, world, r) for r in range(world)]
+            assert sum(c for _, c in parts) == total
+            pos = 0
+            for s, c in parts:
+                assert s == pos and (s % 128 == 0 or c == 0)
+                pos += c
+
+
+def test_combine_single_shard_identity(oracle):
+    r1, r2, st = oracle.trace(0, 5, 3, 10, 999)
+    _, res = oracle.wmvc_step(5, 3, 3, 0, 7, 1, 2, 10, r1, r2, st, lc_in=4, wm_in=10)
+    g = shard.combine([res], [0], [999], 10, 10, 4)
+    assert g.commit_watermark == res["commit_watermark"]
+    assert g.last_committed == res["last_committed_max"]
+    assert g.first_undecided == res["first_undecided"]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "tests"), root]
+    import oracle_lib as O
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n, S, base = 5, 10_000, 1
+        r1, r2, st = O.trace(1, n, 5, base, S)
+        start, count = shard.shard_range(S, world, rank)
+        sl = slice(start, start + count)
+        out, res = O.wmvc_step(n, 3, 3, 0, 11, 2, 1, base + start, r1[sl], r2[sl], st[sl],
+                               lc_in=0, wm_in=1)
+        rows = shard.exchange_results(torch.tensor(shard.result_row(res), dtype=torch.int64))
+        starts = [shard.shard_range(S, world, r)[0] for r in range(world)]
+        counts = [shard.shard_range(S, world, r)[1] for r in range(world)]
+        g = shard.combine([shard.row_result(rw.tolist()) for rw in rows], starts, counts, base, 1, 0)
+        width = max(counts)  # shards differ by <= one alignment unit: pad to equal size
+        bm = np.zeros(width, np.uint8)
+        bm[:count] = out["committed"]
+        bms = shard.exchange_bitmap(torch.from_numpy(bm)).numpy()
+        full = np.concatenate([bms[r][:counts[r]] for r in range(world)])
+        q.put((rank, g, full.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_gloo_global_commit(oracle):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    import queue
+    got = []
+    while len(got) < world:
+        try:
+            got.append(q.get(timeout=1))
+        except queue.Empty:
+            assert all(p.is_alive() or p.exitcode == 0 for p in procs), "a rank died"
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    n, S = 5, 10_000
+    r1, r2, st = oracle.trace(1, n, 5, 1, S)
+    out, res = oracle.wmvc_step(n, 3, 3, 0, 11, 2, 1, 1, r1, r2, st, lc_in=0, wm_in=1)
+    for rank, g, bits in got:
+        assert g.n_decided == res["n_decided"] and g.n_v1 == res["n_v1"]
+        assert g.last_committed == res["last_committed_max"]
+        assert g.first_undecided == res["first_undecided"]
+        assert g.commit_watermark == res["commit_watermark"]
+        assert g.n_draws == res["n_draws"]
+        np.testing.assert_array_equal(np.array(bits, np.uint8), out["committed"])

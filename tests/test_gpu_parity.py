@@ -93,7 +93,8 @@ def test_truth_tables_exhaustive(golden, n, q):
     coins = oracle_lib.coin_range(9, 0, 4, 1, 4 ** n)
     exp_dec = np.where(cls == 0, 0, np.where(cls == 1, 1, 3))
     exp_val = np.select([cls == 0, cls == 1, cls == 2, cls == 3, cls == 4, cls == 5],
-                        [0, 1, 0, 1, coins, st])
+                        [np.zeros_like(st), np.ones_like(st), np.zeros_like(st), np.ones_like(st),
+                         coins.astype(np.uint8), st])
     np.testing.assert_array_equal(got["dec"], exp_dec)
     np.testing.assert_array_equal(got["value"], exp_val)
 
