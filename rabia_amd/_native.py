@@ -68,6 +68,10 @@ _SIGS = {
     "rg_stream_sync": (ctypes.c_int, [vp, vp]),
     "rg_pack_codes": (ctypes.c_int, [vp, u32, u64, u64, vp]),
     "rg_unpack_planes": (ctypes.c_int, [vp, u32, u64, u64, vp]),
+    # diagnostics (include/rabia_gpu_debug.h)
+    "rg_debug_set": (ctypes.c_int, [vp, u32]),
+    "rg_debug_stamps": (ctypes.c_int, [vp, vp, u64]),
+    "rg_debug_stream_probe": (ctypes.c_int, [vp, vp, u64, u64, u32, u32, vp]),
 }
 
 _lib = None

@@ -17,7 +17,7 @@ LIB_DIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIB_DIR, "librabia_gpu.so")
 SOURCES = [os.path.join(CSRC, "rabia_gpu.hip")]
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("rg_common.h", "rg_kernels.h")] + [
-    os.path.join(ROOT, "include", "rabia_gpu.h")]
+    os.path.join(ROOT, "include", "rabia_gpu.h"), os.path.join(ROOT, "include", "rabia_gpu_debug.h")]
 ARCH = "gfx950"
 
 

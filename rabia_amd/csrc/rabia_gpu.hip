@@ -5,6 +5,7 @@
 // memory and are advanced by the last workgroup of every step, so consecutive
 // steps on one stream never round-trip through the host.
 #include "rabia_gpu.h"
+#include "rabia_gpu_debug.h"
 
 #include <hip/hip_runtime.h>
 
@@ -34,6 +35,9 @@ struct rg_ctx {
   uint32_t* d_out = nullptr;
   DevResult* d_user_result = nullptr;
   uint64_t stage_votes_words = 0, stage_out_words = 0;
+  uint32_t diag = 0;
+  unsigned long long* dbg = nullptr;
+  uint64_t dbg_cap = 0;
   std::string err;
 };
 
@@ -231,6 +235,7 @@ int rg_destroy(rg_ctx* ctx) {
   (void)hipFree(ctx->result);
   (void)hipFree(ctx->lookback);
   (void)hipFree(ctx->stats);
+  (void)hipFree(ctx->dbg);
   (void)hipFree(ctx->d_votes);
   (void)hipFree(ctx->d_out);
   (void)hipFree(ctx->d_user_result);
@@ -286,7 +291,8 @@ int rg_phase_step_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_de
   RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
   const int n = (int)ctx->cfg.n_replicas;
   const uint64_t n_words = (n_slots + 31) / 32;
-  const int cfg = pick_cfg(n, n_words);
+  const uint32_t force = (ctx->diag >> 8) & 3u;  // diagnostics: force a tile shape
+  const int cfg = force ? (int)force - 1 : pick_cfg(n, n_words);
   const uint64_t tile_words = (uint64_t)cfg_block(cfg) * cfg_words(cfg, n);
   const uint64_t n_tiles = (n_words + tile_words - 1) / tile_words;
   if (int rc = ensure_tiles(ctx, n_tiles, false)) return rc;
@@ -316,6 +322,19 @@ int rg_phase_step_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_de
   p.self_lane = ctx->cfg.self_lane;
   p.seq = ctx->seq;
   p.n_tiles = (uint32_t)n_tiles;
+  p.diag = ctx->diag & 0xffu;
+  p.dbg = nullptr;
+  if (ctx->diag & 4u) {
+    if (ctx->dbg_cap < n_tiles * 8) {
+      RG_HIP(ctx, hipDeviceSynchronize());
+      (void)hipFree(ctx->dbg);
+      ctx->dbg = nullptr;
+      RG_HIP(ctx, hipMalloc(&ctx->dbg, n_tiles * 8 * 8));
+      ctx->dbg_cap = n_tiles * 8;
+    }
+    RG_HIP(ctx, hipMemsetAsync(ctx->dbg, 0, n_tiles * 8 * 8, pick_stream(ctx, stream)));
+    p.dbg = ctx->dbg;
+  }
   hipStream_t s = pick_stream(ctx, stream);
   (wmvc ? kWmvcLaunch : kRefLaunch)[n](cfg, (uint32_t)n_tiles, s, p);
   RG_HIP(ctx, hipGetLastError());
@@ -464,6 +483,34 @@ int rg_unpack_planes(const uint32_t* planes, uint32_t n, uint64_t n_slots, uint6
       codes[s * n + j] = (uint8_t)(lo | (hi << 1));
     }
   }
+  return RG_OK;
+}
+
+// ---- diagnostics (include/rabia_gpu_debug.h) ---------------------------------
+int rg_debug_set(rg_ctx* ctx, uint32_t diag) {
+  if (!ctx) return fail(nullptr, RG_EINVAL, "rg_debug_set: null context");
+  ctx->diag = diag;
+  return RG_OK;
+}
+
+int rg_debug_stamps(rg_ctx* ctx, uint64_t* host_out, uint64_t n_words) {
+  if (!ctx || !host_out) return fail(ctx, RG_EINVAL, "rg_debug_stamps: null argument");
+  if (!ctx->dbg) return fail(ctx, RG_EINVAL, "rg_debug_stamps: no stamps recorded (diag & 4)");
+  RG_HIP(ctx, hipDeviceSynchronize());
+  const uint64_t n = n_words < ctx->dbg_cap ? n_words : ctx->dbg_cap;
+  RG_HIP(ctx, hipMemcpy(host_out, ctx->dbg, n * 8, hipMemcpyDeviceToHost));
+  return RG_OK;
+}
+
+int rg_debug_stream_probe(const uint32_t* in_dev, uint32_t* out_dev, uint64_t n_words, uint64_t stride,
+                          uint32_t tile_words, uint32_t nt, void* stream) {
+  if (!in_dev || !out_dev || n_words % 4 || stride % 4 || (tile_words && (tile_words % 4 || n_words % tile_words)))
+    return fail(nullptr, RG_EINVAL, "rg_debug_stream_probe: bad arguments");
+  const dim3 grid((uint32_t)((n_words + 1023) / 1024));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (nt) hipLaunchKernelGGL((stream_probe_kernel<20, 8, true>), grid, dim3(256), 0, s, in_dev, out_dev, stride, n_words, tile_words);
+  else hipLaunchKernelGGL((stream_probe_kernel<20, 8, false>), grid, dim3(256), 0, s, in_dev, out_dev, stride, n_words, tile_words);
+  RG_HIP(nullptr, hipGetLastError());
   return RG_OK;
 }
 

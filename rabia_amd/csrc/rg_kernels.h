@@ -37,7 +37,14 @@ struct StepParams {
   int32_t self_lane;
   uint32_t seq;
   uint32_t n_tiles;
+  uint32_t diag;                  // diagnostic build switches (0 in production):
+                                  //  1 skip the look-back wait, 2 skip finish_tile, 4 stamps
+  unsigned long long* dbg;        // [n_tiles][8] s_memrealtime stamps when diag & 4
 };
+
+__device__ __forceinline__ void stamp(const StepParams& p, uint32_t tile, int k, int tid) {
+  if ((p.diag & 4u) && tid == 0) p.dbg[(uint64_t)tile * 8 + k] = __builtin_amdgcn_s_memrealtime();
+}
 
 constexpr int ctr_bits(int n) { return n < 2 ? 1 : n < 4 ? 2 : n < 8 ? 3 : n < 16 ? 4 : 5; }
 
@@ -171,6 +178,13 @@ __device__ __forceinline__ void atomic_store_agent(unsigned long long* p, unsign
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Workgroup barrier for LDS hand-offs only. __syncthreads() also drains every
+// outstanding global load and store (its workgroup-scope release waits on
+// vmcnt), which would serialise the tile's HBM traffic behind each barrier.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // ---- decoupled look-back (run by all 64 lanes of wave 0) ----------------------
 // Granule = {tag:32 | value:32}, tag = seq<<1 | inclusive, written by ONE 8-B
 // agent-scope store and read by agent-scope loads (MI355X_MICROARCH.md,
@@ -267,7 +281,7 @@ __device__ __forceinline__ TileStats block_reduce_stats(TileStats s, int lane, i
     red[wave][0] = s.dec; red[wave][1] = s.v1; red[wave][2] = s.pend;
     red[wave][3] = s.draws; red[wave][4] = s.max_off1; red[wave][5] = s.min_off;
   }
-  __syncthreads();
+  lds_barrier();
   TileStats r{0, 0, 0, 0, 0, ~0u};
 #pragma unroll
   for (int w = 0; w < WAVES; w++) {
@@ -290,7 +304,7 @@ __device__ __forceinline__ void block_reduce_totals(unsigned long long (&v)[7], 
   if (lane == 0)
 #pragma unroll
     for (int k = 0; k < 7; k++) red[wave][k] = v[k];
-  __syncthreads();
+  lds_barrier();
   unsigned long long r[7] = {0, 0, 0, 0, 0, ~0ull, 0};
 #pragma unroll
   for (int w = 0; w < WAVES; w++) {
@@ -326,24 +340,31 @@ __device__ __forceinline__ void finish_tile(const StepParams& p, Record* rec, Ti
   unsigned long long v[7] = {0, 0, 0, 0, 0, ~0ull, 0};  // dec v1 pend draws max(id+1) min(id) fault
   for (uint32_t i = tid; i < p.n_tiles; i += BLOCK) {
     unsigned long long* g = p.stats + (uint64_t)i * kStatGranules;
+    unsigned long long gv[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) gv[k] = atomic_load_agent(g + k);  // all in flight at once
+    uint32_t spins = 0;
+    for (;;) {
+      bool ready = true;
+#pragma unroll
+      for (int k = 0; k < 6; k++) ready &= (uint32_t)(gv[k] >> 32) == p.seq;
+      if (ready) break;
+      if (++spins > kSpinLimit) { v[6] = 2; break; }
+      __builtin_amdgcn_s_sleep(2);
+#pragma unroll
+      for (int k = 0; k < 6; k++)
+        if ((uint32_t)(gv[k] >> 32) != p.seq) gv[k] = atomic_load_agent(g + k);
+    }
     uint32_t x[6];
 #pragma unroll
-    for (int k = 0; k < 6; k++) {
-      unsigned long long gv = atomic_load_agent(g + k);
-      uint32_t spins = 0;
-      while ((uint32_t)(gv >> 32) != p.seq) {
-        if (++spins > kSpinLimit) { v[6] = 2; break; }
-        __builtin_amdgcn_s_sleep(2);
-        gv = atomic_load_agent(g + k);
-      }
-      x[k] = (uint32_t)gv;
-    }
+    for (int k = 0; k < 6; k++) x[k] = (uint32_t)gv[k];
     const unsigned long long tb = p.slot_base + (unsigned long long)i * kTileSlots;
     v[0] += x[0]; v[1] += x[1]; v[2] += x[2]; v[3] += x[3];
     if (x[4] && tb + x[4] > v[4]) v[4] = tb + x[4];
     if (x[5] != ~0u && tb + x[5] < v[5]) v[5] = tb + x[5];
   }
   block_reduce_totals<BLOCK>(v, lane, wave);
+  stamp(p, tile, 5, tid);
   if (tid != 0) return;
   const unsigned long long err = atomicAdd(&rec->error.v, 0ull) | v[6];
   DevState s = *p.state;
@@ -371,9 +392,24 @@ __device__ __forceinline__ void finish_tile(const StepParams& p, Record* rec, Ti
   *p.state = s;
   *p.result = r;
   if (p.result_user) *p.result_user = r;
-  Record* nxt = p.rec + ((p.seq + 1) & 1u);
-  atomic_store_agent(&nxt->ticket.v, 0ull);
-  atomic_store_agent(&nxt->error.v, 0ull);
+}
+
+// Called once per tile right after it learns its index. The holder of the last
+// tile resets the OTHER record of the ring for the next launch (the previous
+// launch, which used it, completed before this one started: stream order).
+// A tile index outside the launch (a ring that was not reset) exits before any
+// memory access and raises a fault bit instead of indexing out of bounds.
+__device__ __forceinline__ bool tile_prologue(const StepParams& p, Record* rec, uint32_t tile, int tid) {
+  if (tile >= p.n_tiles) {
+    if (tid == 0) atomicOr(&rec->error.v, 4ull);
+    return false;
+  }
+  if (tid == 0 && tile == p.n_tiles - 1) {
+    Record* nxt = p.rec + ((p.seq + 1) & 1u);
+    atomic_store_agent(&nxt->ticket.v, 0ull);
+    atomic_store_agent(&nxt->error.v, 0ull);
+  }
+  return true;
 }
 
 // Per-thread statistics; offsets are relative to the tile's first slot.
@@ -415,8 +451,10 @@ __global__ __launch_bounds__(BLOCK) void ref_step_kernel(StepParams p) {
   Record* rec = p.rec + (p.seq & 1u);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (tid == 0) s_ticket = (uint32_t)atomicAdd(&rec->ticket.v, 1ull);
-  __syncthreads();
+  lds_barrier();
   const uint32_t tile = s_ticket;
+  if (!tile_prologue(p, rec, tile, tid)) return;
+  stamp(p, tile, 0, tid);
   const uint32_t tw0 = (uint32_t)tid * W;  // word offset inside the tile
   const uint64_t w0 = (uint64_t)tile * BLOCK * W + tw0;
   const bool active = w0 < p.n_words;
@@ -471,44 +509,61 @@ __global__ __launch_bounds__(BLOCK) void ref_step_kernel(StepParams p) {
   // ---- exclusive prefix of VQ slots: block scan + cross-tile look-back
   const uint32_t incl = wave_incl_scan32(vq_count, lane);
   if (lane == 63) s_wave[wave] = incl;
-  __syncthreads();
+  lds_barrier();
   uint32_t wave_off = 0, tile_total = 0;
 #pragma unroll
   for (int w = 0; w < WAVES; w++) {
     wave_off += (w < wave) ? s_wave[w] : 0u;
     tile_total += s_wave[w];
   }
+  stamp(p, tile, 1, tid);
   if (wave == 0) {
-    const uint32_t e = lookback_exclusive(p.lookback, tile, p.seq, tile_total, lane, &rec->error.v);
+    const uint32_t e = (p.diag & 1u) ? 0u
+                                     : lookback_exclusive(p.lookback, tile, p.seq, tile_total, lane, &rec->error.v);
     if (lane == 0) s_excl = e;
   }
-  __syncthreads();
-  unsigned long long k = p.state->rng_next + s_excl + wave_off + incl - vq_count;
+  lds_barrier();
+  stamp(p, tile, 2, tid);
 
-  // ---- own round-2 vote (engine.rs:523-537; VQ -> one StdRng draw, 567-611)
-  uint32_t own_lo[W];
-  unsigned long long cur_blk = ~0ull;
-  uint32_t blk[16];
+  // ---- own round-2 vote (engine.rs:523-537; VQ -> one StdRng draw, 567-611).
+  // The tile's draws are ONE contiguous index range [k_tile, k_tile + tile_total):
+  // its ChaCha12 blocks are computed once, one per thread, and staged in LDS.
+  const unsigned long long k_tile = p.state->rng_next + s_excl;
+  unsigned long long k = k_tile + wave_off + incl - vq_count;
+  uint32_t own_lo[W], mq[W];
 #pragma unroll
   for (int i = 0; i < W; i++) {
-    uint32_t m = r1vq[i], dv1 = 0;
-    while (m) {
-      const int b = __builtin_ctz(m);
-      m &= m - 1;
-      const unsigned long long bi = k >> 3;
-      if (bi != cur_blk) {
-        chacha_block<12>(p.key, bi, 0, blk);
-        cur_blk = bi;
+    own_lo[i] = r1v1[i];
+    mq[i] = r1vq[i];
+  }
+  if (tile_total) {
+    __shared__ uint32_t s_blk[BLOCK][17];  // +1 word: conflict-free rows
+    const unsigned long long b_first = k_tile >> 3, b_last = (k_tile + tile_total - 1) >> 3;
+    for (unsigned long long cb = b_first; cb <= b_last; cb += BLOCK) {
+      if (cb + tid <= b_last) {
+        uint32_t x[16];
+        chacha_block<12>(p.key, cb + tid, 0, x);
+#pragma unroll
+        for (int j = 0; j < 16; j++) s_blk[tid][j] = x[j];
       }
-      const uint32_t ws = (uint32_t)(k & 7u) * 2u;
-      const unsigned long long u =
-          (unsigned long long)select16(blk, ws) | ((unsigned long long)select16(blk, ws + 1) << 32);
-      const uint32_t c0 = ctr_at(c0s[i], b), c1 = ctr_at(c1s[i], b);
-      const bool v1 = c1 > c0 ? (u < kP90) : (c1 < c0 ? (u >= kP90) : (u < kP80));
-      dv1 |= (uint32_t)v1 << b;
-      k++;
+      lds_barrier();
+      const unsigned long long k_lim = (cb + BLOCK) << 3;
+#pragma unroll
+      for (int i = 0; i < W; i++) {
+        while (mq[i] && k < k_lim) {
+          const int b = __builtin_ctz(mq[i]);
+          mq[i] &= mq[i] - 1;
+          const uint32_t row = (uint32_t)((k >> 3) - cb), ws = (uint32_t)(k & 7u) * 2u;
+          const unsigned long long u =
+              (unsigned long long)s_blk[row][ws] | ((unsigned long long)s_blk[row][ws + 1] << 32);
+          const uint32_t c0 = ctr_at(c0s[i], b), c1 = ctr_at(c1s[i], b);
+          const bool v1 = c1 > c0 ? (u < kP90) : (c1 < c0 ? (u >= kP90) : (u < kP80));
+          own_lo[i] |= (uint32_t)v1 << b;
+          k++;
+        }
+      }
+      lds_barrier();
     }
-    own_lo[i] = r1v1[i] | dv1;
   }
 
   // ---- own vote joins round2_votes (engine.rs:540-542); decision (613-628)
@@ -552,8 +607,11 @@ __global__ __launch_bounds__(BLOCK) void ref_step_kernel(StepParams p) {
 #pragma unroll
     for (int pl = 0; pl < kOutPlanes; pl++) store_words<W>(ob + (uint64_t)pl * p.stride, o[pl]);
   }
+  stamp(p, tile, 3, tid);
+  if (p.diag & 2u) return;
   const TileStats ts = thread_stats<W>(o[6], o[7], pend, vm, vq_count, w0, tw0, p);
   finish_tile<true, BLOCK, W>(p, rec, ts, tile, tid, lane, wave);
+  stamp(p, tile, 4, tid);
 }
 
 // ============================================================================
@@ -584,6 +642,7 @@ __global__ __launch_bounds__(BLOCK) void wmvc_step_kernel(StepParams p) {
   Record* rec = p.rec + (p.seq & 1u);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t tile = blockIdx.x;  // no cross-tile dependency: no ticket needed
+  if (!tile_prologue(p, rec, tile, tid)) return;
   const uint32_t tw0 = (uint32_t)tid * W;
   const uint64_t w0 = (uint64_t)tile * BLOCK * W + tw0;
   const bool active = w0 < p.n_words;
@@ -607,9 +666,7 @@ __global__ __launch_bounds__(BLOCK) void wmvc_step_kernel(StepParams p) {
     }
   }
   uint32_t o[kOutPlanes][W];
-  uint32_t pend_w[W], n_coin = 0;
-  unsigned long long cur_blk = ~0ull;
-  uint32_t blk[16];
+  uint32_t pend_w[W], cm[W], n_coin = 0, any_coin = 0;
 #pragma unroll
   for (int i = 0; i < W; i++) {
     const uint32_t vm = valid_mask(w0 + i, p.n_words, p.n_slots);
@@ -649,10 +706,8 @@ __global__ __launch_bounds__(BLOCK) void wmvc_step_kernel(StepParams p) {
     const uint32_t d0 = live & f0, d1 = live & ~f0 & f1;
     const uint32_t open = live & ~f0 & ~f1;
     const uint32_t a1 = open & ~nz0 & nz1;
-    const uint32_t cm = open & ~nz0 & ~nz1 & vm;  // all round-2 votes '?': common coin
-    uint32_t coin = 0;
-    if (cm) coin = coin_word(p.key, p.coin_stream, p.phase, p.slot_base + 32 * (w0 + i), cur_blk, blk);
-    const uint32_t next = d1 | a1 | (cm & coin) | (~live & st_in[i]);
+    cm[i] = open & ~nz0 & ~nz1 & vm;  // all round-2 votes '?': common coin
+    any_coin |= cm[i];
     o[0][i] = (v1 | pend1) & vm;
     o[1][i] = (vq | pend1) & vm;
     o[2][i] = o[0][i];
@@ -660,9 +715,47 @@ __global__ __launch_bounds__(BLOCK) void wmvc_step_kernel(StepParams p) {
     o[4][i] = ~d0 & vm;
     o[5][i] = ~(d0 | d1) & vm;
     o[6][i] = (d0 | d1) & vm;
-    o[7][i] = next & vm;
+    o[7][i] = (d1 | a1 | (~live & st_in[i])) & vm;  // coin bits join below
     pend_w[i] = pend1 & vm;
-    n_coin += __builtin_popcount(cm);
+    n_coin += __builtin_popcount(cm[i]);
+  }
+  // Common coins (coin(p, v), weak_mvc.ivy:173-186): the tile's slots span at most
+  // kRows coin blocks, computed once (one per thread) and staged in LDS.
+  {
+    constexpr int kRows = BLOCK * W * 32 / 512 + 2;
+    static_assert(kRows <= BLOCK, "one coin block per thread");
+    __shared__ uint32_t s_any[BLOCK / 64];
+    __shared__ uint32_t s_coin[kRows][17];
+    const unsigned long long wave_any = __ballot(any_coin != 0);
+    if (lane == 0) s_any[wave] = wave_any != 0;
+    lds_barrier();
+    uint32_t tile_any = 0;
+#pragma unroll
+    for (int w = 0; w < BLOCK / 64; w++) tile_any |= s_any[w];
+    if (tile_any) {
+      const uint64_t tile_w0 = (uint64_t)tile * BLOCK * W;
+      const uint64_t r0 = (p.slot_base + 32 * tile_w0) >> 9;
+      if (tid < kRows) {
+        uint32_t x[16];
+        chacha_block<12>(p.key, ((p.phase - 1) << 40) | (r0 + tid), p.coin_stream, x);
+#pragma unroll
+        for (int j = 0; j < 16; j++) s_coin[tid][j] = x[j];
+      }
+      lds_barrier();
+#pragma unroll
+      for (int i = 0; i < W; i++) {
+        if (cm[i]) {
+          const uint64_t g0 = p.slot_base + 32 * (w0 + i);
+          const uint32_t sh = (uint32_t)(g0 & 31u);
+          uint32_t coin = s_coin[(uint32_t)((g0 >> 9) - r0)][(g0 >> 5) & 15u];
+          if (sh) {
+            const uint64_t g1 = g0 + 32;
+            coin = (coin >> sh) | (s_coin[(uint32_t)((g1 >> 9) - r0)][(g1 >> 5) & 15u] << (32u - sh));
+          }
+          o[7][i] |= cm[i] & coin;
+        }
+      }
+    }
   }
   if (active) {
     uint32_t* ob = p.out + w0;
@@ -675,6 +768,7 @@ __global__ __launch_bounds__(BLOCK) void wmvc_step_kernel(StepParams p) {
     vm_all[i] = valid_mask(w0 + i, p.n_words, p.n_slots);
     dv1[i] = o[6][i] & o[4][i];  // committed with decision code lo bit set = V1
   }
+  if (p.diag & 2u) return;
   const TileStats ts = thread_stats<W>(o[6], dv1, pend_w, vm_all, n_coin, w0, tw0, p);
   finish_tile<false, BLOCK, W>(p, rec, ts, tile, tid, lane, wave);
 }
@@ -809,6 +903,54 @@ __global__ void digest_trace_kernel(int n, uint64_t seed, uint64_t slot_base, ui
     else if ((u & 15u) == 0) d = 0;
     else d = mix64(u) | 1u;
     dg[(uint64_t)j * dstride + s] = d;
+  }
+}
+
+// Diagnostic: the REF kernel's memory pattern with no protocol (reads NIN planes,
+// writes NOUT planes of XOR mixes). The achievable-bandwidth reference for it.
+// T = 0: planar planes `stride` words apart; T > 0: slot-tiled, the planes of a
+// T-word slot tile stored back to back. NT: non-temporal loads/stores.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ uint4 ld4(const uint32_t* p) {
+  u32x4 x;
+  if constexpr (NT) x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  else x = *reinterpret_cast<const u32x4*>(p);
+  return make_uint4(x.x, x.y, x.z, x.w);
+}
+template <bool NT>
+__device__ __forceinline__ void st4(uint32_t* p, uint4 v) {
+  u32x4 x = {v.x, v.y, v.z, v.w};
+  if constexpr (NT) __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(p));
+  else *reinterpret_cast<u32x4*>(p) = x;
+}
+
+template <int NIN, int NOUT, bool NT>
+__global__ __launch_bounds__(256) void stream_probe_kernel(const uint32_t* in, uint32_t* out, uint64_t stride,
+                                                           uint64_t n_words, uint32_t T) {
+  const uint64_t w0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (w0 >= n_words) return;
+  uint64_t ib, ob, ps_in, ps_out;
+  if (T) {
+    ib = (w0 / T) * (uint64_t)(NIN + 1) * T + (w0 % T);
+    ob = (w0 / T) * (uint64_t)NOUT * T + (w0 % T);
+    ps_in = ps_out = T;
+  } else {
+    ib = ob = w0;
+    ps_in = ps_out = stride;
+  }
+  uint4 v[NIN];
+#pragma unroll
+  for (int j = 0; j < NIN; j++) v[j] = ld4<NT>(in + ib + j * ps_in);
+#pragma unroll
+  for (int k = 0; k < NOUT; k++) {
+    uint4 a = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < NIN; j++) {
+      const int r = (j + k) & 31;
+      a.x ^= rotl32(v[j].x, r); a.y ^= rotl32(v[j].y, r); a.z ^= rotl32(v[j].z, r); a.w ^= rotl32(v[j].w, r);
+    }
+    st4<NT>(out + ob + k * ps_out, a);
   }
 }
 

@@ -1,0 +1,98 @@
+"""Where does a REF step's time go? Interleaved A/B timing of ablation variants
+(diagnostic switches in rg_kernels.h) plus per-tile s_memrealtime stamps.
+Run on the GPU box: python tools/ablate.py > gpurun_out/ablate.json"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from rabia_amd import _native as N  # noqa: E402
+from rabia_amd.engine import PhaseEvaluator  # noqa: E402
+
+lib = N.load()
+stream = torch.cuda.Stream()
+torch.cuda.set_stream(stream)
+sp = stream.cuda_stream
+n = 5
+S = int(os.environ.get("ABL_SLOTS", 1 << 26))
+stride_min = ((S + 127) // 128) * 4
+stride_pad = stride_min + 256
+ev = PhaseEvaluator(n, self_lane=4, seed=42)
+bufs = {}
+for name, stride in (("min", stride_min), ("pad", stride_pad)):
+    sets = []
+    for i in range(3):
+        v = torch.empty((4 * n + 1) * stride, dtype=torch.int32, device="cuda")
+        o = torch.empty(8 * stride, dtype=torch.int32, device="cuda")
+        ev.trace_generate_async(N.RG_TRACE_AGREE90, i, 1, S, stride, v.data_ptr(), sp)
+        sets.append((v, o))
+    bufs[name] = (stride, sets)
+torch.cuda.synchronize()
+
+
+def run(variant, k):
+    stride, sets = bufs[variant.get("stride", "min")]
+    v, o = sets[k % 3]
+    slots = variant.get("slots", S)
+    if variant.get("probe"):
+        N.check(lib.rg_debug_stream_probe(v.data_ptr(), o.data_ptr(), (slots + 31) // 32, stride, 0, 0, sp))
+    else:
+        lib.rg_debug_set(ev.ctx, variant.get("diag", 0))
+        ev.phase_step_async(v.data_ptr(), o.data_ptr(), slots, stride, slot_base=1, stream=sp)
+
+
+variants = {
+    "ref": {}, "ref_padstride": {"stride": "pad"}, "ref_mid": {"diag": 2 << 8}, "ref_small": {"diag": 3 << 8}, "no_lookback": {"diag": 1}, "no_finish": {"diag": 2},
+    "no_lookback_no_finish": {"diag": 3}, "probe": {"probe": True}, "probe_padstride": {"probe": True, "stride": "pad"},
+    "ref_1M": {"slots": 1 << 20}, "no_lb_no_fin_1M": {"slots": 1 << 20, "diag": 3}, "probe_1M": {"probe": True, "slots": 1 << 20},
+}
+times = {k: [] for k in variants}
+for r in range(8):
+    for name, var in variants.items():
+        for k in range(3):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            run(var, k)
+            e1.record(stream)
+            e1.synchronize()
+            if r > 0:
+                times[name].append(e0.elapsed_time(e1) * 1000.0)
+summary = {}
+for name, ts in times.items():
+    slots = variants[name].get("slots", S)
+    med = float(np.median(ts))
+    summary[name] = {"median_us": med, "min_us": float(np.min(ts)),
+                     "GBps_at_3.5B": slots * 3.5 / (med * 1e-6) / 1e9}
+
+stamps = {}
+for slots in (S, 1 << 20):
+    lib.rg_debug_set(ev.ctx, 4)
+    stride, sets = bufs["min"]
+    ev.phase_step_async(sets[0][0].data_ptr(), sets[0][1].data_ptr(), slots, stride, slot_base=1, stream=sp)
+    torch.cuda.synchronize()
+    buf = np.zeros(1 << 20, np.uint64)
+    N.check(lib.rg_debug_stamps(ev.ctx, buf.ctypes.data, buf.size), ev.ctx)
+    st = buf.reshape(-1, 8)
+    st = st[st[:, 0] != 0].astype(np.float64) * 10.0 / 1000.0  # 100 MHz ticks -> us
+    t0 = st[:, 0].min()
+    d = {"tiles": int(st.shape[0]),
+         "start_span_us": float(st[:, 0].max() - t0),
+         "end_us": float(st[:, 4][st[:, 4] > 0].max() - t0),
+         "phase_median_us": {"r1_loads+tally+scan": float(np.median(st[:, 1] - st[:, 0])),
+                             "lookback": float(np.median(st[:, 2] - st[:, 1])),
+                             "draws+r2+stores": float(np.median(st[:, 3] - st[:, 2])),
+                             "finish": float(np.median(st[:, 4] - st[:, 3]))},
+         "phase_p90_us": {"r1_loads+tally+scan": float(np.percentile(st[:, 1] - st[:, 0], 90)),
+                          "lookback": float(np.percentile(st[:, 2] - st[:, 1], 90)),
+                          "draws+r2+stores": float(np.percentile(st[:, 3] - st[:, 2], 90)),
+                          "finish": float(np.percentile(st[:, 4] - st[:, 3], 90))},
+         "tile_life_median_us": float(np.median(st[:, 4] - st[:, 0]))}
+    last = st[np.argmax(st[:, 0])]
+    d["last_tile_reduce_us"] = float(last[5] - last[3]) if last[5] > 0 else None
+    stamps[str(slots)] = d
+lib.rg_debug_set(ev.ctx, 0)
+print(json.dumps({"slots": S, "timing": summary, "stamps": stamps}, indent=1))
