@@ -24,9 +24,16 @@
  *   V0 = 0, V1 = 1, VQuestion = 2, 3 = absent voter / None / pending.
  *
  * Layout: bit-sliced planes of 32-bit words; slot s of a
- * window is bit (s % 32) of word (s / 32). A "plane stride" is the distance in
- * words between planes; it must be a multiple of 4 and >= ceil(n_slots/32)
- * (rg_plane_stride() gives the minimum). Plane pointers must be 16-B aligned.
+ * window is bit (s % 32) of word (s / 32). Plane pointers must be 16-B aligned.
+ * Two plane arrangements, chosen per context by rg_config.tile_words:
+ *  - planar (tile_words = 0): plane p starts at p * stride_words; stride_words is
+ *    a multiple of 4 and >= ceil(n_slots/32) (rg_plane_stride() gives the minimum);
+ *  - slot-tiled (tile_words = T, a power of two >= 64): the window is cut into
+ *    slot tiles of 32*T slots; the planes of one tile are stored back to back, so
+ *    word w of plane p is at (w / T) * (P * T) + p * T + (w % T) for a buffer of P
+ *    planes, and a buffer holds ceil(ceil(n_slots/32) / T) * P * T words.
+ *    stride_words arguments must be 0 or T. This is the faster arrangement
+ *    (one contiguous region per tile; tools/probe_layout.py).
  *   votes  = (4n + 1) planes: [0, 2n)   round-1 received votes, lane j at 2j (bit0), 2j+1 (bit1)
  *                             [2n, 4n)  round-2 received votes, same order
  *                             4n        WMVC own state bit (unused in REF mode)
@@ -44,7 +51,7 @@
 extern "C" {
 #endif
 
-#define RG_ABI_VERSION 1
+#define RG_ABI_VERSION 2
 #define RG_MAX_REPLICAS 16
 #define RG_OUT_PLANES 8
 
@@ -82,6 +89,8 @@ typedef struct rg_config {
   uint64_t seed;             /* RabiaConfig.randomization_seed (StdRng)            */
   uint64_t coin_seed;        /* WMVC cluster-wide common-coin seed                 */
   uint64_t epoch;            /* WMVC configuration epoch (coin stream)             */
+  uint32_t tile_words;       /* plane layout: 0 = planar, else slot-tiled (see top) */
+  uint32_t reserved;
 } rg_config;
 
 /* Per-step result (host or device memory). */
@@ -163,7 +172,12 @@ int rg_digest_trace_async(rg_ctx* ctx, uint64_t seed, uint64_t slot_base, uint64
 
 int rg_stream_sync(rg_ctx* ctx, void* stream);
 
-/* Host-side packing helpers (no device work): slot-major codes [S][n] <-> planes. */
+/* Host-side layout helpers (no device work). */
+int rg_planar_to_tiled(const uint32_t* planar, uint32_t n_planes, uint64_t n_words, uint64_t stride,
+                       uint32_t tile_words, uint32_t* tiled);
+int rg_tiled_to_planar(const uint32_t* tiled, uint32_t n_planes, uint64_t n_words, uint32_t tile_words,
+                       uint64_t stride, uint32_t* planar);
+/* Host-side packing helpers (no device work): slot-major codes [S][n] <-> planar planes. */
 int rg_pack_codes(const uint8_t* codes, uint32_t n, uint64_t n_slots, uint64_t stride_words,
                   uint32_t* planes);
 int rg_unpack_planes(const uint32_t* planes, uint32_t n, uint64_t n_slots,

@@ -28,7 +28,7 @@ OUT_PLANES = 8
 class RgConfig(ctypes.Structure):
     _fields_ = [("n_replicas", u32), ("quorum", u32), ("decide_threshold", u32),
                 ("self_lane", i32), ("mode", u32), ("device", i32), ("seed", u64),
-                ("coin_seed", u64), ("epoch", u64)]
+                ("coin_seed", u64), ("epoch", u64), ("tile_words", u32), ("reserved", u32)]
 
 
 RESULT_FIELDS = ["n_slots", "n_decided", "n_v1", "n_pending_r1", "n_draws",
@@ -68,6 +68,8 @@ _SIGS = {
     "rg_stream_sync": (ctypes.c_int, [vp, vp]),
     "rg_pack_codes": (ctypes.c_int, [vp, u32, u64, u64, vp]),
     "rg_unpack_planes": (ctypes.c_int, [vp, u32, u64, u64, vp]),
+    "rg_planar_to_tiled": (ctypes.c_int, [vp, u32, u64, u64, u32, vp]),
+    "rg_tiled_to_planar": (ctypes.c_int, [vp, u32, u64, u32, u64, vp]),
     # diagnostics (include/rabia_gpu_debug.h)
     "rg_debug_set": (ctypes.c_int, [vp, u32]),
     "rg_debug_stamps": (ctypes.c_int, [vp, vp, u64]),

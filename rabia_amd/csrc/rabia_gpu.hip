@@ -62,7 +62,7 @@ int hip_fail(rg_ctx* ctx, hipError_t e, const char* what) {
     if (e_ != hipSuccess) return hip_fail(ctx, e_, #call);  \
   } while (0)
 
-constexpr int wmax_for(int n) { return n <= 6 ? 4 : (n <= 10 ? 2 : 1); }
+constexpr int wmax_for(int n) { return n <= 5 ? 4 : (n <= 10 ? 2 : 1); }
 
 // Tile shapes: {threads, words per thread}. Big tiles keep the per-launch count
 // of tile tickets and look-back hand-offs low on large windows; small tiles fill
@@ -144,6 +144,31 @@ int ensure_tiles(rg_ctx* ctx, uint64_t n_tiles, bool force_zero) {
   return RG_OK;
 }
 
+// Plane addressing for a buffer of `planes` planes in the context's layout and
+// the number of words the buffer must hold for n_words words per plane.
+int make_layout(rg_ctx* ctx, uint32_t planes, uint64_t n_words, uint64_t stride, Layout* lay,
+                uint64_t* words_needed, const char* who) {
+  const uint32_t T = ctx->cfg.tile_words;
+  if (T == 0) {
+    if (stride % 4 || stride < n_words)
+      return fail(ctx, RG_EINVAL, std::string(who) + ": stride_words must be a multiple of 4 and >= ceil(n_slots/32)");
+    lay->tshift = 63;
+    lay->tmask = ~0ull;
+    lay->tile_stride = 0;
+    lay->pstride = stride;
+    *words_needed = (uint64_t)planes * stride;
+  } else {
+    if (stride != 0 && stride != T)
+      return fail(ctx, RG_EINVAL, std::string(who) + ": slot-tiled layout: stride_words must be 0 or tile_words");
+    lay->tshift = (uint32_t)__builtin_ctz(T);
+    lay->tmask = T - 1;
+    lay->tile_stride = (uint64_t)planes * T;
+    lay->pstride = T;
+    *words_needed = ((n_words + T - 1) / T) * (uint64_t)planes * T;
+  }
+  return RG_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -177,6 +202,8 @@ int rg_create(rg_ctx** out, const rg_config* cfg) {
   if (fp1 < 1 || fp1 > n) return fail(nullptr, RG_EINVAL, "rg_create: decide_threshold must be 1..n");
   if (cfg->mode != RG_MODE_REF && cfg->mode != RG_MODE_WMVC)
     return fail(nullptr, RG_EINVAL, "rg_create: unknown mode");
+  if (cfg->tile_words && (cfg->tile_words < 64 || (cfg->tile_words & (cfg->tile_words - 1))))
+    return fail(nullptr, RG_EINVAL, "rg_create: tile_words must be 0 (planar) or a power of two >= 64");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
     return fail(nullptr, RG_ENODEV, "rg_create: no HIP device (the evaluator has no CPU fallback)");
@@ -281,8 +308,6 @@ int rg_phase_step_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_de
   if (!votes_dev || !out_dev) return fail(ctx, RG_EINVAL, "rg_phase_step: null plane pointer");
   if ((reinterpret_cast<uintptr_t>(votes_dev) | reinterpret_cast<uintptr_t>(out_dev)) & 15u)
     return fail(ctx, RG_EINVAL, "rg_phase_step: plane pointers must be 16-byte aligned");
-  if (stride_words % 4 || stride_words < (n_slots + 31) / 32)
-    return fail(ctx, RG_EINVAL, "rg_phase_step: stride_words must be a multiple of 4 and >= ceil(n_slots/32)");
   const bool wmvc = ctx->cfg.mode == RG_MODE_WMVC;
   if (wmvc && (phase < 1 || phase > (1ull << 24)))
     return fail(ctx, RG_EINVAL, "rg_phase_step: WMVC phase must be 1..2^24");
@@ -291,6 +316,10 @@ int rg_phase_step_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_de
   RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
   const int n = (int)ctx->cfg.n_replicas;
   const uint64_t n_words = (n_slots + 31) / 32;
+  Layout lin, lout;
+  uint64_t need_in, need_out;
+  if (int rc = make_layout(ctx, 4 * n + 1, n_words, stride_words, &lin, &need_in, "rg_phase_step")) return rc;
+  if (int rc = make_layout(ctx, kOutPlanes, n_words, stride_words, &lout, &need_out, "rg_phase_step")) return rc;
   const uint32_t force = (ctx->diag >> 8) & 3u;  // diagnostics: force a tile shape
   const int cfg = force ? (int)force - 1 : pick_cfg(n, n_words);
   const uint64_t tile_words = (uint64_t)cfg_block(cfg) * cfg_words(cfg, n);
@@ -309,7 +338,8 @@ int rg_phase_step_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_de
   p.state = ctx->state;
   p.result = ctx->result;
   p.result_user = reinterpret_cast<DevResult*>(result_dev);
-  p.stride = stride_words;
+  p.lin = lin;
+  p.lout = lout;
   p.n_slots = n_slots;
   p.n_words = n_words;
   p.slot_base = slot_base;
@@ -354,11 +384,12 @@ int rg_phase_step(rg_ctx* ctx, const uint32_t* votes_host, uint32_t* out_host, u
                   uint64_t stride_words, uint64_t slot_base, uint64_t phase, uint64_t max_phase,
                   rg_step_result* result_host) {
   if (!ctx || !votes_host || !out_host) return fail(ctx, RG_EINVAL, "rg_phase_step: null argument");
-  if (stride_words % 4 || stride_words < (n_slots + 31) / 32)
-    return fail(ctx, RG_EINVAL, "rg_phase_step: stride_words must be a multiple of 4 and >= ceil(n_slots/32)");
   RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
-  const uint64_t n = ctx->cfg.n_replicas;
-  const uint64_t vw = (4 * n + 1) * stride_words, ow = (uint64_t)kOutPlanes * stride_words;
+  const uint64_t n = ctx->cfg.n_replicas, n_words = (n_slots + 31) / 32;
+  Layout lay;
+  uint64_t vw, ow;
+  if (int rc = make_layout(ctx, (uint32_t)(4 * n + 1), n_words, stride_words, &lay, &vw, "rg_phase_step")) return rc;
+  if (int rc = make_layout(ctx, kOutPlanes, n_words, stride_words, &lay, &ow, "rg_phase_step")) return rc;
   if (vw > ctx->stage_votes_words) {
     RG_HIP(ctx, hipStreamSynchronize(ctx->stream));
     (void)hipFree(ctx->d_votes);
@@ -428,12 +459,15 @@ int rg_trace_generate_async(rg_ctx* ctx, int kind, uint64_t seed, uint64_t slot_
                             uint64_t stride_words, uint32_t* votes_dev, void* stream) {
   if (!ctx || !votes_dev || n_slots == 0) return fail(ctx, RG_EINVAL, "rg_trace_generate: bad argument");
   if (kind < 0 || kind > 2) return fail(ctx, RG_EINVAL, "rg_trace_generate: unknown kind");
-  if (stride_words < (n_slots + 31) / 32) return fail(ctx, RG_EINVAL, "rg_trace_generate: stride too small");
-  RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
   const uint64_t n_words = (n_slots + 31) / 32;
+  Layout lay;
+  uint64_t need;
+  if (int rc = make_layout(ctx, 4 * ctx->cfg.n_replicas + 1, n_words, stride_words, &lay, &need, "rg_trace_generate"))
+    return rc;
+  RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
   hipLaunchKernelGGL(trace_kernel, dim3((uint32_t)((n_words + 127) / 128)), dim3(128), 0,
                      pick_stream(ctx, stream), kind, (int)ctx->cfg.n_replicas, seed, slot_base, n_slots,
-                     stride_words, votes_dev);
+                     lay, votes_dev);
   RG_HIP(ctx, hipGetLastError());
   return RG_OK;
 }
@@ -483,6 +517,34 @@ int rg_unpack_planes(const uint32_t* planes, uint32_t n, uint64_t n_slots, uint6
       codes[s * n + j] = (uint8_t)(lo | (hi << 1));
     }
   }
+  return RG_OK;
+}
+
+int rg_planar_to_tiled(const uint32_t* planar, uint32_t n_planes, uint64_t n_words, uint64_t stride,
+                       uint32_t tile_words, uint32_t* tiled) {
+  if (!planar || !tiled || !n_planes || stride < n_words || tile_words < 64 || (tile_words & (tile_words - 1)))
+    return fail(nullptr, RG_EINVAL, "rg_planar_to_tiled: bad argument");
+  const uint64_t T = tile_words, n_t = (n_words + T - 1) / T;
+  std::memset(tiled, 0, sizeof(uint32_t) * n_t * n_planes * T);
+  for (uint64_t t = 0; t < n_t; t++)
+    for (uint32_t pl = 0; pl < n_planes; pl++) {
+      const uint64_t w_lo = t * T, cnt = (w_lo + T <= n_words) ? T : n_words - w_lo;
+      std::memcpy(tiled + (t * n_planes + pl) * T, planar + pl * stride + w_lo, cnt * 4);
+    }
+  return RG_OK;
+}
+
+int rg_tiled_to_planar(const uint32_t* tiled, uint32_t n_planes, uint64_t n_words, uint32_t tile_words,
+                       uint64_t stride, uint32_t* planar) {
+  if (!planar || !tiled || !n_planes || stride < n_words || tile_words < 64 || (tile_words & (tile_words - 1)))
+    return fail(nullptr, RG_EINVAL, "rg_tiled_to_planar: bad argument");
+  const uint64_t T = tile_words, n_t = (n_words + T - 1) / T;
+  std::memset(planar, 0, sizeof(uint32_t) * n_planes * stride);
+  for (uint64_t t = 0; t < n_t; t++)
+    for (uint32_t pl = 0; pl < n_planes; pl++) {
+      const uint64_t w_lo = t * T, cnt = (w_lo + T <= n_words) ? T : n_words - w_lo;
+      std::memcpy(planar + pl * stride + w_lo, tiled + (t * n_planes + pl) * T, cnt * 4);
+    }
   return RG_OK;
 }
 

@@ -16,16 +16,27 @@
 
 namespace rg {
 
+// Plane addressing: word w of plane pl of a buffer lives at
+//   (w >> tshift) * tile_stride + pl * pstride + (w & tmask)
+// planar      : tshift 63, tmask ~0, tile_stride 0, pstride = stride
+// slot-tiled T: tshift log2 T, tmask T-1, tile_stride = planes * T, pstride = T
+// (the planes of one T-word slot tile are stored back to back).
+struct Layout {
+  uint32_t tshift;
+  uint64_t tmask, tile_stride, pstride;
+  RG_HD uint64_t base(uint64_t w) const { return (w >> tshift) * tile_stride + (w & tmask); }
+};
+
 struct StepParams {
-  const uint32_t* votes;          // [4N+1][stride]
+  const uint32_t* votes;          // 4N+1 planes (layout lin)
   unsigned long long* stats;      // [n_tiles][kStatGranules] tagged granules
-  uint32_t* out;                  // [8][stride]
+  uint32_t* out;                  // 8 planes (layout lout)
   unsigned long long* lookback;   // [n_tiles] {tag:32 | value:32} granules
   Record* rec;                    // ring of 2
   DevState* state;
   DevResult* result;              // ctx-internal, always written
   DevResult* result_user;         // optional copy
-  uint64_t stride;
+  Layout lin, lout;
   uint64_t n_slots;
   uint64_t n_words;
   uint64_t slot_base;
@@ -99,17 +110,35 @@ RG_HD uint32_t ctr_at(const Ctr<B>& c, int bit) {
   return v;
 }
 
+// Per-slot masks of (a > b) and (a < b) for two bit-sliced counters.
+template <int B>
+RG_HD void ctr_cmp(const Ctr<B>& a, const Ctr<B>& b, uint32_t& gt, uint32_t& lt) {
+  uint32_t eq = ~0u;
+  gt = lt = 0;
+#pragma unroll
+  for (int i = B - 1; i >= 0; i--) {
+    gt |= eq & a.b[i] & ~b.b[i];
+    lt |= eq & ~a.b[i] & b.b[i];
+    eq &= ~(a.b[i] ^ b.b[i]);
+  }
+}
+
 // ---- vector plane access ----------------------------------------------------
+// Vote planes are read exactly once: non-temporal loads (measured +5-15 % on
+// this pattern, tools/probe_layout.py).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
 template <int W>
 __device__ __forceinline__ void load_words(const uint32_t* p, uint32_t (&v)[W]) {
   if constexpr (W == 4) {
-    uint4 x = *reinterpret_cast<const uint4*>(p);
+    const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
     v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
   } else if constexpr (W == 2) {
-    uint2 x = *reinterpret_cast<const uint2*>(p);
+    const u32x2 x = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(p));
     v[0] = x.x; v[1] = x.y;
   } else {
-    v[0] = *p;
+    v[0] = __builtin_nontemporal_load(p);
   }
 }
 
@@ -441,8 +470,11 @@ __device__ __forceinline__ TileStats thread_stats(const uint32_t (&committed)[W]
 // ============================================================================
 // REF phase step: engine.rs:483-682 on the final vote sets of every slot.
 // ============================================================================
+// Occupancy: 4 waves per SIMD (<= 128 VGPRs) so that at least two 512-thread or
+// four 256-thread tiles are resident per CU and one tile's look-back / stores
+// overlap another's loads.
 template <int N, int W, int BLOCK>
-__global__ __launch_bounds__(BLOCK) void ref_step_kernel(StepParams p) {
+__global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
   constexpr int B = ctr_bits(N);
   constexpr int WAVES = BLOCK / 64;
   __shared__ uint32_t s_ticket;
@@ -462,16 +494,17 @@ __global__ __launch_bounds__(BLOCK) void ref_step_kernel(StepParams p) {
   // Issue every plane load up front (R2 stays in flight across the look-back).
   uint32_t r1lo[N][W], r1hi[N][W], r2lo[N][W], r2hi[N][W];
   if (active) {
-    const uint32_t* base = p.votes + w0;
+    const uint32_t* base = p.votes + p.lin.base(w0);
+    const uint64_t ps = p.lin.pstride;
 #pragma unroll
     for (int j = 0; j < N; j++) {
-      load_words<W>(base + (uint64_t)(2 * j) * p.stride, r1lo[j]);
-      load_words<W>(base + (uint64_t)(2 * j + 1) * p.stride, r1hi[j]);
+      load_words<W>(base + (2 * j) * ps, r1lo[j]);
+      load_words<W>(base + (2 * j + 1) * ps, r1hi[j]);
     }
 #pragma unroll
     for (int j = 0; j < N; j++) {
-      load_words<W>(base + (uint64_t)(2 * N + 2 * j) * p.stride, r2lo[j]);
-      load_words<W>(base + (uint64_t)(2 * N + 2 * j + 1) * p.stride, r2hi[j]);
+      load_words<W>(base + (2 * N + 2 * j) * ps, r2lo[j]);
+      load_words<W>(base + (2 * N + 2 * j + 1) * ps, r2hi[j]);
     }
   } else {
 #pragma unroll
@@ -483,26 +516,27 @@ __global__ __launch_bounds__(BLOCK) void ref_step_kernel(StepParams p) {
 #pragma unroll
   for (int i = 0; i < W; i++) vm[i] = valid_mask(w0 + i, p.n_words, p.n_slots);
 
-  // ---- round 1: count_votes + |votes| >= quorum fallback (engine.rs:495-505)
-  uint32_t r1v1[W], r1vq[W], pend[W];
-  Ctr<B> c0s[W], c1s[W];
+  // ---- round 1: count_votes + |votes| >= quorum fallback (engine.rs:495-505).
+  // Only what the draws need survives the tally: per-slot (c1 > c0), (c1 < c0).
+  uint32_t r1v1[W], r1vq[W], pend[W], c1gt[W], c1lt[W];
   uint32_t vq_count = 0;
 #pragma unroll
   for (int i = 0; i < W; i++) {
-    Ctr<B> cp;
-    ctr_zero(c0s[i]); ctr_zero(c1s[i]); ctr_zero(cp);
+    Ctr<B> c0, c1, cp;
+    ctr_zero(c0); ctr_zero(c1); ctr_zero(cp);
 #pragma unroll
     for (int j = 0; j < N; j++) {
       const uint32_t lo = r1lo[j][i], hi = r1hi[j][i];
-      ctr_add(c0s[i], ~lo & ~hi);
-      ctr_add(c1s[i], lo & ~hi);
+      ctr_add(c0, ~lo & ~hi);
+      ctr_add(c1, lo & ~hi);
       ctr_add(cp, ~(lo & hi));
     }
-    const uint32_t g0 = ctr_ge(c0s[i], p.q), g1 = ctr_ge(c1s[i], p.q), gp = ctr_ge(cp, p.q);
+    const uint32_t g0 = ctr_ge(c0, p.q), g1 = ctr_ge(c1, p.q), gp = ctr_ge(cp, p.q);
     const uint32_t v0 = g0 & vm[i];
     r1v1[i] = ~g0 & g1 & vm[i];
     r1vq[i] = ~g0 & ~g1 & gp & vm[i];  // cq >= q implies present >= q
     pend[i] = ~(v0 | r1v1[i] | r1vq[i]) & vm[i];
+    ctr_cmp(c1, c0, c1gt[i], c1lt[i]);
     vq_count += __builtin_popcount(r1vq[i]);
   }
 
@@ -556,8 +590,8 @@ __global__ __launch_bounds__(BLOCK) void ref_step_kernel(StepParams p) {
           const uint32_t row = (uint32_t)((k >> 3) - cb), ws = (uint32_t)(k & 7u) * 2u;
           const unsigned long long u =
               (unsigned long long)s_blk[row][ws] | ((unsigned long long)s_blk[row][ws + 1] << 32);
-          const uint32_t c0 = ctr_at(c0s[i], b), c1 = ctr_at(c1s[i], b);
-          const bool v1 = c1 > c0 ? (u < kP90) : (c1 < c0 ? (u >= kP90) : (u < kP80));
+          const bool gt = (c1gt[i] >> b) & 1u, lt = (c1lt[i] >> b) & 1u;
+          const bool v1 = gt ? (u < kP90) : (lt ? (u >= kP90) : (u < kP80));
           own_lo[i] |= (uint32_t)v1 << b;
           k++;
         }
@@ -603,9 +637,9 @@ __global__ __launch_bounds__(BLOCK) void ref_step_kernel(StepParams p) {
     o[7][i] = d1 & vm[i];          // V1: apply_batch + commit_phase
   }
   if (active) {
-    uint32_t* ob = p.out + w0;
+    uint32_t* ob = p.out + p.lout.base(w0);
 #pragma unroll
-    for (int pl = 0; pl < kOutPlanes; pl++) store_words<W>(ob + (uint64_t)pl * p.stride, o[pl]);
+    for (int pl = 0; pl < kOutPlanes; pl++) store_words<W>(ob + pl * p.lout.pstride, o[pl]);
   }
   stamp(p, tile, 3, tid);
   if (p.diag & 2u) return;
@@ -637,7 +671,7 @@ __device__ __forceinline__ uint32_t coin_word(const Key& key, uint64_t stream, u
 }
 
 template <int N, int W, int BLOCK>
-__global__ __launch_bounds__(BLOCK) void wmvc_step_kernel(StepParams p) {
+__global__ __launch_bounds__(BLOCK, 4) void wmvc_step_kernel(StepParams p) {
   constexpr int B = ctr_bits(N);
   Record* rec = p.rec + (p.seq & 1u);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -648,15 +682,16 @@ __global__ __launch_bounds__(BLOCK) void wmvc_step_kernel(StepParams p) {
   const bool active = w0 < p.n_words;
   uint32_t r1lo[N][W], r1hi[N][W], r2lo[N][W], r2hi[N][W], st_in[W];
   if (active) {
-    const uint32_t* base = p.votes + w0;
+    const uint32_t* base = p.votes + p.lin.base(w0);
+    const uint64_t ps = p.lin.pstride;
 #pragma unroll
     for (int j = 0; j < N; j++) {
-      load_words<W>(base + (uint64_t)(2 * j) * p.stride, r1lo[j]);
-      load_words<W>(base + (uint64_t)(2 * j + 1) * p.stride, r1hi[j]);
-      load_words<W>(base + (uint64_t)(2 * N + 2 * j) * p.stride, r2lo[j]);
-      load_words<W>(base + (uint64_t)(2 * N + 2 * j + 1) * p.stride, r2hi[j]);
+      load_words<W>(base + (2 * j) * ps, r1lo[j]);
+      load_words<W>(base + (2 * j + 1) * ps, r1hi[j]);
+      load_words<W>(base + (2 * N + 2 * j) * ps, r2lo[j]);
+      load_words<W>(base + (2 * N + 2 * j + 1) * ps, r2hi[j]);
     }
-    load_words<W>(base + (uint64_t)(4 * N) * p.stride, st_in);
+    load_words<W>(base + (4 * N) * ps, st_in);
   } else {
 #pragma unroll
     for (int i = 0; i < W; i++) {
@@ -758,9 +793,9 @@ __global__ __launch_bounds__(BLOCK) void wmvc_step_kernel(StepParams p) {
     }
   }
   if (active) {
-    uint32_t* ob = p.out + w0;
+    uint32_t* ob = p.out + p.lout.base(w0);
 #pragma unroll
-    for (int pl = 0; pl < kOutPlanes; pl++) store_words<W>(ob + (uint64_t)pl * p.stride, o[pl]);
+    for (int pl = 0; pl < kOutPlanes; pl++) store_words<W>(ob + pl * p.lout.pstride, o[pl]);
   }
   uint32_t vm_all[W], dv1[W];
 #pragma unroll
@@ -831,7 +866,7 @@ __global__ void draws_kernel(Key key, uint64_t first, uint64_t count, unsigned l
 
 // Synthetic traces, one thread per 32-slot word (restated in oracle/rabia_oracle.c:or_trace).
 __global__ void trace_kernel(int kind, int n, uint64_t seed, uint64_t slot_base, uint64_t n_slots,
-                             uint64_t stride, uint32_t* planes) {
+                             Layout lay, uint32_t* planes) {
   const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t n_words = (n_slots + 31) / 32;
   if (w >= n_words) return;
@@ -884,10 +919,10 @@ __global__ void trace_kernel(int kind, int n, uint64_t seed, uint64_t slot_base,
 #pragma unroll
     for (int j = 0; j < kMaxReplicas; j++) {
       if (j >= n) continue;
-      planes[(uint64_t)(2 * n * r + 2 * j) * stride + w] = lo[r][j];
-      planes[(uint64_t)(2 * n * r + 2 * j + 1) * stride + w] = hi[r][j];
+      planes[lay.base(w) + (uint64_t)(2 * n * r + 2 * j) * lay.pstride] = lo[r][j];
+      planes[lay.base(w) + (uint64_t)(2 * n * r + 2 * j + 1) * lay.pstride] = hi[r][j];
     }
-  planes[(uint64_t)(4 * n) * stride + w] = stw;
+  planes[lay.base(w) + (uint64_t)(4 * n) * lay.pstride] = stw;
 }
 
 __global__ void digest_trace_kernel(int n, uint64_t seed, uint64_t slot_base, uint64_t n_slots,
@@ -910,7 +945,6 @@ __global__ void digest_trace_kernel(int n, uint64_t seed, uint64_t slot_base, ui
 // writes NOUT planes of XOR mixes). The achievable-bandwidth reference for it.
 // T = 0: planar planes `stride` words apart; T > 0: slot-tiled, the planes of a
 // T-word slot tile stored back to back. NT: non-temporal loads/stores.
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 template <bool NT>
 __device__ __forceinline__ uint4 ld4(const uint32_t* p) {
   u32x4 x;

@@ -73,6 +73,24 @@ def decode_outputs(out: np.ndarray, n_slots: int) -> dict:
     }
 
 
+def to_tiled(planar: np.ndarray, n_words: int, tile_words: int) -> np.ndarray:
+    """Planar planes [P][stride] -> slot-tiled buffer (include/rabia_gpu.h layout)."""
+    planar = np.ascontiguousarray(planar, np.uint32)
+    P, stride = planar.shape
+    tiles = (n_words + tile_words - 1) // tile_words
+    out = np.zeros(tiles * P * tile_words, np.uint32)
+    N.check(N.load().rg_planar_to_tiled(planar.ctypes.data, P, n_words, stride, tile_words, out.ctypes.data))
+    return out
+
+
+def from_tiled(tiled: np.ndarray, n_planes: int, n_words: int, tile_words: int, stride: int) -> np.ndarray:
+    tiled = np.ascontiguousarray(tiled, np.uint32)
+    out = np.zeros((n_planes, stride), np.uint32)
+    N.check(N.load().rg_tiled_to_planar(tiled.ctypes.data, n_planes, n_words, tile_words, stride,
+                                        out.ctypes.data))
+    return out
+
+
 class PhaseWindow:
     """A window of `n_slots` consecutive phases' vote sets, packed as the device
     layout: (4n+1) planes of uint32 words (R1 lanes, R2 lanes, own state)."""
@@ -149,7 +167,7 @@ class PhaseEvaluator:
 
     def __init__(self, n_replicas: int, *, quorum: int = 0, decide_threshold: int = 0,
                  self_lane: int = -1, mode: str = "ref", seed: int = 0, coin_seed=None,
-                 epoch: int = 0, device: int = 0):
+                 epoch: int = 0, device: int = 0, tile_words: int = 0):
         self.lib = N.load()
         self.n = int(n_replicas)
         self.mode = mode
@@ -157,7 +175,7 @@ class PhaseEvaluator:
                          self_lane=self_lane, mode=N.RG_MODE_WMVC if mode == "wmvc" else N.RG_MODE_REF,
                          device=device, seed=seed & (2 ** 64 - 1),
                          coin_seed=(seed if coin_seed is None else coin_seed) & (2 ** 64 - 1),
-                         epoch=epoch)
+                         epoch=epoch, tile_words=tile_words)
         ctx = ctypes.c_void_p()
         N.check(self.lib.rg_create(ctypes.byref(ctx), ctypes.byref(cfg)))
         self.ctx = ctx
@@ -165,6 +183,7 @@ class PhaseEvaluator:
         N.check(self.lib.rg_get_config(self.ctx, ctypes.byref(got)), self.ctx)
         self.quorum = got.quorum
         self.decide_threshold = got.decide_threshold
+        self.tile_words = got.tile_words
 
     @classmethod
     def from_configs(cls, cluster: ClusterConfig, seed: int, mode: str = "ref", **kw):
@@ -212,10 +231,19 @@ class PhaseEvaluator:
         out = np.zeros((N.OUT_PLANES, window.stride), np.uint32)
         votes = np.ascontiguousarray(window.planes)
         r = N.RgStepResult()
-        N.check(self.lib.rg_phase_step(self.ctx, votes.ctypes.data, out.ctypes.data, window.n_slots,
-                                       window.stride, window.slot_base, phase, max_phase,
-                                       ctypes.byref(r)), self.ctx)
-        return out, r.as_dict()
+        if not self.tile_words:
+            N.check(self.lib.rg_phase_step(self.ctx, votes.ctypes.data, out.ctypes.data, window.n_slots,
+                                           window.stride, window.slot_base, phase, max_phase,
+                                           ctypes.byref(r)), self.ctx)
+            return out, r.as_dict()
+        T = self.tile_words
+        nw = (window.n_slots + 31) // 32
+        tiles = (nw + T - 1) // T
+        tv = to_tiled(votes, nw, T)
+        to = np.zeros(tiles * N.OUT_PLANES * T, np.uint32)
+        N.check(self.lib.rg_phase_step(self.ctx, tv.ctypes.data, to.ctypes.data, window.n_slots, T,
+                                       window.slot_base, phase, max_phase, ctypes.byref(r)), self.ctx)
+        return from_tiled(to, N.OUT_PLANES, nw, T, window.stride), r.as_dict()
 
     def phase_step_async(self, votes_ptr: int, out_ptr: int, n_slots: int, stride: int,
                          slot_base: int = 1, phase: int = 1, max_phase: int = 0,

@@ -16,7 +16,7 @@ def test_header_symbols_exported():
     for s in syms:
         assert hasattr(lib, s), f"librabia_gpu.so does not export {s}"
         assert s in N._SIGS, f"binding lacks a signature for {s}"
-    assert lib.rg_abi_version() == 1
+    assert lib.rg_abi_version() == 2
 
 
 def test_plane_stride():
@@ -97,3 +97,19 @@ def test_create_without_device_fails_loudly():
     assert rc in (N.RG_ENODEV, N.RG_EHIP)
     assert not ctx.value
     assert lib.rg_last_error(None)
+
+
+@pytest.mark.parametrize("P,nw,T", [(21, 1, 64), (21, 1000, 64), (8, 4096, 1024), (3, 5000, 2048)])
+def test_tiled_layout_roundtrip(P, nw, T):
+    """Slot-tiled arrangement: word w of plane p at (w//T)*P*T + p*T + w%T."""
+    from rabia_amd.engine import to_tiled, from_tiled
+    stride = ((nw + 3) // 4) * 4
+    rng = np.random.default_rng(P * nw)
+    planar = rng.integers(0, 2 ** 32, (P, stride), dtype=np.uint64).astype(np.uint32)
+    planar[:, nw:] = 0
+    tiled = to_tiled(planar, nw, T)
+    assert tiled.size == ((nw + T - 1) // T) * P * T
+    for w in (0, nw // 2, nw - 1):
+        for p_ in (0, P - 1):
+            assert tiled[(w // T) * P * T + p_ * T + w % T] == planar[p_, w]
+    np.testing.assert_array_equal(from_tiled(tiled, P, nw, T, stride), planar)

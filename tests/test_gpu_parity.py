@@ -310,3 +310,35 @@ def test_state_resume_roundtrip(oracle):
         np.testing.assert_array_equal(got[k], exp[k][2500:], err_msg=k)
     assert res["rng_next"] == eres["rng_next"]
     assert res["last_committed_max"] == eres["last_committed_max"]
+
+
+@pytest.mark.parametrize("T", [64, 1024, 4096])
+@pytest.mark.parametrize("mode", ["ref", "wmvc"])
+def test_slot_tiled_layout(oracle, T, mode):
+    """The slot-tiled plane arrangement gives bit-identical results."""
+    n, S = 5, 300_007
+    r1, r2, st = oracle.trace(0, n, T, 1, S)
+    if mode == "ref":
+        exp, eres = oracle.ref_step(n, 3, 4, 42, 7, 1, r1, r2)
+    else:
+        exp, eres = oracle.wmvc_step(n, 3, 3, 4, 42, 2, 3, 1, r1, r2, st)
+    with PhaseEvaluator(n, self_lane=4, seed=42, mode=mode, coin_seed=42, epoch=2, tile_words=T) as ev:
+        ev.set_state(rng_next=7 if mode == "ref" else 0)
+        out, res = ev.phase_step_host(PhaseWindow.from_codes(r1, r2, st, slot_base=1), phase=3)
+    assert_same(decode_outputs(out, S), exp, res, eres)
+
+
+def test_device_tiled_generator_matches_planar(oracle):
+    """Device trace generator writing the tiled arrangement == planar arrangement."""
+    torch = torch_cuda()
+    from rabia_amd.engine import from_tiled
+    n, S, T = 5, 1 << 20, 1024
+    nw = S // 32
+    vt = torch.zeros(((nw + T - 1) // T) * (4 * n + 1) * T, dtype=torch.int32, device="cuda")
+    with PhaseEvaluator(n, tile_words=T) as ev:
+        ev.trace_generate_async(1, 5, 1, S, T, vt.data_ptr())
+        ev.sync()
+    planar = from_tiled(vt.cpu().numpy().view(np.uint32), 4 * n + 1, nw, T, nw)
+    r1, r2, st = oracle.trace(1, n, 5, 1, S)
+    np.testing.assert_array_equal(planar[: 2 * n], oracle.pack_planes(r1, nw))
+    np.testing.assert_array_equal(planar[2 * n: 4 * n], oracle.pack_planes(r2, nw))

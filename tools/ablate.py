@@ -22,6 +22,15 @@ S = int(os.environ.get("ABL_SLOTS", 1 << 26))
 stride_min = ((S + 127) // 128) * 4
 stride_pad = stride_min + 256
 ev = PhaseEvaluator(n, self_lane=4, seed=42)
+T = 1024
+ev_t = PhaseEvaluator(n, self_lane=4, seed=42, tile_words=T)
+nw = S // 32
+tiled_sets = []
+for i in range(3):
+    v = torch.empty(((nw + T - 1) // T) * (4 * n + 1) * T, dtype=torch.int32, device="cuda")
+    o = torch.empty(((nw + T - 1) // T) * 8 * T, dtype=torch.int32, device="cuda")
+    ev_t.trace_generate_async(N.RG_TRACE_AGREE90, i, 1, S, T, v.data_ptr(), sp)
+    tiled_sets.append((v, o))
 bufs = {}
 for name, stride in (("min", stride_min), ("pad", stride_pad)):
     sets = []
@@ -35,6 +44,11 @@ torch.cuda.synchronize()
 
 
 def run(variant, k):
+    if variant.get("tiled"):
+        v, o = tiled_sets[k % 3]
+        lib.rg_debug_set(ev_t.ctx, variant.get("diag", 0))
+        ev_t.phase_step_async(v.data_ptr(), o.data_ptr(), variant.get("slots", S), T, slot_base=1, stream=sp)
+        return
     stride, sets = bufs[variant.get("stride", "min")]
     v, o = sets[k % 3]
     slots = variant.get("slots", S)
@@ -46,7 +60,9 @@ def run(variant, k):
 
 
 variants = {
-    "ref": {}, "ref_padstride": {"stride": "pad"}, "ref_mid": {"diag": 2 << 8}, "ref_small": {"diag": 3 << 8}, "no_lookback": {"diag": 1}, "no_finish": {"diag": 2},
+    "ref": {}, "ref_padstride": {"stride": "pad"}, "ref_mid": {"diag": 2 << 8},
+    "tiled1024": {"tiled": True}, "tiled1024_mid": {"tiled": True, "diag": 2 << 8},
+    "tiled1024_nolb_nofin": {"tiled": True, "diag": 3}, "tiled1024_1M": {"tiled": True, "slots": 1 << 20}, "no_lookback": {"diag": 1}, "no_finish": {"diag": 2},
     "no_lookback_no_finish": {"diag": 3}, "probe": {"probe": True}, "probe_padstride": {"probe": True, "stride": "pad"},
     "ref_1M": {"slots": 1 << 20}, "no_lb_no_fin_1M": {"slots": 1 << 20, "diag": 3}, "probe_1M": {"probe": True, "slots": 1 << 20},
 }
@@ -70,12 +86,13 @@ for name, ts in times.items():
 
 stamps = {}
 for slots in (S, 1 << 20):
-    lib.rg_debug_set(ev.ctx, 4)
-    stride, sets = bufs["min"]
-    ev.phase_step_async(sets[0][0].data_ptr(), sets[0][1].data_ptr(), slots, stride, slot_base=1, stream=sp)
+    lib.rg_debug_set(ev_t.ctx, 4)
+    v, o = tiled_sets[0]
+    ev_t.phase_step_async(v.data_ptr(), o.data_ptr(), slots, T, slot_base=1, stream=sp)
     torch.cuda.synchronize()
     buf = np.zeros(1 << 20, np.uint64)
-    N.check(lib.rg_debug_stamps(ev.ctx, buf.ctypes.data, buf.size), ev.ctx)
+    N.check(lib.rg_debug_stamps(ev_t.ctx, buf.ctypes.data, buf.size), ev_t.ctx)
+    ntl = int(np.count_nonzero(buf.reshape(-1, 8)[:, 0]))
     st = buf.reshape(-1, 8)
     st = st[st[:, 0] != 0].astype(np.float64) * 10.0 / 1000.0  # 100 MHz ticks -> us
     t0 = st[:, 0].min()
@@ -95,4 +112,5 @@ for slots in (S, 1 << 20):
     d["last_tile_reduce_us"] = float(last[5] - last[3]) if last[5] > 0 else None
     stamps[str(slots)] = d
 lib.rg_debug_set(ev.ctx, 0)
+lib.rg_debug_set(ev_t.ctx, 0)
 print(json.dumps({"slots": S, "timing": summary, "stamps": stamps}, indent=1))
