@@ -224,6 +224,7 @@ __device__ __forceinline__ void lds_barrier() {
 __device__ __forceinline__ uint32_t lookback_exclusive(unsigned long long* status, uint32_t tile,
                                                        uint32_t seq, uint32_t agg, int lane,
                                                        unsigned long long* err) {
+  constexpr int G = 4;  // granules per lane per poll: a 256-tile window per round trip
   const uint32_t tag_agg = seq << 1, tag_inc = (seq << 1) | 1u;
   if (tile == 0) {
     if (lane == 0) atomic_store_agent(status, ((unsigned long long)tag_inc << 32) | agg);
@@ -234,17 +235,32 @@ __device__ __forceinline__ uint32_t lookback_exclusive(unsigned long long* statu
   int64_t pos = (int64_t)tile - 1;
   uint32_t spins = 0;
   for (;;) {
-    const int64_t pidx = pos - lane;
-    unsigned long long g = pidx >= 0 ? atomic_load_agent(status + pidx)
-                                     : ((unsigned long long)tag_inc << 32);
-    const uint32_t tag = (uint32_t)(g >> 32);
-    const bool ready = (tag >> 1) == seq;
-    const bool incl = ready && (tag & 1u);
-    const unsigned long long incl_mask = __ballot(incl);
-    const unsigned long long notready = __ballot(!ready);
-    const int first = incl_mask ? __builtin_ctzll(incl_mask) : 64;
-    const unsigned long long need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);
-    if (notready & need) {
+    unsigned long long g[G];
+#pragma unroll
+    for (int k = 0; k < G; k++) {  // all G loads in flight together; distance order k-major
+      const int64_t pidx = pos - (64 * k + lane);
+      g[k] = pidx >= 0 ? atomic_load_agent(status + pidx) : ((unsigned long long)tag_inc << 32);
+    }
+    int consumed = 0;  // groups fully summed this round
+    bool found = false;
+#pragma unroll
+    for (int k = 0; k < G; k++) {
+      if (found || consumed < k) break;  // uniform
+      const uint32_t tag = (uint32_t)(g[k] >> 32);
+      const bool ready = (tag >> 1) == seq;
+      const bool incl = ready && (tag & 1u);
+      const unsigned long long incl_mask = __ballot(incl);
+      const unsigned long long notready = __ballot(!ready);
+      const int first = incl_mask ? __builtin_ctzll(incl_mask) : 64;
+      const unsigned long long need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);
+      if (notready & need) break;  // a needed predecessor has not published yet
+      excl += (uint32_t)wave_sum64((lane <= first) ? (uint32_t)g[k] : 0u);
+      consumed = k + 1;
+      found = first < 64;
+    }
+    if (found) break;
+    pos -= 64 * consumed;
+    if (consumed < G) {
       if (++spins > (1u << 22)) {  // ~seconds: a protocol fault, not a wait
         if (lane == 0) {
           atomicOr(err, 1ull);
@@ -253,12 +269,7 @@ __device__ __forceinline__ uint32_t lookback_exclusive(unsigned long long* statu
         break;
       }
       __builtin_amdgcn_s_sleep(1);
-      continue;
     }
-    const uint32_t v = (lane <= first) ? (uint32_t)g : 0u;
-    excl += (uint32_t)wave_sum64(v);
-    if (first < 64) break;
-    pos -= 64;
   }
   if (lane == 0)
     atomic_store_agent(status + tile, ((unsigned long long)tag_inc << 32) | (agg + excl));
@@ -470,48 +481,54 @@ __device__ __forceinline__ TileStats thread_stats(const uint32_t (&committed)[W]
 // ============================================================================
 // REF phase step: engine.rs:483-682 on the final vote sets of every slot.
 // ============================================================================
-// Occupancy: 4 waves per SIMD (<= 128 VGPRs) so that at least two 512-thread or
-// four 256-thread tiles are resident per CU and one tile's look-back / stores
-// overlap another's loads.
-template <int N, int W, int BLOCK>
-__global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
-  constexpr int B = ctr_bits(N);
-  constexpr int WAVES = BLOCK / 64;
-  __shared__ uint32_t s_ticket;
-  __shared__ uint32_t s_wave[WAVES];
-  __shared__ uint32_t s_excl;
-  Record* rec = p.rec + (p.seq & 1u);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid == 0) s_ticket = (uint32_t)atomicAdd(&rec->ticket.v, 1ull);
-  lds_barrier();
-  const uint32_t tile = s_ticket;
-  if (!tile_prologue(p, rec, tile, tid)) return;
-  stamp(p, tile, 0, tid);
-  const uint32_t tw0 = (uint32_t)tid * W;  // word offset inside the tile
-  const uint64_t w0 = (uint64_t)tile * BLOCK * W + tw0;
-  const bool active = w0 < p.n_words;
-
-  // Issue every plane load up front (R2 stays in flight across the look-back).
+// One REF tile's register-resident inputs: round-1 and round-2 vote planes.
+template <int N, int W>
+struct RefTileIn {
   uint32_t r1lo[N][W], r1hi[N][W], r2lo[N][W], r2hi[N][W];
-  if (active) {
+};
+
+template <int N, int W, int BLOCK>
+__device__ __forceinline__ void ref_load_tile(const StepParams& p, uint32_t tile, int tid, RefTileIn<N, W>& in) {
+  const uint64_t w0 = (uint64_t)tile * BLOCK * W + (uint64_t)tid * W;
+  if (w0 < p.n_words) {
     const uint32_t* base = p.votes + p.lin.base(w0);
     const uint64_t ps = p.lin.pstride;
 #pragma unroll
     for (int j = 0; j < N; j++) {
-      load_words<W>(base + (2 * j) * ps, r1lo[j]);
-      load_words<W>(base + (2 * j + 1) * ps, r1hi[j]);
+      load_words<W>(base + (2 * j) * ps, in.r1lo[j]);
+      load_words<W>(base + (2 * j + 1) * ps, in.r1hi[j]);
     }
 #pragma unroll
     for (int j = 0; j < N; j++) {
-      load_words<W>(base + (2 * N + 2 * j) * ps, r2lo[j]);
-      load_words<W>(base + (2 * N + 2 * j + 1) * ps, r2hi[j]);
+      load_words<W>(base + (2 * N + 2 * j) * ps, in.r2lo[j]);
+      load_words<W>(base + (2 * N + 2 * j + 1) * ps, in.r2hi[j]);
     }
   } else {
 #pragma unroll
     for (int j = 0; j < N; j++)
 #pragma unroll
-      for (int i = 0; i < W; i++) r1lo[j][i] = r1hi[j][i] = r2lo[j][i] = r2hi[j][i] = ~0u;
+      for (int i = 0; i < W; i++) in.r1lo[j][i] = in.r1hi[j][i] = in.r2lo[j][i] = in.r2hi[j][i] = ~0u;
   }
+}
+
+// REF phase step of one tile (engine.rs:483-682 on the final vote sets of each
+// slot), inputs already in registers (or in flight).
+template <int N, int W, int BLOCK>
+__device__ __forceinline__ void ref_process_tile(const StepParams& p, Record* rec, uint32_t tile, int tid,
+                                                 int lane, int wave, RefTileIn<N, W>& in) {
+  constexpr int B = ctr_bits(N);
+  constexpr int WAVES = BLOCK / 64;
+  __shared__ uint32_t s_wave[WAVES];
+  __shared__ uint32_t s_excl;
+  if (tid == 0 && tile == p.n_tiles - 1) {  // reset the other ring record (see tile_prologue)
+    Record* nxt = p.rec + ((p.seq + 1) & 1u);
+    atomic_store_agent(&nxt->ticket.v, 0ull);
+    atomic_store_agent(&nxt->error.v, 0ull);
+  }
+  stamp(p, tile, 0, tid);
+  const uint32_t tw0 = (uint32_t)tid * W;  // word offset inside the tile
+  const uint64_t w0 = (uint64_t)tile * BLOCK * W + tw0;
+  const bool active = w0 < p.n_words;
   uint32_t vm[W];
 #pragma unroll
   for (int i = 0; i < W; i++) vm[i] = valid_mask(w0 + i, p.n_words, p.n_slots);
@@ -526,7 +543,7 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
     ctr_zero(c0); ctr_zero(c1); ctr_zero(cp);
 #pragma unroll
     for (int j = 0; j < N; j++) {
-      const uint32_t lo = r1lo[j][i], hi = r1hi[j][i];
+      const uint32_t lo = in.r1lo[j][i], hi = in.r1hi[j][i];
       ctr_add(c0, ~lo & ~hi);
       ctr_add(c1, lo & ~hi);
       ctr_add(cp, ~(lo & hi));
@@ -606,8 +623,8 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
     if (j == p.self_lane) {
 #pragma unroll
       for (int i = 0; i < W; i++) {
-        r2lo[j][i] = (r2lo[j][i] & pend[i]) | (own_lo[i] & ~pend[i]);
-        r2hi[j][i] &= pend[i];
+        in.r2lo[j][i] = (in.r2lo[j][i] & pend[i]) | (own_lo[i] & ~pend[i]);
+        in.r2hi[j][i] &= pend[i];
       }
     }
   }
@@ -618,7 +635,7 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
     ctr_zero(c0); ctr_zero(c1); ctr_zero(cq);
 #pragma unroll
     for (int j = 0; j < N; j++) {
-      const uint32_t lo = r2lo[j][i], hi = r2hi[j][i];
+      const uint32_t lo = in.r2lo[j][i], hi = in.r2hi[j][i];
       ctr_add(c0, ~lo & ~hi);
       ctr_add(c1, lo & ~hi);
       ctr_add(cq, ~lo & hi);
@@ -646,6 +663,54 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
   const TileStats ts = thread_stats<W>(o[6], o[7], pend, vm, vq_count, w0, tw0, p);
   finish_tile<true, BLOCK, W>(p, rec, ts, tile, tid, lane, wave);
   stamp(p, tile, 4, tid);
+}
+
+// Tile ticket (decoupled look-back needs tiles handed out in dispatch order).
+// Two LDS slots alternate so a new ticket never overwrites one still being read.
+__device__ __forceinline__ uint32_t take_ticket(Record* rec, uint32_t* slot, int tid) {
+  if (tid == 0) *slot = (uint32_t)atomicAdd(&rec->ticket.v, 1ull);
+  lds_barrier();
+  return *slot;
+}
+
+// One tile per workgroup (small and mid windows). Occupancy: 4 waves per SIMD
+// (<= 128 VGPRs) so several tiles are resident per CU.
+template <int N, int W, int BLOCK>
+__global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
+  __shared__ uint32_t s_ticket;
+  Record* rec = p.rec + (p.seq & 1u);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t tile = take_ticket(rec, &s_ticket, tid);
+  if (!tile_prologue(p, rec, tile, tid)) return;
+  RefTileIn<N, W> in;
+  ref_load_tile<N, W, BLOCK>(p, tile, tid, in);
+  ref_process_tile<N, W, BLOCK>(p, rec, tile, tid, lane, wave, in);
+}
+
+// Persistent, double-buffered (large windows): a resident workgroup walks tiles in
+// ticket order and issues the NEXT tile's plane loads before it runs the current
+// tile's look-back, draws and stores, so HBM stays busy while it waits.
+// Progress: tickets rise in every workgroup and a tile only waits on smaller
+// tickets, so the smallest unfinished ticket is always being processed.
+template <int N, int W, int BLOCK>
+__global__ __launch_bounds__(BLOCK, 2) void ref_stream_kernel(StepParams p) {
+  __shared__ uint32_t s_ticket[2];
+  Record* rec = p.rec + (p.seq & 1u);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  RefTileIn<N, W> a, b;
+  uint32_t t = take_ticket(rec, &s_ticket[0], tid);
+  if (t < p.n_tiles) ref_load_tile<N, W, BLOCK>(p, t, tid, a);
+  while (t < p.n_tiles) {
+    uint32_t tn = take_ticket(rec, &s_ticket[1], tid);
+    if (tn < p.n_tiles) ref_load_tile<N, W, BLOCK>(p, tn, tid, b);
+    ref_process_tile<N, W, BLOCK>(p, rec, t, tid, lane, wave, a);
+    t = tn;
+    if (t >= p.n_tiles) break;
+    tn = take_ticket(rec, &s_ticket[0], tid);
+    if (tn < p.n_tiles) ref_load_tile<N, W, BLOCK>(p, tn, tid, a);
+    ref_process_tile<N, W, BLOCK>(p, rec, t, tid, lane, wave, b);
+    t = tn;
+  }
 }
 
 // ============================================================================
