@@ -64,7 +64,7 @@ int hip_fail(rg_ctx* ctx, hipError_t e, const char* what) {
     if (e_ != hipSuccess) return hip_fail(ctx, e_, #call);  \
   } while (0)
 
-constexpr int wmax_for(int n) { return n <= 5 ? 4 : (n <= 10 ? 2 : 1); }
+constexpr int wmax_for(int n) { return n <= 10 ? 2 : 1; }
 
 constexpr int wstream_for(int n) { return n <= 5 ? 2 : 1; }
 
@@ -78,8 +78,7 @@ inline int cfg_words(int c, int n) {
 }
 
 int pick_cfg(int n, uint64_t n_words) {
-  // the persistent kernel holds two tiles in registers: spill-free for n <= 10
-  if (n <= 10 && n_words / (512ull * wstream_for(n)) >= 1024) return kCfgStream;
+  if (n_words / (512ull * wmax_for(n)) >= 512) return kCfgBig;
   if (n_words / (256ull * wmax_for(n)) >= 128) return kCfgMid;
   return kCfgSmall;
 }

@@ -224,13 +224,14 @@ __device__ __forceinline__ void lds_barrier() {
 __device__ __forceinline__ uint32_t lookback_exclusive(unsigned long long* status, uint32_t tile,
                                                        uint32_t seq, uint32_t agg, int lane,
                                                        unsigned long long* err) {
-  constexpr int G = 4;  // granules per lane per poll: a 256-tile window per round trip
+  constexpr int G = 16;  // granules per lane per poll: a 1024-tile window per round trip (covers
+                         // every tile in flight, so an inclusive predecessor is in reach)
   const uint32_t tag_agg = seq << 1, tag_inc = (seq << 1) | 1u;
   if (tile == 0) {
     if (lane == 0) atomic_store_agent(status, ((unsigned long long)tag_inc << 32) | agg);
     return 0;
   }
-  if (lane == 0) atomic_store_agent(status + tile, ((unsigned long long)tag_agg << 32) | agg);
+  (void)tag_agg;  // the caller published this tile's aggregate right after its round-1 tally
   uint32_t excl = 0;
   int64_t pos = (int64_t)tile - 1;
   uint32_t spins = 0;
@@ -513,6 +514,13 @@ __device__ __forceinline__ void ref_load_tile(const StepParams& p, uint32_t tile
 
 // REF phase step of one tile (engine.rs:483-682 on the final vote sets of each
 // slot), inputs already in registers (or in flight).
+//
+// Order of work: the only input from other tiles is the StdRng draw index of the
+// tile's VQ slots (the look-back). Round 2 is therefore evaluated for BOTH
+// possible outcomes of every VQ slot's draw (own vote V0 or V1 at the self lane:
+// the counts differ by one), draw-independent planes are stored, and the
+// look-back runs last, when the vote registers are dead, so a 1024-tile window
+// fits and the draw only selects between the two precomputed outcomes.
 template <int N, int W, int BLOCK>
 __device__ __forceinline__ void ref_process_tile(const StepParams& p, Record* rec, uint32_t tile, int tid,
                                                  int lane, int wave, RefTileIn<N, W>& in) {
@@ -557,7 +565,7 @@ __device__ __forceinline__ void ref_process_tile(const StepParams& p, Record* re
     vq_count += __builtin_popcount(r1vq[i]);
   }
 
-  // ---- exclusive prefix of VQ slots: block scan + cross-tile look-back
+  // ---- tile VQ total -> publish this tile's look-back aggregate right away
   const uint32_t incl = wave_incl_scan32(vq_count, lane);
   if (lane == 63) s_wave[wave] = incl;
   lds_barrier();
@@ -567,7 +575,68 @@ __device__ __forceinline__ void ref_process_tile(const StepParams& p, Record* re
     wave_off += (w < wave) ? s_wave[w] : 0u;
     tile_total += s_wave[w];
   }
+  const uint32_t tag_agg = p.seq << 1;
+  if (tid == 0 && tile != 0 && !(p.diag & 1u))
+    atomic_store_agent(p.lookback + tile, ((unsigned long long)tag_agg << 32) | tile_total);
   stamp(p, tile, 1, tid);
+
+  // ---- round 2 for both outcomes of the VQ slots' own vote (engine.rs:540-542, 613-628).
+  // Self-lane contribution: pending -> its received vote stays; V0/V1 -> own vote;
+  // VQ -> V0 (outcome A) or V1 (outcome B).
+  const bool has_self = p.self_lane >= 0 && p.self_lane < N;
+  uint32_t oA[5][W], oB[5][W];  // planes 2,4,5,6,7 under outcome A / B
+  uint32_t o0[W], o1[W];
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    Ctr<B> c0, c1, cq;
+    ctr_zero(c0); ctr_zero(c1); ctr_zero(cq);
+    uint32_t slo = ~0u, shi = ~0u;  // self lane's received code
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      const uint32_t lo = in.r2lo[j][i], hi = in.r2hi[j][i];
+      if (has_self && j == p.self_lane) {
+        slo = lo;
+        shi = hi;
+        continue;
+      }
+      ctr_add(c0, ~lo & ~hi);
+      ctr_add(c1, lo & ~hi);
+      ctr_add(cq, ~lo & hi);
+    }
+    if (has_self) {
+      const uint32_t known = ~pend[i] & ~r1vq[i];
+      ctr_add(c0, (pend[i] & ~slo & ~shi) | (known & ~r1v1[i]));
+      ctr_add(c1, (pend[i] & slo & ~shi) | (known & r1v1[i]));
+      ctr_add(cq, pend[i] & ~slo & shi);
+    }
+    const uint32_t vq = has_self ? r1vq[i] : 0u;
+#pragma unroll
+    for (int alt = 0; alt < 2; alt++) {
+      Ctr<B> a0 = c0, a1 = c1;
+      if (alt == 0) ctr_add(a0, vq);
+      else ctr_add(a1, vq);
+      const uint32_t d0 = ctr_ge(a0, p.q);
+      const uint32_t d1 = ~d0 & ctr_ge(a1, p.q);
+      const uint32_t dq = ~d0 & ~d1 & ctr_ge(cq, p.q);
+      const uint32_t dn = ~(d0 | d1 | dq);
+      uint32_t(&o)[5][W] = alt == 0 ? oA : oB;
+      o[0][i] = (r1v1[i] | (alt ? r1vq[i] : 0u) | pend[i]) & vm[i];  // own r2 vote lo bit
+      o[1][i] = (d1 | dn) & vm[i];
+      o[2][i] = (dq | dn) & vm[i];
+      o[3][i] = (d0 | d1) & vm[i];   // set_decision: committed iff not VQuestion
+      o[4][i] = d1 & vm[i];          // V1: apply_batch + commit_phase
+    }
+    o0[i] = (r1v1[i] | pend[i]) & vm[i];
+    o1[i] = (r1vq[i] | pend[i]) & vm[i];
+  }
+  if (active) {  // draw-independent planes: round-1 result, own-vote hi bit
+    uint32_t* ob = p.out + p.lout.base(w0);
+    store_words<W>(ob + 0 * p.lout.pstride, o0);
+    store_words<W>(ob + 1 * p.lout.pstride, o1);
+    store_words<W>(ob + 3 * p.lout.pstride, pend);
+  }
+
+  // ---- look-back: exclusive VQ prefix of this tile (vote registers are dead now)
   if (wave == 0) {
     const uint32_t e = (p.diag & 1u) ? 0u
                                      : lookback_exclusive(p.lookback, tile, p.seq, tile_total, lane, &rec->error.v);
@@ -576,15 +645,15 @@ __device__ __forceinline__ void ref_process_tile(const StepParams& p, Record* re
   lds_barrier();
   stamp(p, tile, 2, tid);
 
-  // ---- own round-2 vote (engine.rs:523-537; VQ -> one StdRng draw, 567-611).
+  // ---- own round-2 vote of VQ slots: one StdRng draw each (engine.rs:567-611).
   // The tile's draws are ONE contiguous index range [k_tile, k_tile + tile_total):
   // its ChaCha12 blocks are computed once, one per thread, and staged in LDS.
   const unsigned long long k_tile = p.state->rng_next + s_excl;
   unsigned long long k = k_tile + wave_off + incl - vq_count;
-  uint32_t own_lo[W], mq[W];
+  uint32_t drawv1[W], mq[W];
 #pragma unroll
   for (int i = 0; i < W; i++) {
-    own_lo[i] = r1v1[i];
+    drawv1[i] = 0;
     mq[i] = r1vq[i];
   }
   if (tile_total) {
@@ -609,58 +678,27 @@ __device__ __forceinline__ void ref_process_tile(const StepParams& p, Record* re
               (unsigned long long)s_blk[row][ws] | ((unsigned long long)s_blk[row][ws + 1] << 32);
           const bool gt = (c1gt[i] >> b) & 1u, lt = (c1lt[i] >> b) & 1u;
           const bool v1 = gt ? (u < kP90) : (lt ? (u >= kP90) : (u < kP80));
-          own_lo[i] |= (uint32_t)v1 << b;
+          drawv1[i] |= (uint32_t)v1 << b;
           k++;
         }
       }
       lds_barrier();
     }
   }
-
-  // ---- own vote joins round2_votes (engine.rs:540-542); decision (613-628)
+  uint32_t o[5][W];
 #pragma unroll
-  for (int j = 0; j < N; j++) {
-    if (j == p.self_lane) {
+  for (int pl = 0; pl < 5; pl++)
 #pragma unroll
-      for (int i = 0; i < W; i++) {
-        in.r2lo[j][i] = (in.r2lo[j][i] & pend[i]) | (own_lo[i] & ~pend[i]);
-        in.r2hi[j][i] &= pend[i];
-      }
-    }
-  }
-  uint32_t o[kOutPlanes][W];
-#pragma unroll
-  for (int i = 0; i < W; i++) {
-    Ctr<B> c0, c1, cq;
-    ctr_zero(c0); ctr_zero(c1); ctr_zero(cq);
-#pragma unroll
-    for (int j = 0; j < N; j++) {
-      const uint32_t lo = in.r2lo[j][i], hi = in.r2hi[j][i];
-      ctr_add(c0, ~lo & ~hi);
-      ctr_add(c1, lo & ~hi);
-      ctr_add(cq, ~lo & hi);
-    }
-    const uint32_t d0 = ctr_ge(c0, p.q);
-    const uint32_t d1 = ~d0 & ctr_ge(c1, p.q);
-    const uint32_t dq = ~d0 & ~d1 & ctr_ge(cq, p.q);
-    const uint32_t dn = ~(d0 | d1 | dq);
-    o[0][i] = (r1v1[i] | pend[i]) & vm[i];
-    o[1][i] = (r1vq[i] | pend[i]) & vm[i];
-    o[2][i] = (own_lo[i] | pend[i]) & vm[i];
-    o[3][i] = pend[i];
-    o[4][i] = (d1 | dn) & vm[i];
-    o[5][i] = (dq | dn) & vm[i];
-    o[6][i] = (d0 | d1) & vm[i];   // set_decision: committed iff not VQuestion
-    o[7][i] = d1 & vm[i];          // V1: apply_batch + commit_phase
-  }
+    for (int i = 0; i < W; i++) o[pl][i] = (oA[pl][i] & ~drawv1[i]) | (oB[pl][i] & drawv1[i]);
   if (active) {
     uint32_t* ob = p.out + p.lout.base(w0);
+    store_words<W>(ob + 2 * p.lout.pstride, o[0]);
 #pragma unroll
-    for (int pl = 0; pl < kOutPlanes; pl++) store_words<W>(ob + pl * p.lout.pstride, o[pl]);
+    for (int pl = 1; pl < 5; pl++) store_words<W>(ob + (3 + pl) * p.lout.pstride, o[pl]);
   }
   stamp(p, tile, 3, tid);
   if (p.diag & 2u) return;
-  const TileStats ts = thread_stats<W>(o[6], o[7], pend, vm, vq_count, w0, tw0, p);
+  const TileStats ts = thread_stats<W>(o[3], o[4], pend, vm, vq_count, w0, tw0, p);
   finish_tile<true, BLOCK, W>(p, rec, ts, tile, tid, lane, wave);
   stamp(p, tile, 4, tid);
 }
