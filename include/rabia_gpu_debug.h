@@ -11,8 +11,7 @@ extern "C" {
 #endif
 /* diag bits: 1 skip the look-back wait (wrong draws), 2 skip per-tile statistics
  * and the step result, 4 record per-tile s_memrealtime stamps (100 MHz);
- * bits 8-10: 0 = automatic tile shape, 1 persistent stream (512 x Ws), 2 mid (256 x W),
- * 3 small (128 x 1), 4 big (512 x W, one tile per workgroup). */
+ * bits 8-9: 0 = automatic tile shape, 1 big (512 x W), 2 mid (256 x W), 3 small (128 x 1). */
 int rg_debug_set(rg_ctx* ctx, uint32_t diag);
 int rg_debug_stamps(rg_ctx* ctx, uint64_t* host_out, uint64_t n_words);
 /* REF kernel memory pattern (20 in-planes, 8 out-planes, 16 B/lane) without protocol.

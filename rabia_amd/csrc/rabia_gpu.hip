@@ -36,8 +36,6 @@ struct rg_ctx {
   DevResult* d_user_result = nullptr;
   uint64_t stage_votes_words = 0, stage_out_words = 0;
   uint32_t diag = 0;
-  int cu_count = 0;
-  int stream_blocks_per_cu = 0;
   unsigned long long* dbg = nullptr;
   uint64_t dbg_cap = 0;
   std::string err;
@@ -64,48 +62,34 @@ int hip_fail(rg_ctx* ctx, hipError_t e, const char* what) {
     if (e_ != hipSuccess) return hip_fail(ctx, e_, #call);  \
   } while (0)
 
-constexpr int wmax_for(int n) { return n <= 10 ? 2 : 1; }
+constexpr int wmax_for(int n) { return n <= 5 ? 4 : (n <= 10 ? 2 : 1); }
 
-constexpr int wstream_for(int n) { return n <= 5 ? 2 : 1; }
-
-// Tile shapes: {threads, words per thread}. Large windows run the persistent
-// double-buffered kernel; mid windows one 256 x W tile per workgroup; small
-// windows 128 x 1 tiles so that a single 2^20-slot window fills the 256 CUs.
-enum TileCfg { kCfgStream = 0, kCfgMid = 1, kCfgSmall = 2, kCfgBig = 3 };
-constexpr int cfg_block(int c) { return c == kCfgStream || c == kCfgBig ? 512 : (c == kCfgMid ? 256 : 128); }
-inline int cfg_words(int c, int n) {
-  return c == kCfgSmall ? 1 : (c == kCfgStream ? wstream_for(n) : wmax_for(n));
-}
+// Tile shapes: {threads, words per thread}. Big tiles keep the per-launch count
+// of tile tickets and look-back hand-offs low on large windows; small tiles fill
+// the 256 CUs on single 2^20-slot windows.
+enum TileCfg { kCfgBig = 0, kCfgMid = 1, kCfgSmall = 2 };
+constexpr int cfg_block(int c) { return c == kCfgBig ? 512 : (c == kCfgMid ? 256 : 128); }
+inline int cfg_words(int c, int n) { return c == kCfgSmall ? 1 : wmax_for(n); }
 
 int pick_cfg(int n, uint64_t n_words) {
-  if (n_words / (512ull * wmax_for(n)) >= 512) return kCfgBig;
-  if (n_words / (256ull * wmax_for(n)) >= 128) return kCfgMid;
+  const uint64_t wm = (uint64_t)wmax_for(n);
+  if (n_words / (512 * wm) >= 256) return kCfgBig;
+  if (n_words / (256 * wm) >= 128) return kCfgMid;
   return kCfgSmall;
 }
 
 using StepLaunch = void (*)(int, uint32_t, hipStream_t, const StepParams&);
-using OccFn = int (*)();
 
 template <int N>
 struct Disp {
   static constexpr int WM = wmax_for(N);
-  static constexpr int WS = wstream_for(N);
   static void ref(int c, uint32_t grid, hipStream_t s, const StepParams& p) {
-    if (c == kCfgStream) hipLaunchKernelGGL((ref_stream_kernel<N, WS, 512>), dim3(grid), dim3(512), 0, s, p);
-    else if (c == kCfgBig) hipLaunchKernelGGL((ref_step_kernel<N, WM, 512>), dim3(grid), dim3(512), 0, s, p);
+    if (c == kCfgBig) hipLaunchKernelGGL((ref_step_kernel<N, WM, 512>), dim3(grid), dim3(512), 0, s, p);
     else if (c == kCfgMid) hipLaunchKernelGGL((ref_step_kernel<N, WM, 256>), dim3(grid), dim3(256), 0, s, p);
     else hipLaunchKernelGGL((ref_step_kernel<N, 1, 128>), dim3(grid), dim3(128), 0, s, p);
   }
-  // Resident workgroups per CU of the persistent kernel.
-  static int ref_stream_occupancy() {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ref_stream_kernel<N, WS, 512>, 512, 0) != hipSuccess)
-      return 1;
-    return nb > 0 ? nb : 1;
-  }
   static void wmvc(int c, uint32_t grid, hipStream_t s, const StepParams& p) {
-    if (c == kCfgStream || c == kCfgBig)
-      hipLaunchKernelGGL((wmvc_step_kernel<N, WM, 512>), dim3(grid), dim3(512), 0, s, p);
+    if (c == kCfgBig) hipLaunchKernelGGL((wmvc_step_kernel<N, WM, 512>), dim3(grid), dim3(512), 0, s, p);
     else if (c == kCfgMid) hipLaunchKernelGGL((wmvc_step_kernel<N, WM, 256>), dim3(grid), dim3(256), 0, s, p);
     else hipLaunchKernelGGL((wmvc_step_kernel<N, 1, 128>), dim3(grid), dim3(128), 0, s, p);
   }
@@ -124,7 +108,6 @@ using DigestLaunch = void (*)(uint32_t, hipStream_t, const uint64_t*, uint64_t, 
    &Disp<12>::fn, &Disp<13>::fn, &Disp<14>::fn, &Disp<15>::fn, &Disp<16>::fn}
 
 const StepLaunch kRefLaunch[17] = RG_TABLE(ref);
-const OccFn kRefStreamOcc[17] = RG_TABLE(ref_stream_occupancy);
 const StepLaunch kWmvcLaunch[17] = RG_TABLE(wmvc);
 const DigestLaunch kDigestLaunch[17] = RG_TABLE(digest);
 
@@ -241,7 +224,6 @@ int rg_create(rg_ctx** out, const rg_config* cfg) {
   seed_from_u64(cfg->seed, ctx->ref_key.k);
   seed_from_u64(cfg->coin_seed, ctx->coin_key.k);
   ctx->coin_stream = cfg->epoch | kCoinStreamBit;
-  ctx->cu_count = prop.multiProcessorCount;
   auto bail = [&](hipError_t e, const char* what) {
     int rc = hip_fail(nullptr, e, what);
     rg_destroy(ctx);
@@ -338,17 +320,10 @@ int rg_phase_step_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_de
   uint64_t need_in, need_out;
   if (int rc = make_layout(ctx, 4 * n + 1, n_words, stride_words, &lin, &need_in, "rg_phase_step")) return rc;
   if (int rc = make_layout(ctx, kOutPlanes, n_words, stride_words, &lout, &need_out, "rg_phase_step")) return rc;
-  const uint32_t force = (ctx->diag >> 8) & 7u;  // diagnostics: force a tile shape
-  int cfg = force ? (int)force - 1 : pick_cfg(n, n_words);
-  if (wmvc && cfg == kCfgStream) cfg = kCfgBig;  // WMVC has no cross-tile wait to hide
+  const uint32_t force = (ctx->diag >> 8) & 3u;  // diagnostics: force a tile shape
+  const int cfg = force ? (int)force - 1 : pick_cfg(n, n_words);
   const uint64_t tile_words = (uint64_t)cfg_block(cfg) * cfg_words(cfg, n);
   const uint64_t n_tiles = (n_words + tile_words - 1) / tile_words;
-  uint64_t grid = n_tiles;
-  if (cfg == kCfgStream) {
-    if (!ctx->stream_blocks_per_cu) ctx->stream_blocks_per_cu = kRefStreamOcc[n]();
-    const uint64_t resident = (uint64_t)ctx->cu_count * ctx->stream_blocks_per_cu;
-    grid = n_tiles < resident ? n_tiles : resident;
-  }
   if (int rc = ensure_tiles(ctx, n_tiles, false)) return rc;
   if (++ctx->seq >= (1u << 31)) {  // tags wrap: start a fresh epoch on zeroed granules
     if (int rc = ensure_tiles(ctx, n_tiles, true)) return rc;
@@ -391,7 +366,7 @@ int rg_phase_step_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_de
     p.dbg = ctx->dbg;
   }
   hipStream_t s = pick_stream(ctx, stream);
-  (wmvc ? kWmvcLaunch : kRefLaunch)[n](cfg, (uint32_t)grid, s, p);
+  (wmvc ? kWmvcLaunch : kRefLaunch)[n](cfg, (uint32_t)n_tiles, s, p);
   RG_HIP(ctx, hipGetLastError());
   return RG_OK;
 }

@@ -224,44 +224,27 @@ __device__ __forceinline__ void lds_barrier() {
 __device__ __forceinline__ uint32_t lookback_exclusive(unsigned long long* status, uint32_t tile,
                                                        uint32_t seq, uint32_t agg, int lane,
                                                        unsigned long long* err) {
-  constexpr int G = 16;  // granules per lane per poll: a 1024-tile window per round trip (covers
-                         // every tile in flight, so an inclusive predecessor is in reach)
   const uint32_t tag_agg = seq << 1, tag_inc = (seq << 1) | 1u;
   if (tile == 0) {
     if (lane == 0) atomic_store_agent(status, ((unsigned long long)tag_inc << 32) | agg);
     return 0;
   }
-  (void)tag_agg;  // the caller published this tile's aggregate right after its round-1 tally
+  if (lane == 0) atomic_store_agent(status + tile, ((unsigned long long)tag_agg << 32) | agg);
   uint32_t excl = 0;
   int64_t pos = (int64_t)tile - 1;
   uint32_t spins = 0;
   for (;;) {
-    unsigned long long g[G];
-#pragma unroll
-    for (int k = 0; k < G; k++) {  // all G loads in flight together; distance order k-major
-      const int64_t pidx = pos - (64 * k + lane);
-      g[k] = pidx >= 0 ? atomic_load_agent(status + pidx) : ((unsigned long long)tag_inc << 32);
-    }
-    int consumed = 0;  // groups fully summed this round
-    bool found = false;
-#pragma unroll
-    for (int k = 0; k < G; k++) {
-      if (found || consumed < k) break;  // uniform
-      const uint32_t tag = (uint32_t)(g[k] >> 32);
-      const bool ready = (tag >> 1) == seq;
-      const bool incl = ready && (tag & 1u);
-      const unsigned long long incl_mask = __ballot(incl);
-      const unsigned long long notready = __ballot(!ready);
-      const int first = incl_mask ? __builtin_ctzll(incl_mask) : 64;
-      const unsigned long long need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);
-      if (notready & need) break;  // a needed predecessor has not published yet
-      excl += (uint32_t)wave_sum64((lane <= first) ? (uint32_t)g[k] : 0u);
-      consumed = k + 1;
-      found = first < 64;
-    }
-    if (found) break;
-    pos -= 64 * consumed;
-    if (consumed < G) {
+    const int64_t pidx = pos - lane;
+    unsigned long long g = pidx >= 0 ? atomic_load_agent(status + pidx)
+                                     : ((unsigned long long)tag_inc << 32);
+    const uint32_t tag = (uint32_t)(g >> 32);
+    const bool ready = (tag >> 1) == seq;
+    const bool incl = ready && (tag & 1u);
+    const unsigned long long incl_mask = __ballot(incl);
+    const unsigned long long notready = __ballot(!ready);
+    const int first = incl_mask ? __builtin_ctzll(incl_mask) : 64;
+    const unsigned long long need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);
+    if (notready & need) {
       if (++spins > (1u << 22)) {  // ~seconds: a protocol fault, not a wait
         if (lane == 0) {
           atomicOr(err, 1ull);
@@ -270,7 +253,12 @@ __device__ __forceinline__ uint32_t lookback_exclusive(unsigned long long* statu
         break;
       }
       __builtin_amdgcn_s_sleep(1);
+      continue;
     }
+    const uint32_t v = (lane <= first) ? (uint32_t)g : 0u;
+    excl += (uint32_t)wave_sum64(v);
+    if (first < 64) break;
+    pos -= 64;
   }
   if (lane == 0)
     atomic_store_agent(status + tile, ((unsigned long long)tag_inc << 32) | (agg + excl));
@@ -482,61 +470,48 @@ __device__ __forceinline__ TileStats thread_stats(const uint32_t (&committed)[W]
 // ============================================================================
 // REF phase step: engine.rs:483-682 on the final vote sets of every slot.
 // ============================================================================
-// One REF tile's register-resident inputs: round-1 and round-2 vote planes.
-template <int N, int W>
-struct RefTileIn {
-  uint32_t r1lo[N][W], r1hi[N][W], r2lo[N][W], r2hi[N][W];
-};
-
+// Occupancy: 4 waves per SIMD (<= 128 VGPRs) so that at least two 512-thread or
+// four 256-thread tiles are resident per CU and one tile's look-back / stores
+// overlap another's loads.
 template <int N, int W, int BLOCK>
-__device__ __forceinline__ void ref_load_tile(const StepParams& p, uint32_t tile, int tid, RefTileIn<N, W>& in) {
-  const uint64_t w0 = (uint64_t)tile * BLOCK * W + (uint64_t)tid * W;
-  if (w0 < p.n_words) {
+__global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
+  constexpr int B = ctr_bits(N);
+  constexpr int WAVES = BLOCK / 64;
+  __shared__ uint32_t s_ticket;
+  __shared__ uint32_t s_wave[WAVES];
+  __shared__ uint32_t s_excl;
+  Record* rec = p.rec + (p.seq & 1u);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) s_ticket = (uint32_t)atomicAdd(&rec->ticket.v, 1ull);
+  lds_barrier();
+  const uint32_t tile = s_ticket;
+  if (!tile_prologue(p, rec, tile, tid)) return;
+  stamp(p, tile, 0, tid);
+  const uint32_t tw0 = (uint32_t)tid * W;  // word offset inside the tile
+  const uint64_t w0 = (uint64_t)tile * BLOCK * W + tw0;
+  const bool active = w0 < p.n_words;
+
+  // Issue every plane load up front (R2 stays in flight across the look-back).
+  uint32_t r1lo[N][W], r1hi[N][W], r2lo[N][W], r2hi[N][W];
+  if (active) {
     const uint32_t* base = p.votes + p.lin.base(w0);
     const uint64_t ps = p.lin.pstride;
 #pragma unroll
     for (int j = 0; j < N; j++) {
-      load_words<W>(base + (2 * j) * ps, in.r1lo[j]);
-      load_words<W>(base + (2 * j + 1) * ps, in.r1hi[j]);
+      load_words<W>(base + (2 * j) * ps, r1lo[j]);
+      load_words<W>(base + (2 * j + 1) * ps, r1hi[j]);
     }
 #pragma unroll
     for (int j = 0; j < N; j++) {
-      load_words<W>(base + (2 * N + 2 * j) * ps, in.r2lo[j]);
-      load_words<W>(base + (2 * N + 2 * j + 1) * ps, in.r2hi[j]);
+      load_words<W>(base + (2 * N + 2 * j) * ps, r2lo[j]);
+      load_words<W>(base + (2 * N + 2 * j + 1) * ps, r2hi[j]);
     }
   } else {
 #pragma unroll
     for (int j = 0; j < N; j++)
 #pragma unroll
-      for (int i = 0; i < W; i++) in.r1lo[j][i] = in.r1hi[j][i] = in.r2lo[j][i] = in.r2hi[j][i] = ~0u;
+      for (int i = 0; i < W; i++) r1lo[j][i] = r1hi[j][i] = r2lo[j][i] = r2hi[j][i] = ~0u;
   }
-}
-
-// REF phase step of one tile (engine.rs:483-682 on the final vote sets of each
-// slot), inputs already in registers (or in flight).
-//
-// Order of work: the only input from other tiles is the StdRng draw index of the
-// tile's VQ slots (the look-back). Round 2 is therefore evaluated for BOTH
-// possible outcomes of every VQ slot's draw (own vote V0 or V1 at the self lane:
-// the counts differ by one), draw-independent planes are stored, and the
-// look-back runs last, when the vote registers are dead, so a 1024-tile window
-// fits and the draw only selects between the two precomputed outcomes.
-template <int N, int W, int BLOCK>
-__device__ __forceinline__ void ref_process_tile(const StepParams& p, Record* rec, uint32_t tile, int tid,
-                                                 int lane, int wave, RefTileIn<N, W>& in) {
-  constexpr int B = ctr_bits(N);
-  constexpr int WAVES = BLOCK / 64;
-  __shared__ uint32_t s_wave[WAVES];
-  __shared__ uint32_t s_excl;
-  if (tid == 0 && tile == p.n_tiles - 1) {  // reset the other ring record (see tile_prologue)
-    Record* nxt = p.rec + ((p.seq + 1) & 1u);
-    atomic_store_agent(&nxt->ticket.v, 0ull);
-    atomic_store_agent(&nxt->error.v, 0ull);
-  }
-  stamp(p, tile, 0, tid);
-  const uint32_t tw0 = (uint32_t)tid * W;  // word offset inside the tile
-  const uint64_t w0 = (uint64_t)tile * BLOCK * W + tw0;
-  const bool active = w0 < p.n_words;
   uint32_t vm[W];
 #pragma unroll
   for (int i = 0; i < W; i++) vm[i] = valid_mask(w0 + i, p.n_words, p.n_slots);
@@ -551,7 +526,7 @@ __device__ __forceinline__ void ref_process_tile(const StepParams& p, Record* re
     ctr_zero(c0); ctr_zero(c1); ctr_zero(cp);
 #pragma unroll
     for (int j = 0; j < N; j++) {
-      const uint32_t lo = in.r1lo[j][i], hi = in.r1hi[j][i];
+      const uint32_t lo = r1lo[j][i], hi = r1hi[j][i];
       ctr_add(c0, ~lo & ~hi);
       ctr_add(c1, lo & ~hi);
       ctr_add(cp, ~(lo & hi));
@@ -565,7 +540,7 @@ __device__ __forceinline__ void ref_process_tile(const StepParams& p, Record* re
     vq_count += __builtin_popcount(r1vq[i]);
   }
 
-  // ---- tile VQ total -> publish this tile's look-back aggregate right away
+  // ---- exclusive prefix of VQ slots: block scan + cross-tile look-back
   const uint32_t incl = wave_incl_scan32(vq_count, lane);
   if (lane == 63) s_wave[wave] = incl;
   lds_barrier();
@@ -575,68 +550,7 @@ __device__ __forceinline__ void ref_process_tile(const StepParams& p, Record* re
     wave_off += (w < wave) ? s_wave[w] : 0u;
     tile_total += s_wave[w];
   }
-  const uint32_t tag_agg = p.seq << 1;
-  if (tid == 0 && tile != 0 && !(p.diag & 1u))
-    atomic_store_agent(p.lookback + tile, ((unsigned long long)tag_agg << 32) | tile_total);
   stamp(p, tile, 1, tid);
-
-  // ---- round 2 for both outcomes of the VQ slots' own vote (engine.rs:540-542, 613-628).
-  // Self-lane contribution: pending -> its received vote stays; V0/V1 -> own vote;
-  // VQ -> V0 (outcome A) or V1 (outcome B).
-  const bool has_self = p.self_lane >= 0 && p.self_lane < N;
-  uint32_t oA[5][W], oB[5][W];  // planes 2,4,5,6,7 under outcome A / B
-  uint32_t o0[W], o1[W];
-#pragma unroll
-  for (int i = 0; i < W; i++) {
-    Ctr<B> c0, c1, cq;
-    ctr_zero(c0); ctr_zero(c1); ctr_zero(cq);
-    uint32_t slo = ~0u, shi = ~0u;  // self lane's received code
-#pragma unroll
-    for (int j = 0; j < N; j++) {
-      const uint32_t lo = in.r2lo[j][i], hi = in.r2hi[j][i];
-      if (has_self && j == p.self_lane) {
-        slo = lo;
-        shi = hi;
-        continue;
-      }
-      ctr_add(c0, ~lo & ~hi);
-      ctr_add(c1, lo & ~hi);
-      ctr_add(cq, ~lo & hi);
-    }
-    if (has_self) {
-      const uint32_t known = ~pend[i] & ~r1vq[i];
-      ctr_add(c0, (pend[i] & ~slo & ~shi) | (known & ~r1v1[i]));
-      ctr_add(c1, (pend[i] & slo & ~shi) | (known & r1v1[i]));
-      ctr_add(cq, pend[i] & ~slo & shi);
-    }
-    const uint32_t vq = has_self ? r1vq[i] : 0u;
-#pragma unroll
-    for (int alt = 0; alt < 2; alt++) {
-      Ctr<B> a0 = c0, a1 = c1;
-      if (alt == 0) ctr_add(a0, vq);
-      else ctr_add(a1, vq);
-      const uint32_t d0 = ctr_ge(a0, p.q);
-      const uint32_t d1 = ~d0 & ctr_ge(a1, p.q);
-      const uint32_t dq = ~d0 & ~d1 & ctr_ge(cq, p.q);
-      const uint32_t dn = ~(d0 | d1 | dq);
-      uint32_t(&o)[5][W] = alt == 0 ? oA : oB;
-      o[0][i] = (r1v1[i] | (alt ? r1vq[i] : 0u) | pend[i]) & vm[i];  // own r2 vote lo bit
-      o[1][i] = (d1 | dn) & vm[i];
-      o[2][i] = (dq | dn) & vm[i];
-      o[3][i] = (d0 | d1) & vm[i];   // set_decision: committed iff not VQuestion
-      o[4][i] = d1 & vm[i];          // V1: apply_batch + commit_phase
-    }
-    o0[i] = (r1v1[i] | pend[i]) & vm[i];
-    o1[i] = (r1vq[i] | pend[i]) & vm[i];
-  }
-  if (active) {  // draw-independent planes: round-1 result, own-vote hi bit
-    uint32_t* ob = p.out + p.lout.base(w0);
-    store_words<W>(ob + 0 * p.lout.pstride, o0);
-    store_words<W>(ob + 1 * p.lout.pstride, o1);
-    store_words<W>(ob + 3 * p.lout.pstride, pend);
-  }
-
-  // ---- look-back: exclusive VQ prefix of this tile (vote registers are dead now)
   if (wave == 0) {
     const uint32_t e = (p.diag & 1u) ? 0u
                                      : lookback_exclusive(p.lookback, tile, p.seq, tile_total, lane, &rec->error.v);
@@ -645,15 +559,15 @@ __device__ __forceinline__ void ref_process_tile(const StepParams& p, Record* re
   lds_barrier();
   stamp(p, tile, 2, tid);
 
-  // ---- own round-2 vote of VQ slots: one StdRng draw each (engine.rs:567-611).
+  // ---- own round-2 vote (engine.rs:523-537; VQ -> one StdRng draw, 567-611).
   // The tile's draws are ONE contiguous index range [k_tile, k_tile + tile_total):
   // its ChaCha12 blocks are computed once, one per thread, and staged in LDS.
   const unsigned long long k_tile = p.state->rng_next + s_excl;
   unsigned long long k = k_tile + wave_off + incl - vq_count;
-  uint32_t drawv1[W], mq[W];
+  uint32_t own_lo[W], mq[W];
 #pragma unroll
   for (int i = 0; i < W; i++) {
-    drawv1[i] = 0;
+    own_lo[i] = r1v1[i];
     mq[i] = r1vq[i];
   }
   if (tile_total) {
@@ -678,77 +592,60 @@ __device__ __forceinline__ void ref_process_tile(const StepParams& p, Record* re
               (unsigned long long)s_blk[row][ws] | ((unsigned long long)s_blk[row][ws + 1] << 32);
           const bool gt = (c1gt[i] >> b) & 1u, lt = (c1lt[i] >> b) & 1u;
           const bool v1 = gt ? (u < kP90) : (lt ? (u >= kP90) : (u < kP80));
-          drawv1[i] |= (uint32_t)v1 << b;
+          own_lo[i] |= (uint32_t)v1 << b;
           k++;
         }
       }
       lds_barrier();
     }
   }
-  uint32_t o[5][W];
+
+  // ---- own vote joins round2_votes (engine.rs:540-542); decision (613-628)
 #pragma unroll
-  for (int pl = 0; pl < 5; pl++)
+  for (int j = 0; j < N; j++) {
+    if (j == p.self_lane) {
 #pragma unroll
-    for (int i = 0; i < W; i++) o[pl][i] = (oA[pl][i] & ~drawv1[i]) | (oB[pl][i] & drawv1[i]);
+      for (int i = 0; i < W; i++) {
+        r2lo[j][i] = (r2lo[j][i] & pend[i]) | (own_lo[i] & ~pend[i]);
+        r2hi[j][i] &= pend[i];
+      }
+    }
+  }
+  uint32_t o[kOutPlanes][W];
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    Ctr<B> c0, c1, cq;
+    ctr_zero(c0); ctr_zero(c1); ctr_zero(cq);
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      const uint32_t lo = r2lo[j][i], hi = r2hi[j][i];
+      ctr_add(c0, ~lo & ~hi);
+      ctr_add(c1, lo & ~hi);
+      ctr_add(cq, ~lo & hi);
+    }
+    const uint32_t d0 = ctr_ge(c0, p.q);
+    const uint32_t d1 = ~d0 & ctr_ge(c1, p.q);
+    const uint32_t dq = ~d0 & ~d1 & ctr_ge(cq, p.q);
+    const uint32_t dn = ~(d0 | d1 | dq);
+    o[0][i] = (r1v1[i] | pend[i]) & vm[i];
+    o[1][i] = (r1vq[i] | pend[i]) & vm[i];
+    o[2][i] = (own_lo[i] | pend[i]) & vm[i];
+    o[3][i] = pend[i];
+    o[4][i] = (d1 | dn) & vm[i];
+    o[5][i] = (dq | dn) & vm[i];
+    o[6][i] = (d0 | d1) & vm[i];   // set_decision: committed iff not VQuestion
+    o[7][i] = d1 & vm[i];          // V1: apply_batch + commit_phase
+  }
   if (active) {
     uint32_t* ob = p.out + p.lout.base(w0);
-    store_words<W>(ob + 2 * p.lout.pstride, o[0]);
 #pragma unroll
-    for (int pl = 1; pl < 5; pl++) store_words<W>(ob + (3 + pl) * p.lout.pstride, o[pl]);
+    for (int pl = 0; pl < kOutPlanes; pl++) store_words<W>(ob + pl * p.lout.pstride, o[pl]);
   }
   stamp(p, tile, 3, tid);
   if (p.diag & 2u) return;
-  const TileStats ts = thread_stats<W>(o[3], o[4], pend, vm, vq_count, w0, tw0, p);
+  const TileStats ts = thread_stats<W>(o[6], o[7], pend, vm, vq_count, w0, tw0, p);
   finish_tile<true, BLOCK, W>(p, rec, ts, tile, tid, lane, wave);
   stamp(p, tile, 4, tid);
-}
-
-// Tile ticket (decoupled look-back needs tiles handed out in dispatch order).
-// Two LDS slots alternate so a new ticket never overwrites one still being read.
-__device__ __forceinline__ uint32_t take_ticket(Record* rec, uint32_t* slot, int tid) {
-  if (tid == 0) *slot = (uint32_t)atomicAdd(&rec->ticket.v, 1ull);
-  lds_barrier();
-  return *slot;
-}
-
-// One tile per workgroup (small and mid windows). Occupancy: 4 waves per SIMD
-// (<= 128 VGPRs) so several tiles are resident per CU.
-template <int N, int W, int BLOCK>
-__global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
-  __shared__ uint32_t s_ticket;
-  Record* rec = p.rec + (p.seq & 1u);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t tile = take_ticket(rec, &s_ticket, tid);
-  if (!tile_prologue(p, rec, tile, tid)) return;
-  RefTileIn<N, W> in;
-  ref_load_tile<N, W, BLOCK>(p, tile, tid, in);
-  ref_process_tile<N, W, BLOCK>(p, rec, tile, tid, lane, wave, in);
-}
-
-// Persistent, double-buffered (large windows): a resident workgroup walks tiles in
-// ticket order and issues the NEXT tile's plane loads before it runs the current
-// tile's look-back, draws and stores, so HBM stays busy while it waits.
-// Progress: tickets rise in every workgroup and a tile only waits on smaller
-// tickets, so the smallest unfinished ticket is always being processed.
-template <int N, int W, int BLOCK>
-__global__ __launch_bounds__(BLOCK, 2) void ref_stream_kernel(StepParams p) {
-  __shared__ uint32_t s_ticket[2];
-  Record* rec = p.rec + (p.seq & 1u);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  RefTileIn<N, W> a, b;
-  uint32_t t = take_ticket(rec, &s_ticket[0], tid);
-  if (t < p.n_tiles) ref_load_tile<N, W, BLOCK>(p, t, tid, a);
-  while (t < p.n_tiles) {
-    uint32_t tn = take_ticket(rec, &s_ticket[1], tid);
-    if (tn < p.n_tiles) ref_load_tile<N, W, BLOCK>(p, tn, tid, b);
-    ref_process_tile<N, W, BLOCK>(p, rec, t, tid, lane, wave, a);
-    t = tn;
-    if (t >= p.n_tiles) break;
-    tn = take_ticket(rec, &s_ticket[0], tid);
-    if (tn < p.n_tiles) ref_load_tile<N, W, BLOCK>(p, tn, tid, a);
-    ref_process_tile<N, W, BLOCK>(p, rec, t, tid, lane, wave, b);
-    t = tn;
-  }
 }
 
 // ============================================================================

@@ -60,10 +60,8 @@ def run(variant, k):
 
 
 variants = {
-    "ref": {}, "ref_padstride": {"stride": "pad"}, "ref_mid": {"diag": 2 << 8}, "ref_big": {"diag": 4 << 8},
-    "tiled1024": {"tiled": True}, "tiled1024_stream": {"tiled": True, "diag": 1 << 8},
-    "tiled1024_mid": {"tiled": True, "diag": 2 << 8}, "tiled1024_big": {"tiled": True, "diag": 4 << 8},
-    "tiled1024_stream_nolb": {"tiled": True, "diag": (1 << 8) | 1},
+    "ref": {}, "ref_padstride": {"stride": "pad"}, "ref_mid": {"diag": 2 << 8},
+    "tiled1024": {"tiled": True}, "tiled1024_mid": {"tiled": True, "diag": 2 << 8},
     "tiled1024_nolb_nofin": {"tiled": True, "diag": 3}, "tiled1024_1M": {"tiled": True, "slots": 1 << 20}, "no_lookback": {"diag": 1}, "no_finish": {"diag": 2},
     "no_lookback_no_finish": {"diag": 3}, "probe": {"probe": True}, "probe_padstride": {"probe": True, "stride": "pad"},
     "ref_1M": {"slots": 1 << 20}, "no_lb_no_fin_1M": {"slots": 1 << 20, "diag": 3}, "probe_1M": {"probe": True, "slots": 1 << 20},
