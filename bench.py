@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--windows", type=int, default=64)
     ap.add_argument("--replicas", type=int, default=5)
     ap.add_argument("--sets", type=int, default=3)
+    ap.add_argument("--tile-words", type=int, default=1024,
+                    help="slot-tiled plane layout (include/rabia_gpu.h); 0 = planar")
     ap.add_argument("--cpu-sample-windows", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_c2.json"))
@@ -97,7 +99,15 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     n, G = a.replicas, a.windows
     S = G * WINDOW
-    stride = ((S + 127) // 128) * 4
+    T = a.tile_words
+    nw = S // 32
+    if T:  # slot-tiled: the planes of each T-word slot tile are contiguous
+        stride = T
+        in_words = ((nw + T - 1) // T) * (4 * n + 1) * T
+        out_words = ((nw + T - 1) // T) * 8 * T
+    else:
+        stride = ((S + 127) // 128) * 4
+        in_words, out_words = (4 * n + 1) * stride, 8 * stride
     # A dedicated stream: the legacy default stream has handle 0, which the C ABI
     # reads as "the context's own stream"; events must sit on the launch stream.
     stream = torch.cuda.Stream()
@@ -105,11 +115,11 @@ def main():
     sp = stream.cuda_stream
     assert sp != 0
 
-    ev = PhaseEvaluator(n, self_lane=n - 1, mode="ref", seed=42 + rank, device=local)
+    ev = PhaseEvaluator(n, self_lane=n - 1, mode="ref", seed=42 + rank, device=local, tile_words=T)
     sets = []
     for i in range(a.sets):
-        votes = torch.empty((4 * n + 1) * stride, dtype=torch.int32, device="cuda")
-        out = torch.empty(8 * stride, dtype=torch.int32, device="cuda")
+        votes = torch.empty(in_words, dtype=torch.int32, device="cuda")
+        out = torch.empty(out_words, dtype=torch.int32, device="cuda")
         ev.trace_generate_async(N.RG_TRACE_AGREE90, 1000 * rank + i, 1 + i * S, S, stride,
                                 votes.data_ptr(), sp)
         sets.append((votes, out))
@@ -209,7 +219,8 @@ def main():
             "config": {"workload": f"C2: {n} replicas x 2^20-slot windows, agree90 trace, REF single phase "
                                    f"sweep; {G} windows per step per GPU",
                        "replicas": n, "slots_per_window": WINDOW, "windows_per_step": G,
-                       "slots_per_step_per_gpu": S, "mode": "ref", "parallelism": f"slot-shard x{world}"},
+                       "slots_per_step_per_gpu": S, "mode": "ref", "layout": f"slot-tiled {T}" if T else "planar",
+                       "parallelism": f"slot-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": load_pmc(a.pmc_file, n, S),
