@@ -14,17 +14,23 @@ import sys
 
 
 def per_dispatch(d, counter, kernel_sub="ref_step_kernel"):
-    vals = {}
+    """Counter value per dispatch of the headline launch: the step kernel dispatches
+    with the largest grid (bench.py also times single-window launches)."""
+    rows = []
     for path in glob.glob(f"{d}/**/*counter_collection*.csv", recursive=True):
         with open(path) as f:
             for row in csv.DictReader(f):
-                name = row.get("Kernel_Name") or row.get("Kernel-Name") or ""
-                if kernel_sub not in name:
-                    continue
-                if (row.get("Counter_Name") or "") != counter:
-                    continue
-                key = row.get("Dispatch_Id") or row.get("Correlation_Id")
-                vals[key] = vals.get(key, 0.0) + float(row.get("Counter_Value") or 0)
+                name = row.get("Kernel_Name") or ""
+                if kernel_sub in name and (row.get("Counter_Name") or "") == counter:
+                    rows.append(row)
+    if not rows:
+        return []
+    gmax = max(int(r["Grid_Size"]) for r in rows)
+    vals = {}
+    for r in rows:
+        if int(r["Grid_Size"]) == gmax:
+            key = r.get("Dispatch_Id") or r.get("Correlation_Id")
+            vals[key] = vals.get(key, 0.0) + float(r.get("Counter_Value") or 0)
     return list(vals.values())
 
 
