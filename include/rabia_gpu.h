@@ -170,6 +170,22 @@ int rg_trace_generate_async(rg_ctx* ctx, int kind, uint64_t seed, uint64_t slot_
 int rg_digest_trace_async(rg_ctx* ctx, uint64_t seed, uint64_t slot_base, uint64_t n_slots,
                           uint64_t digest_stride, uint64_t* digests_dev, void* stream);
 
+/* Weak-MVC to termination, cluster view (config 3): every replica of each slot
+ * runs phase_rnd1/phase_rnd2 (weak_mvc.ivy:129-191) under a deterministic
+ * adversarial scheduler (each receiver hears itself + quorum-1 others chosen by
+ * a hash keyed by delivery_seed, slot, phase, round, receiver) with the common
+ * coin, until all replicas decided or max_phases (<= 255).
+ * states_dev: n planar planes (replica r's initial state bit), stride_words apart.
+ * info_dev[s] = decision (0 V0, 1 V1, 3 not all decided) | phases << 8 |
+ *               first decision phase << 16 | coin phases << 24.
+ * stats_dev (8 x u64, may be NULL): slots all decided, decided V1, sum of phases,
+ * max phases, sum of coin phases, sum of first-decision phases, slots, 0. */
+int rg_wmvc_cluster_async(rg_ctx* ctx, const uint32_t* states_dev, uint64_t stride_words,
+                          uint64_t n_slots, uint64_t slot_base, uint64_t delivery_seed,
+                          uint32_t max_phases, uint32_t* info_dev, uint64_t* stats_dev, void* stream);
+int rg_cluster_trace_async(rg_ctx* ctx, uint64_t seed, uint64_t slot_base, uint64_t n_slots,
+                           uint64_t stride_words, uint32_t* states_dev, void* stream);
+
 int rg_stream_sync(rg_ctx* ctx, void* stream);
 
 /* Host-side layout helpers (no device work). */

@@ -487,6 +487,106 @@ void or_digest_trace(int n, uint64_t seed, uint64_t slot_base, uint64_t S, uint6
   }
 }
 
+/* ------------------------------------------------------------------------- */
+/* WMVC cluster view (DESIGN.md §Spec "cluster"): every replica of one slot   */
+/* runs docs/weak_mvc.ivy phase_rnd1 / phase_rnd2 (ivy:129-191) each phase;  */
+/* in each round replica r hears exactly q messages: its own and q-1 of the  */
+/* other n-1, chosen by a keyed hash of (slot, phase, round, r) -- a          */
+/* deterministic adversarial scheduler. A decided replica keeps voting its   */
+/* decision (ivy:158-160). Runs until every replica decided or max_phases.   */
+/* ------------------------------------------------------------------------- */
+static uint64_t cluster_key(uint64_t seed, uint32_t phase, uint32_t round, int r) {
+  return mix64(seed ^ (((uint64_t)phase << 32) | ((uint64_t)round << 16) | (uint64_t)r) *
+                          0x9E6C63D0676A9A99ULL);
+}
+
+/* Bit mask (bit j = sender j heard) of receiver r's round `round` in `phase`:
+ * itself plus q-1 of the other senders; pick i takes the k-th (ascending) still
+ * available sender, k = 6-bit chunk i of one mix64 modulo the number left. */
+uint32_t or_heard(uint64_t delivery_seed, uint64_t slot, uint32_t phase, uint32_t round,
+                  int r, int n, int q) {
+  uint64_t h = mix64(cluster_key(delivery_seed, phase, round, r) + slot);
+  uint32_t avail = ((1u << n) - 1u) & ~(1u << r);
+  uint32_t mask = 1u << r;
+  for (int i = 0; i < q - 1; i++) {
+    int span = n - 1 - i;
+    int k = (int)((h >> (6 * i)) & 63u) % span;
+    uint32_t a = avail;
+    for (int t = 0; t < k; t++) a &= a - 1;
+    uint32_t pick = a & (~a + 1u);  /* lowest remaining set bit */
+    mask |= pick;
+    avail &= ~pick;
+  }
+  return mask;
+}
+
+int or_wmvc_cluster(int n, int q, int fp1, uint64_t coin_seed, uint64_t epoch,
+                    uint64_t delivery_seed, uint32_t max_phases, uint64_t slot_base,
+                    const uint8_t* states, uint64_t S, or_cluster_out* out) {
+  if (n < 1 || n > 16 || q < 1 || q > n || fp1 < 1 || max_phases < 1 || max_phases > 255) return -1;
+  uint32_t ckey[8];
+  or_seed_from_u64(coin_seed, ckey);
+  const uint32_t all = (n == 32) ? ~0u : ((1u << n) - 1u);
+  for (uint64_t s = 0; s < S; s++) {
+    const uint64_t id = slot_base + s;
+    uint32_t st = 0, decided = 0, decv = 0;  /* bit r: replica r's state / decided / decision */
+    for (int r = 0; r < n; r++) st |= (uint32_t)(states[s * n + r] & 1u) << r;
+    or_cluster_out o = {OR_NONE, 0, 0, 0};
+    for (uint32_t p = 1; p <= max_phases && decided != all; p++) {
+      /* round 1 (phase_rnd1): vote2 = v if all q heard states are v, else '?' */
+      uint32_t v1 = 0, vq = 0;  /* bit r: replica r votes V1 / '?' in round 2 */
+      for (int r = 0; r < n; r++) {
+        uint32_t h = or_heard(delivery_seed, id, p, 1, r, n, q);
+        int c1 = __builtin_popcount(h & st), c0 = __builtin_popcount(h & ~st);
+        if (c1 >= q) v1 |= 1u << r;
+        else if (c0 < q) vq |= 1u << r;
+      }
+      /* round 2 (phase_rnd2) */
+      uint32_t nst = 0;
+      int coin = -1;
+      for (int r = 0; r < n; r++) {
+        uint32_t h = or_heard(delivery_seed, id, p, 2, r, n, q);
+        int c1 = __builtin_popcount(h & v1), cq = __builtin_popcount(h & vq);
+        int c0 = q - c1 - cq;
+        int nv;
+        if (c0 >= fp1) nv = 0;
+        else if (c1 >= fp1) nv = 1;
+        else nv = -1;
+        if (nv >= 0 && !((decided >> r) & 1u)) {
+          decided |= 1u << r;
+          decv |= (uint32_t)nv << r;
+          if (!o.first) o.first = (uint8_t)p;
+        }
+        if (nv < 0) {
+          if (c0 > 0) nv = 0;
+          else if (c1 > 0) nv = 1;
+          else {
+            if (coin < 0) { coin = or_coin(ckey, epoch, id, p); o.coins++; }
+            nv = coin;
+          }
+        }
+        if ((decided >> r) & 1u) nv = (int)((decv >> r) & 1u);
+        nst |= (uint32_t)nv << r;
+      }
+      st = nst;
+      if (decided == all) o.phases = (uint8_t)p;
+    }
+    if (decided == all) o.dec = (uint8_t)(decv & 1u);  /* agreement: every decider decided decv bit 0's value */
+    out[s] = o;
+  }
+  return 0;
+}
+
+/* Initial states for the adversarial cluster trace (config 3): (n-1)/2 replicas
+ * hold 1, the rest 0, rotated per slot. */
+void or_cluster_trace(int n, uint64_t seed, uint64_t slot_base, uint64_t S, uint8_t* states) {
+  uint64_t krot = trace_key(seed, 4);
+  for (uint64_t s = 0; s < S; s++) {
+    uint32_t rot = (uint32_t)(mix64(krot + slot_base + s) % (uint64_t)n);
+    for (int r = 0; r < n; r++) states[s * n + r] = (uint8_t)(((uint32_t)r + rot) % (uint32_t)n < (uint32_t)(n - 1) / 2);
+  }
+}
+
 /* Bit-plane layout: plane 2j+b holds bit b of lane j's code;
  * slot s lives in word s/32, bit s%32. */
 void or_pack_planes(const uint8_t* codes, int n, uint64_t S, uint64_t stride,

@@ -69,6 +69,20 @@ void or_digest_majority(int n, int q, const uint64_t* digests /*[n][S]*/,
 void or_coin_range(uint64_t coin_seed, uint64_t epoch, uint64_t phase,
                    uint64_t slot_base, uint64_t S, uint8_t* out);
 
+/* --- WMVC cluster view: all n replicas of a slot, phases to termination ----- */
+typedef struct or_cluster_out {
+  uint8_t dec;        /* OR_V0 / OR_V1 / OR_NONE (not every replica decided)   */
+  uint8_t phases;     /* phase at which the last replica decided, 0 = none     */
+  uint8_t first;      /* phase of the first decision, 0 = none                 */
+  uint8_t coins;      /* phases in which some replica took the common coin     */
+} or_cluster_out;
+uint32_t or_heard(uint64_t delivery_seed, uint64_t slot, uint32_t phase, uint32_t round,
+                  int r, int n, int q);
+int or_wmvc_cluster(int n, int q, int fp1, uint64_t coin_seed, uint64_t epoch,
+                    uint64_t delivery_seed, uint32_t max_phases, uint64_t slot_base,
+                    const uint8_t* states /*[S][n]*/, uint64_t S, or_cluster_out* out);
+void or_cluster_trace(int n, uint64_t seed, uint64_t slot_base, uint64_t S, uint8_t* states);
+
 /* --- structure-faithful REF path (CPU baseline) ----------------------------- */
 int or_ref_structured(int n, int q, int self_lane, uint64_t seed, uint64_t rng_base,
                       uint64_t slot_base, const uint8_t* r1, const uint8_t* r2,

@@ -282,3 +282,81 @@ def trace(kind, n, seed, slot_base, S):
             rows.append(row)
         r1.append(rows[0]); r2.append(rows[1])
     return r1, r2, st
+
+
+def _cluster_key(seed, phase, rnd, r):
+    return _mix64(seed ^ ((((phase << 32) | (rnd << 16) | r) * 0x9E6C63D0676A9A99) & MASK64))
+
+
+def heard(delivery_seed, slot, phase, rnd, r, n, q):
+    """Receiver r hears itself and q-1 others (cluster view)."""
+    h = _mix64((_cluster_key(delivery_seed, phase, rnd, r) + slot) & MASK64)
+    avail = [j for j in range(n) if j != r]
+    mask = 1 << r
+    for i in range(q - 1):
+        span = n - 1 - i
+        k = ((h >> (6 * i)) & 63) % span
+        pick = avail.pop(k)
+        mask |= 1 << pick
+    return mask
+
+
+def wmvc_cluster(n, q, fp1, coin_seed, epoch, delivery_seed, max_phases, slot_base, states):
+    """Every replica of each slot runs weak_mvc.ivy phase_rnd1/phase_rnd2 until
+    all decided. Returns per slot (dec, phases, first, coins)."""
+    ckey = seed_from_u64(coin_seed)
+    outs = []
+    for s, row in enumerate(states):
+        sid = slot_base + s
+        st = list(row)
+        decided = [None] * n
+        o = [NONE, 0, 0, 0]
+        for p in range(1, max_phases + 1):
+            if all(d is not None for d in decided):
+                break
+            vote = []
+            for r in range(n):
+                h = heard(delivery_seed, sid, p, 1, r, n, q)
+                got = [st[j] for j in range(n) if (h >> j) & 1]
+                vote.append(1 if got.count(1) >= q else (0 if got.count(0) >= q else None))
+            coin_v = None
+            nst = []
+            for r in range(n):
+                h = heard(delivery_seed, sid, p, 2, r, n, q)
+                got = [vote[j] for j in range(n) if (h >> j) & 1]
+                c0, c1 = got.count(0), got.count(1)
+                nv = 0 if c0 >= fp1 else (1 if c1 >= fp1 else None)
+                if nv is not None and decided[r] is None:
+                    decided[r] = nv
+                    if not o[2]:
+                        o[2] = p
+                if nv is None:
+                    if c0 > 0:
+                        nv = 0
+                    elif c1 > 0:
+                        nv = 1
+                    else:
+                        if coin_v is None:
+                            coin_v = coin(ckey, epoch, sid, p)
+                            o[3] += 1
+                        nv = coin_v
+                if decided[r] is not None:
+                    nv = decided[r]
+                nst.append(nv)
+            st = nst
+            if all(d is not None for d in decided):
+                o[1] = p
+        if all(d is not None for d in decided):
+            assert len(set(decided)) == 1, "agreement violated"
+            o[0] = decided[0]
+        outs.append(tuple(o))
+    return outs
+
+
+def cluster_trace(n, seed, slot_base, S):
+    krot = _trace_key(seed, 4)
+    out = []
+    for s in range(S):
+        rot = _mix64((krot + slot_base + s) & MASK64) % n
+        out.append([1 if (r + rot) % n < (n - 1) // 2 else 0 for r in range(n)])
+    return out

@@ -65,6 +65,8 @@ _SIGS = {
     "rg_ref_draws_async": (ctypes.c_int, [vp, u64, u64, vp, vp]),
     "rg_trace_generate_async": (ctypes.c_int, [vp, ctypes.c_int, u64, u64, u64, u64, vp, vp]),
     "rg_digest_trace_async": (ctypes.c_int, [vp, u64, u64, u64, u64, vp, vp]),
+    "rg_wmvc_cluster_async": (ctypes.c_int, [vp, vp, u64, u64, u64, u64, u32, vp, vp, vp]),
+    "rg_cluster_trace_async": (ctypes.c_int, [vp, u64, u64, u64, u64, vp, vp]),
     "rg_stream_sync": (ctypes.c_int, [vp, vp]),
     "rg_pack_codes": (ctypes.c_int, [vp, u32, u64, u64, vp]),
     "rg_unpack_planes": (ctypes.c_int, [vp, u32, u64, u64, vp]),

@@ -38,6 +38,8 @@ struct rg_ctx {
   uint32_t diag = 0;
   unsigned long long* dbg = nullptr;
   uint64_t dbg_cap = 0;
+  unsigned long long* cluster_part = nullptr;  // [blocks][kClusterStats]
+  unsigned long long* cluster_stats = nullptr;  // [kClusterStats]
   std::string err;
 };
 
@@ -97,7 +99,16 @@ struct Disp {
                      uint64_t n, uint32_t q) {
     hipLaunchKernelGGL((digest_kernel<N>), dim3(grid), dim3(kBlock), 0, s, dg, ds, out, n, q);
   }
+  static void cluster(uint32_t grid, hipStream_t s, const uint32_t* st, uint64_t stride, uint64_t n_slots,
+                      uint64_t base, uint32_t q, uint32_t fp1, Key key, uint64_t cs, uint64_t dseed,
+                      uint32_t maxp, uint32_t* info, unsigned long long* part) {
+    hipLaunchKernelGGL((wmvc_cluster_kernel<N>), dim3(grid), dim3(256), 0, s, st, stride, n_slots, base, q, fp1,
+                       key, cs, dseed, maxp, info, part);
+  }
 };
+
+using ClusterLaunch = void (*)(uint32_t, hipStream_t, const uint32_t*, uint64_t, uint64_t, uint64_t, uint32_t,
+                               uint32_t, Key, uint64_t, uint64_t, uint32_t, uint32_t*, unsigned long long*);
 
 using DigestLaunch = void (*)(uint32_t, hipStream_t, const uint64_t*, uint64_t, uint32_t*, uint64_t,
                               uint32_t);
@@ -110,6 +121,7 @@ using DigestLaunch = void (*)(uint32_t, hipStream_t, const uint64_t*, uint64_t, 
 const StepLaunch kRefLaunch[17] = RG_TABLE(ref);
 const StepLaunch kWmvcLaunch[17] = RG_TABLE(wmvc);
 const DigestLaunch kDigestLaunch[17] = RG_TABLE(digest);
+const ClusterLaunch kClusterLaunch[17] = RG_TABLE(cluster);
 
 hipStream_t pick_stream(rg_ctx* ctx, void* stream) {
   return stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
@@ -263,6 +275,8 @@ int rg_destroy(rg_ctx* ctx) {
   (void)hipFree(ctx->lookback);
   (void)hipFree(ctx->stats);
   (void)hipFree(ctx->dbg);
+  (void)hipFree(ctx->cluster_part);
+  (void)hipFree(ctx->cluster_stats);
   (void)hipFree(ctx->d_votes);
   (void)hipFree(ctx->d_out);
   (void)hipFree(ctx->d_user_result);
@@ -358,6 +372,8 @@ int rg_phase_step_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_de
     if (ctx->dbg_cap < n_tiles * 8) {
       RG_HIP(ctx, hipDeviceSynchronize());
       (void)hipFree(ctx->dbg);
+  (void)hipFree(ctx->cluster_part);
+  (void)hipFree(ctx->cluster_stats);
       ctx->dbg = nullptr;
       RG_HIP(ctx, hipMalloc(&ctx->dbg, n_tiles * 8 * 8));
       ctx->dbg_cap = n_tiles * 8;
@@ -480,6 +496,44 @@ int rg_digest_trace_async(rg_ctx* ctx, uint64_t seed, uint64_t slot_base, uint64
   hipLaunchKernelGGL(digest_trace_kernel, dim3((uint32_t)((n_slots + 255) / 256)), dim3(256), 0,
                      pick_stream(ctx, stream), (int)ctx->cfg.n_replicas, seed, slot_base, n_slots,
                      digest_stride, reinterpret_cast<unsigned long long*>(digests_dev));
+  RG_HIP(ctx, hipGetLastError());
+  return RG_OK;
+}
+
+int rg_wmvc_cluster_async(rg_ctx* ctx, const uint32_t* states_dev, uint64_t stride_words, uint64_t n_slots,
+                          uint64_t slot_base, uint64_t delivery_seed, uint32_t max_phases, uint32_t* info_dev,
+                          uint64_t* stats_dev, void* stream) {
+  if (!ctx || !states_dev || !info_dev || n_slots == 0) return fail(ctx, RG_EINVAL, "rg_wmvc_cluster: bad argument");
+  if (stride_words < (n_slots + 31) / 32) return fail(ctx, RG_EINVAL, "rg_wmvc_cluster: stride too small");
+  if (max_phases < 1 || max_phases > 255) return fail(ctx, RG_EINVAL, "rg_wmvc_cluster: max_phases must be 1..255");
+  if (slot_base + n_slots > (1ull << 49)) return fail(ctx, RG_EINVAL, "rg_wmvc_cluster: slot ids must be < 2^49");
+  RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
+  constexpr uint32_t kGrid = 2048;
+  const uint64_t need = (n_slots + 255) / 256;
+  const uint32_t grid = (uint32_t)(need < kGrid ? need : kGrid);
+  if (!ctx->cluster_part) {
+    RG_HIP(ctx, hipMalloc(&ctx->cluster_part, (uint64_t)kGrid * kClusterStats * 8));
+    RG_HIP(ctx, hipMalloc(&ctx->cluster_stats, kClusterStats * 8));
+  }
+  hipStream_t s = pick_stream(ctx, stream);
+  kClusterLaunch[ctx->cfg.n_replicas](grid, s, states_dev, stride_words, n_slots, slot_base, ctx->q, ctx->fp1,
+                                      ctx->coin_key, ctx->coin_stream, delivery_seed, max_phases, info_dev,
+                                      ctx->cluster_part);
+  unsigned long long* dst = stats_dev ? reinterpret_cast<unsigned long long*>(stats_dev) : ctx->cluster_stats;
+  hipLaunchKernelGGL(cluster_stats_kernel, dim3(1), dim3(64), 0, s, ctx->cluster_part, grid, dst);
+  RG_HIP(ctx, hipGetLastError());
+  return RG_OK;
+}
+
+int rg_cluster_trace_async(rg_ctx* ctx, uint64_t seed, uint64_t slot_base, uint64_t n_slots, uint64_t stride_words,
+                           uint32_t* states_dev, void* stream) {
+  if (!ctx || !states_dev || n_slots == 0 || stride_words < (n_slots + 31) / 32)
+    return fail(ctx, RG_EINVAL, "rg_cluster_trace: bad argument");
+  RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
+  const uint64_t n_words = (n_slots + 31) / 32;
+  hipLaunchKernelGGL(cluster_trace_kernel, dim3((uint32_t)((n_words + 255) / 256)), dim3(256), 0,
+                     pick_stream(ctx, stream), (int)ctx->cfg.n_replicas, seed, slot_base, n_slots, stride_words,
+                     states_dev);
   RG_HIP(ctx, hipGetLastError());
   return RG_OK;
 }

@@ -941,6 +941,153 @@ __global__ void digest_trace_kernel(int n, uint64_t seed, uint64_t slot_base, ui
   }
 }
 
+// ============================================================================
+// WMVC cluster view (config 3): all n replicas of a slot run weak_mvc.ivy
+// phase_rnd1 / phase_rnd2 (ivy:129-191) phase after phase, under a deterministic
+// adversarial scheduler (each receiver hears itself + q-1 others picked by a keyed
+// hash), until every replica decided or max_phases. One lane per slot; replica
+// sets are n-bit masks, so each round is popcounts. Restated in
+// oracle/rabia_oracle.c:or_wmvc_cluster.
+// ============================================================================
+__device__ __forceinline__ uint64_t cluster_key(uint64_t seed, uint32_t phase, uint32_t round, int r) {
+  return mix64(seed ^ (((uint64_t)phase << 32) | ((uint64_t)round << 16) | (uint64_t)r) *
+                          0x9E6C63D0676A9A99ull);
+}
+
+template <int N>
+__device__ __forceinline__ uint32_t heard_mask(uint64_t dseed, uint64_t slot, uint32_t phase, uint32_t round,
+                                               int r, uint32_t q) {
+  const uint64_t h = mix64(cluster_key(dseed, phase, round, r) + slot);
+  uint32_t avail = ((1u << N) - 1u) & ~(1u << r);
+  uint32_t mask = 1u << r;
+  for (uint32_t i = 0; i + 1 < q; i++) {
+    const uint32_t span = N - 1 - i;
+    const uint32_t k = (uint32_t)((h >> (6 * i)) & 63u) % span;
+    uint32_t a = avail;
+    for (uint32_t t = 0; t < k; t++) a &= a - 1;
+    const uint32_t pick = a & (~a + 1u);
+    mask |= pick;
+    avail &= ~pick;
+  }
+  return mask;
+}
+
+constexpr int kClusterStats = 8;  // all_decided, v1, sum_phases, max_phases, sum_coin_phases, sum_first, slots, -
+
+template <int N>
+__global__ __launch_bounds__(256) void wmvc_cluster_kernel(const uint32_t* states, uint64_t stride, uint64_t n_slots,
+                                                           uint64_t slot_base, uint32_t q, uint32_t fp1, Key ckey,
+                                                           uint64_t coin_stream, uint64_t dseed, uint32_t max_phases,
+                                                           uint32_t* info, unsigned long long* partials) {
+  constexpr uint32_t kAll = (1u << N) - 1u;
+  unsigned long long acc[kClusterStats] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s < n_slots; s += (uint64_t)gridDim.x * 256) {
+    const uint64_t id = slot_base + s;
+    uint32_t st = 0;
+#pragma unroll
+    for (int r = 0; r < N; r++) st |= ((states[(uint64_t)r * stride + s / 32] >> (s & 31)) & 1u) << r;
+    uint32_t decided = 0, decv = 0, phases = 0, first = 0, coins = 0;
+    for (uint32_t p = 1; p <= max_phases && decided != kAll; p++) {
+      uint32_t v1 = 0, vq = 0;  // round 1 (phase_rnd1): unanimous heard states -> vote, else '?'
+#pragma unroll
+      for (int r = 0; r < N; r++) {
+        const uint32_t h = heard_mask<N>(dseed, id, p, 1, r, q);
+        const uint32_t c1 = __builtin_popcount(h & st), c0 = __builtin_popcount(h & ~st);
+        if (c1 >= q) v1 |= 1u << r;
+        else if (c0 < q) vq |= 1u << r;
+      }
+      uint32_t nst = 0;
+      int coin = -1;
+#pragma unroll
+      for (int r = 0; r < N; r++) {  // round 2 (phase_rnd2): f+1 decide / adopt / common coin
+        const uint32_t h = heard_mask<N>(dseed, id, p, 2, r, q);
+        const uint32_t c1 = __builtin_popcount(h & v1), cq = __builtin_popcount(h & vq);
+        const uint32_t c0 = q - c1 - cq;
+        int nv = c0 >= fp1 ? 0 : (c1 >= fp1 ? 1 : -1);
+        if (nv >= 0 && !((decided >> r) & 1u)) {
+          decided |= 1u << r;
+          decv |= (uint32_t)nv << r;
+          if (!first) first = p;
+        }
+        if (nv < 0) {
+          if (c0 > 0) nv = 0;
+          else if (c1 > 0) nv = 1;
+          else {
+            if (coin < 0) {
+              uint32_t blk[16];
+              chacha_block<12>(ckey, ((uint64_t)(p - 1) << 40) | (id >> 9), coin_stream, blk);
+              coin = (int)((select16(blk, (uint32_t)(id >> 5) & 15u) >> (id & 31)) & 1u);
+              coins++;
+            }
+            nv = coin;
+          }
+        }
+        if ((decided >> r) & 1u) nv = (int)((decv >> r) & 1u);
+        nst |= (uint32_t)nv << r;
+      }
+      st = nst;
+      if (decided == kAll) phases = p;
+    }
+    const uint32_t dec = decided == kAll ? (decv & 1u) : kCodeNone;
+    info[s] = dec | (phases << 8) | (first << 16) | (coins << 24);
+    acc[0] += decided == kAll;
+    acc[1] += dec == kCodeV1;
+    acc[2] += phases;
+    acc[3] = phases > acc[3] ? phases : acc[3];
+    acc[4] += coins;
+    acc[5] += first;
+    acc[6] += 1;
+  }
+  __shared__ unsigned long long red[4][kClusterStats];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < kClusterStats; k++) acc[k] = k == 3 ? wave_max64(acc[k]) : wave_sum64(acc[k]);
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < kClusterStats; k++) red[wave][k] = acc[k];
+  lds_barrier();
+  if (threadIdx.x < kClusterStats) {
+    const int k = threadIdx.x;
+    unsigned long long v = 0;
+    for (int w = 0; w < 4; w++) v = k == 3 ? (red[w][k] > v ? red[w][k] : v) : v + red[w][k];
+    partials[(uint64_t)blockIdx.x * kClusterStats + k] = v;  // plain stores: folded by the next launch
+  }
+}
+
+__global__ void cluster_stats_kernel(const unsigned long long* partials, uint32_t nblocks, unsigned long long* out) {
+  const int k = threadIdx.x;
+  if (k >= kClusterStats) return;
+  unsigned long long v = 0;
+  for (uint32_t b = 0; b < nblocks; b++) {
+    const unsigned long long x = partials[(uint64_t)b * kClusterStats + k];
+    v = k == 3 ? (x > v ? x : v) : v + x;
+  }
+  out[k] = v;
+}
+
+// Initial states of the adversarial cluster trace (restated in or_cluster_trace).
+__global__ void cluster_trace_kernel(int n, uint64_t seed, uint64_t slot_base, uint64_t n_slots, uint64_t stride,
+                                     uint32_t* states) {
+  const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t n_words = (n_slots + 31) / 32;
+  if (w >= n_words) return;
+  const uint64_t krot = trace_key(seed, 4);
+  const uint32_t vm = valid_mask(w, n_words, n_slots);
+  uint32_t planes[kMaxReplicas];
+#pragma unroll
+  for (int r = 0; r < kMaxReplicas; r++) planes[r] = 0;
+  for (int b = 0; b < 32; b++) {
+    if (!((vm >> b) & 1u)) break;
+    const uint32_t rot = (uint32_t)(mix64(krot + slot_base + 32 * w + b) % (uint64_t)n);
+#pragma unroll
+    for (int r = 0; r < kMaxReplicas; r++)
+      if (r < n && ((uint32_t)r + rot) % (uint32_t)n < (uint32_t)(n - 1) / 2) planes[r] |= 1u << b;
+  }
+#pragma unroll
+  for (int r = 0; r < kMaxReplicas; r++)
+    if (r < n) states[(uint64_t)r * stride + w] = planes[r];
+}
+
 // Diagnostic: the REF kernel's memory pattern with no protocol (reads NIN planes,
 // writes NOUT planes of XOR mixes). The achievable-bandwidth reference for it.
 // T = 0: planar planes `stride` words apart; T > 0: slot-tiled, the planes of a

@@ -272,5 +272,14 @@ class PhaseEvaluator:
         N.check(self.lib.rg_digest_trace_async(self.ctx, seed, slot_base, n_slots, digest_stride,
                                                digests_ptr, stream or None), self.ctx)
 
+    def wmvc_cluster_async(self, states_ptr, stride, n_slots, slot_base, delivery_seed, max_phases,
+                           info_ptr, stats_ptr=0, stream=0):
+        N.check(self.lib.rg_wmvc_cluster_async(self.ctx, states_ptr, stride, n_slots, slot_base, delivery_seed,
+                                               max_phases, info_ptr, stats_ptr or None, stream or None), self.ctx)
+
+    def cluster_trace_async(self, seed, slot_base, n_slots, stride, states_ptr, stream=0):
+        N.check(self.lib.rg_cluster_trace_async(self.ctx, seed, slot_base, n_slots, stride, states_ptr,
+                                                stream or None), self.ctx)
+
     def sync(self, stream=0):
         N.check(self.lib.rg_stream_sync(self.ctx, stream or None), self.ctx)

@@ -180,3 +180,30 @@ def count_votes_table(n, q):
     cv = np.array([lib.or_count_votes(_p(codes[k], u8p), n, q) for k in range(N)], np.uint8)
     r1 = np.array([lib.or_ref_round1(_p(codes[k], u8p), n, q) for k in range(N)], np.uint8)
     return codes, cv, r1
+
+
+class ClusterOut(ctypes.Structure):
+    _fields_ = [("dec", ctypes.c_uint8), ("phases", ctypes.c_uint8), ("first", ctypes.c_uint8),
+                ("coins", ctypes.c_uint8)]
+
+
+def wmvc_cluster(n, q, fp1, coin_seed, epoch, delivery_seed, max_phases, slot_base, states):
+    """Returns uint32 info per slot packed like the device (dec | phases<<8 | first<<16 | coins<<24)."""
+    lib = load()
+    lib.or_wmvc_cluster.argtypes = [i, i, i, u64, u64, u64, ctypes.c_uint32, u64, u8p, u64,
+                                    ctypes.POINTER(ClusterOut)]
+    S = states.shape[0]
+    out = (ClusterOut * S)()
+    rc = lib.or_wmvc_cluster(n, q, fp1, coin_seed, epoch, delivery_seed, max_phases, slot_base,
+                             _p(np.ascontiguousarray(states, np.uint8), u8p), S, out)
+    assert rc == 0
+    raw = np.frombuffer(out, dtype=np.uint8).reshape(S, 4).astype(np.uint32)
+    return raw[:, 0] | (raw[:, 1] << 8) | (raw[:, 2] << 16) | (raw[:, 3] << 24)
+
+
+def cluster_trace(n, seed, slot_base, S):
+    lib = load()
+    lib.or_cluster_trace.argtypes = [i, u64, u64, u64, u8p]
+    st = np.zeros((S, n), np.uint8)
+    lib.or_cluster_trace(n, seed, slot_base, S, _p(st, u8p))
+    return st

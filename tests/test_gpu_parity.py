@@ -342,3 +342,34 @@ def test_device_tiled_generator_matches_planar(oracle):
     r1, r2, st = oracle.trace(1, n, 5, 1, S)
     np.testing.assert_array_equal(planar[: 2 * n], oracle.pack_planes(r1, nw))
     np.testing.assert_array_equal(planar[2 * n: 4 * n], oracle.pack_planes(r2, nw))
+
+
+@pytest.mark.parametrize("n", [3, 5, 7, 9, 16])
+def test_wmvc_cluster_vs_oracle(oracle, golden, n):
+    """Weak-MVC to termination over all replicas of each slot (config 3)."""
+    torch = torch_cuda()
+    q, fp1 = n // 2 + 1, (n - 1) // 2 + 1
+    S = 50_001
+    stride = ((S + 127) // 128) * 4
+    states = torch.zeros(n * stride, dtype=torch.int32, device="cuda")
+    info = torch.zeros(S, dtype=torch.int32, device="cuda")
+    stats = torch.zeros(8, dtype=torch.int64, device="cuda")
+    with PhaseEvaluator(n, mode="wmvc", coin_seed=7, epoch=3) as ev:
+        ev.cluster_trace_async(42, 1, S, stride, states.data_ptr())
+        ev.wmvc_cluster_async(states.data_ptr(), stride, S, 1, 99, 32, info.data_ptr(), stats.data_ptr())
+        ev.sync()
+    st = oracle.cluster_trace(n, 42, 1, S)
+    planes = states.view(n, stride).cpu().numpy().view(np.uint32)
+    for r in range(n):
+        bits = np.unpackbits(planes[r].view(np.uint8), bitorder="little")[:S]
+        np.testing.assert_array_equal(bits, st[:, r])
+    exp = oracle.wmvc_cluster(n, q, fp1, 7, 3, 99, 32, 1, st)
+    got = info.cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(got, exp)
+    sv = stats.cpu().numpy().view(np.uint64)
+    dec = exp & 255
+    assert sv[0] == (dec != 3).sum() and sv[1] == (dec == 1).sum()
+    assert sv[2] == ((exp >> 8) & 255).sum() and sv[3] == ((exp >> 8) & 255).max() and sv[6] == S
+    if n in (3, 5, 7):
+        g = golden(f"cluster_n{n}.npz")
+        np.testing.assert_array_equal(got[: g["info"].shape[0]], g["info"])

@@ -153,3 +153,31 @@ def test_oracle_sanitized():
                        timeout=300)
     assert p.returncode == 0, p.stderr[-2000:]
     assert "selftest ok" in p.stdout
+
+
+@pytest.mark.parametrize("n", [3, 5, 7])
+def test_cluster_fixture(oracle, golden, n):
+    """Weak-MVC to termination (cluster view): C restatement == Python fixture."""
+    g = golden(f"cluster_n{n}.npz")
+    p = json.loads(str(g["params"]))
+    st = oracle.cluster_trace(n, 42, p["slot_base"], g["states"].shape[0])
+    np.testing.assert_array_equal(st, g["states"])
+    info = oracle.wmvc_cluster(n, p["q"], p["fp1"], p["coin_seed"], p["epoch"], p["delivery_seed"],
+                               p["max_phases"], p["slot_base"], g["states"])
+    np.testing.assert_array_equal(info, g["info"])
+    phases = (info >> 8) & 255
+    assert (info & 255 != 3).all() and phases.max() >= 3  # multi-round coin phases occur
+
+
+def test_cluster_safety_and_validity():
+    """Agreement (asserted inside the restatement) and validity over random and
+    unanimous initial states (weak_mvc.ivy invariants decision_bc_same_round_agree,
+    vl_decision_bc_agree)."""
+    rng = np.random.default_rng(11)
+    for n in (3, 4, 5, 6, 9):
+        q, fp1 = n // 2 + 1, (n - 1) // 2 + 1
+        st = rng.integers(0, 2, (300, n)).tolist()
+        R.wmvc_cluster(n, q, fp1, 1, 0, 5, 64, 1, st)
+        for v in (0, 1):
+            outs = R.wmvc_cluster(n, q, fp1, 1, 0, 5, 64, 1, [[v] * n] * 50)
+            assert all(o[0] == v and o[1] == 1 for o in outs)

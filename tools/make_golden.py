@@ -137,9 +137,26 @@ def digests():
         print("wrote digest", n, sum(st))
 
 
+def clusters():
+    """WMVC cluster view to termination (config 3 shape), Python restatement."""
+    for n, S in ((5, 2048), (7, 1024), (3, 1024)):
+        q, fp1 = n // 2 + 1, (n - 1) // 2 + 1
+        st = R.cluster_trace(n, 42, 1, S)
+        outs = R.wmvc_cluster(n, q, fp1, 7, 3, 99, 32, 1, st)
+        info = np.array([o[0] | (o[1] << 8) | (o[2] << 16) | (o[3] << 24) for o in outs], np.uint32)
+        np.savez_compressed(os.path.join(GOLD, f"cluster_n{n}.npz"), states=np.array(st, np.uint8),
+                            info=info, params=json.dumps(dict(n=n, q=q, fp1=fp1, coin_seed=7, epoch=3,
+                                                              delivery_seed=99, max_phases=32, slot_base=1)))
+        print("wrote cluster", n, "mean phases", float(np.mean([o[1] for o in outs])))
+
+
 if __name__ == "__main__":
     os.makedirs(GOLD, exist_ok=True)
+    if sys.argv[1:] == ["clusters"]:
+        clusters()
+        sys.exit(0)
     truth_tables()
     traces()
     coins_and_draws()
     digests()
+    clusters()
