@@ -69,9 +69,9 @@ constexpr int wmax_for(int n) { return n <= 5 ? 4 : (n <= 10 ? 2 : 1); }
 // Tile shapes: {threads, words per thread}. Big tiles keep the per-launch count
 // of tile tickets and look-back hand-offs low on large windows; small tiles fill
 // the 256 CUs on single 2^20-slot windows.
-enum TileCfg { kCfgBig = 0, kCfgMid = 1, kCfgSmall = 2 };
-constexpr int cfg_block(int c) { return c == kCfgBig ? 512 : (c == kCfgMid ? 256 : 128); }
-inline int cfg_words(int c, int n) { return c == kCfgSmall ? 1 : wmax_for(n); }
+enum TileCfg { kCfgBig = 0, kCfgMid = 1, kCfgSmall = 2, kCfgBigW2 = 3, kCfgMidW2 = 4 };
+constexpr int cfg_block(int c) { return (c == kCfgBig || c == kCfgBigW2) ? 512 : (c == kCfgSmall ? 128 : 256); }
+inline int cfg_words(int c, int n) { return c == kCfgSmall ? 1 : (c >= kCfgBigW2 ? 2 : wmax_for(n)); }
 
 int pick_cfg(int n, uint64_t n_words) {
   const uint64_t wm = (uint64_t)wmax_for(n);
@@ -86,6 +86,16 @@ template <int N>
 struct Disp {
   static constexpr int WM = wmax_for(N);
   static void ref(int c, uint32_t grid, hipStream_t s, const StepParams& p) {
+    if constexpr (N == 5) {  // diagnostic shapes (rg_debug_set force 4, 5): 2 words per thread
+      if (c == kCfgBigW2) {
+        hipLaunchKernelGGL((ref_step_kernel<N, 2, 512>), dim3(grid), dim3(512), 0, s, p);
+        return;
+      }
+      if (c == kCfgMidW2) {
+        hipLaunchKernelGGL((ref_step_kernel<N, 2, 256>), dim3(grid), dim3(256), 0, s, p);
+        return;
+      }
+    }
     if (c == kCfgBig) hipLaunchKernelGGL((ref_step_kernel<N, WM, 512>), dim3(grid), dim3(512), 0, s, p);
     else if (c == kCfgMid) hipLaunchKernelGGL((ref_step_kernel<N, WM, 256>), dim3(grid), dim3(256), 0, s, p);
     else hipLaunchKernelGGL((ref_step_kernel<N, 1, 128>), dim3(grid), dim3(128), 0, s, p);
@@ -334,7 +344,8 @@ int rg_phase_step_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_de
   uint64_t need_in, need_out;
   if (int rc = make_layout(ctx, 4 * n + 1, n_words, stride_words, &lin, &need_in, "rg_phase_step")) return rc;
   if (int rc = make_layout(ctx, kOutPlanes, n_words, stride_words, &lout, &need_out, "rg_phase_step")) return rc;
-  const uint32_t force = (ctx->diag >> 8) & 3u;  // diagnostics: force a tile shape
+  uint32_t force = (ctx->diag >> 8) & 7u;  // diagnostics: force a tile shape
+  if (force > 3 && (n != 5 || wmvc)) force = 0;
   const int cfg = force ? (int)force - 1 : pick_cfg(n, n_words);
   const uint64_t tile_words = (uint64_t)cfg_block(cfg) * cfg_words(cfg, n);
   const uint64_t n_tiles = (n_words + tile_words - 1) / tile_words;
@@ -372,8 +383,6 @@ int rg_phase_step_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_de
     if (ctx->dbg_cap < n_tiles * 8) {
       RG_HIP(ctx, hipDeviceSynchronize());
       (void)hipFree(ctx->dbg);
-  (void)hipFree(ctx->cluster_part);
-  (void)hipFree(ctx->cluster_stats);
       ctx->dbg = nullptr;
       RG_HIP(ctx, hipMalloc(&ctx->dbg, n_tiles * 8 * 8));
       ctx->dbg_cap = n_tiles * 8;

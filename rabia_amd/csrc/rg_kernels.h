@@ -9,7 +9,7 @@
 // REF mode needs, per VQ slot, the index of its StdRng draw = number of VQ slots
 // before it in ascending slot order (engine.rs:567-611 consumes the engine's one
 // RNG stream). That is an exclusive prefix sum across the launch, done in the
-// same pass by a decoupled look-back over dynamically ticketed tiles.
+// same pass by a decoupled look-back over tiles in blockIdx order.
 #pragma once
 
 #include "rg_common.h"
@@ -218,9 +218,11 @@ __device__ __forceinline__ void lds_barrier() {
 // Granule = {tag:32 | value:32}, tag = seq<<1 | inclusive, written by ONE 8-B
 // agent-scope store and read by agent-scope loads (MI355X_MICROARCH.md,
 // visibility: "R2" granules need no separate flag or fence). seq changes every
-// launch, so the array is never re-zeroed. Tickets are handed out in dispatch
-// order, so every predecessor is already resident: the spin terminates. It is
-// still bounded; a timeout raises Record.error and the step reports RG_ESTATE.
+// launch, so the array is never re-zeroed. Tiles are blockIdx.x: workgroups
+// are dispatched in blockIdx order on each XCD, so the lowest unfinished tile is
+// always resident and every wait terminates (ticket atomics on one address
+// serialise at ~12 ns each: measured slower). The spin is still bounded; a
+// timeout raises Record.error and the step reports RG_ESTATE.
 __device__ __forceinline__ uint32_t lookback_exclusive(unsigned long long* status, uint32_t tile,
                                                        uint32_t seq, uint32_t agg, int lane,
                                                        unsigned long long* err) {
@@ -271,7 +273,7 @@ __device__ __forceinline__ uint32_t lookback_exclusive(unsigned long long* statu
 //   4 (largest V1 slot offset in the tile that commit_phase accepts) + 1, 0 = none,
 //   5 smallest undecided slot offset in the tile, ~0 = none.
 // One lane writes them with 8-B agent-scope stores; the tile with the last
-// ticket polls and folds them. No per-tile atomics on shared words: thousands of
+// tile index polls and folds them. No per-tile atomics on shared words: thousands of
 // same-address atomics per launch serialise at the memory side.
 constexpr int kStatGranules = 8;
 constexpr uint32_t kSpinLimit = 1u << 24;
@@ -347,7 +349,7 @@ __device__ __forceinline__ void block_reduce_totals(unsigned long long (&v)[7], 
   for (int k = 0; k < 7; k++) v[k] = r[k];
 }
 
-// Publish this tile's statistics; the tile holding the last ticket folds every
+// Publish this tile's statistics; the tile with the last index folds every
 // tile's granules, advances the device engine state and writes the step result.
 template <bool IS_REF, int BLOCK, int W>
 __device__ __forceinline__ void finish_tile(const StepParams& p, Record* rec, TileStats ts,
@@ -477,14 +479,11 @@ template <int N, int W, int BLOCK>
 __global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
   constexpr int B = ctr_bits(N);
   constexpr int WAVES = BLOCK / 64;
-  __shared__ uint32_t s_ticket;
   __shared__ uint32_t s_wave[WAVES];
   __shared__ uint32_t s_excl;
   Record* rec = p.rec + (p.seq & 1u);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid == 0) s_ticket = (uint32_t)atomicAdd(&rec->ticket.v, 1ull);
-  lds_barrier();
-  const uint32_t tile = s_ticket;
+  const uint32_t tile = blockIdx.x;
   if (!tile_prologue(p, rec, tile, tid)) return;
   stamp(p, tile, 0, tid);
   const uint32_t tw0 = (uint32_t)tid * W;  // word offset inside the tile

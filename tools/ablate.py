@@ -44,6 +44,10 @@ torch.cuda.synchronize()
 
 
 def run(variant, k):
+    if variant.get("tiled") and variant.get("probe"):
+        v, o = tiled_sets[k % 3]
+        N.check(lib.rg_debug_stream_probe(v.data_ptr(), o.data_ptr(), S // 32, 0, T, 1, sp))
+        return
     if variant.get("tiled"):
         v, o = tiled_sets[k % 3]
         lib.rg_debug_set(ev_t.ctx, variant.get("diag", 0))
@@ -60,11 +64,18 @@ def run(variant, k):
 
 
 variants = {
-    "ref": {}, "ref_padstride": {"stride": "pad"}, "ref_mid": {"diag": 2 << 8},
-    "tiled1024": {"tiled": True}, "tiled1024_mid": {"tiled": True, "diag": 2 << 8},
-    "tiled1024_nolb_nofin": {"tiled": True, "diag": 3}, "tiled1024_1M": {"tiled": True, "slots": 1 << 20}, "no_lookback": {"diag": 1}, "no_finish": {"diag": 2},
-    "no_lookback_no_finish": {"diag": 3}, "probe": {"probe": True}, "probe_padstride": {"probe": True, "stride": "pad"},
-    "ref_1M": {"slots": 1 << 20}, "no_lb_no_fin_1M": {"slots": 1 << 20, "diag": 3}, "probe_1M": {"probe": True, "slots": 1 << 20},
+    "big": {"tiled": True, "diag": 1 << 8},
+    "mid": {"tiled": True, "diag": 2 << 8},
+    "big_w2": {"tiled": True, "diag": 4 << 8},
+    "mid_w2": {"tiled": True, "diag": 5 << 8},
+    "small": {"tiled": True, "diag": 3 << 8},
+    "big_nolb": {"tiled": True, "diag": 1 | (1 << 8)},
+    "big_nofin": {"tiled": True, "diag": 2 | (1 << 8)},
+    "big_nolb_nofin": {"tiled": True, "diag": 3 | (1 << 8)},
+    "mid_w2_nolb_nofin": {"tiled": True, "diag": 3 | (5 << 8)},
+    "t_probe": {"tiled": True, "probe": True},
+    "auto_1M": {"tiled": True, "slots": 1 << 20},
+    "planar_1M": {"slots": 1 << 20},
 }
 times = {k: [] for k in variants}
 for r in range(8):
