@@ -3,7 +3,7 @@
 
 Workload (BASELINE.json configs[1], "C2"): 5 replicas, windows of 2^20 slots,
 90%-agreement synthetic vote trace, REF single phase sweep. One bench "step" is
-one launch over `--windows` consecutive 2^20-slot windows (default 64: the
+one launch over `--windows` consecutive 2^20-slot windows (default 256: the
 steady-state streaming batch; --windows 1 is the single-sweep latency case and is
 also reported as `sweep_1m_us`). Inputs are generated on the device before the
 timed region and rotate over 3 buffer sets (> 2x the 256 MiB Infinity Cache) so
@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--windows", type=int, default=64)
+    ap.add_argument("--windows", type=int, default=256)
     ap.add_argument("--replicas", type=int, default=5)
     ap.add_argument("--sets", type=int, default=3)
     ap.add_argument("--tile-words", type=int, default=1024,
