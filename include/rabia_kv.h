@@ -1,0 +1,118 @@
+/*
+ * rabia_kv.h — C ABI of the device-resident kvstore apply.
+ *
+ * After a phase step (rabia_gpu.h) the V1-decided slots' batches are applied to
+ * the replicated state machine in total order (ascending slot, then command order
+ * inside the batch): engine.rs:646-655 (proposer) and 727-735 (follower) call
+ * StateMachine::apply_commands, which for the kvstore example is
+ * KVStoreSMR::apply_commands (examples/kvstore_smr/src/smr_impl.rs:72-127) over
+ * KVStore::set/get/delete/exists (examples/kvstore_smr/src/store.rs:144-262).
+ * The store lives in HBM: an open-addressing table of keys plus a byte heap of key
+ * and value bytes; commands arrive as their Command.data bytes (bincode 1.3.3 of
+ * KVOperation, operations.rs:10-19) and are decoded on the device.
+ *
+ * Same conventions as rabia_gpu.h: plain C types, streams as void* (NULL = the
+ * store's own stream), RG_OK (0) or a negative rg_status, rg_kv_last_error() for
+ * the text, no CPU fallback (rg_kv_create fails with RG_ENODEV without gfx950).
+ *
+ * Result codes, one byte per command (KVResult, operations.rs:55-63, and
+ * StoreError, operations.rs:97-108):
+ *   0 Success   1 NotFound   2 Error(InvalidKey "Key cannot be empty")
+ *   3 Error(InvalidKey "Key too long")   4 Error(ValueTooLarge)   5 Error(StoreFull)
+ *   6 Command.data is not a bincode KVOperation   7 not applied (slot not decided V1)
+ */
+#ifndef RABIA_KV_H
+#define RABIA_KV_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct rg_kv rg_kv;
+
+enum {
+  RG_KV_SUCCESS = 0,
+  RG_KV_NOT_FOUND = 1,
+  RG_KV_E_KEY_EMPTY = 2,
+  RG_KV_E_KEY_LONG = 3,
+  RG_KV_E_VALUE_LARGE = 4,
+  RG_KV_E_FULL = 5,
+  RG_KV_E_DECODE = 6,
+  RG_KV_NOT_APPLIED = 7,
+};
+
+/* KVStoreConfig (store.rs:17-42) fields the apply reads, plus device capacities. */
+typedef struct rg_kv_config {
+  uint64_t max_keys;             /* KVStoreConfig.max_keys; 0 => 1,000,000               */
+  uint64_t max_value_size;       /* KVStoreConfig.max_value_size; 0 => 1 MiB             */
+  uint32_t enable_notifications; /* KVStoreConfig.enable_notifications (drives version)  */
+  int32_t device;                /* HIP device ordinal                                   */
+  uint64_t table_slots;          /* power of two; 0 => next pow2 >= 2 * max_keys          */
+  uint64_t heap_bytes;           /* key + value byte heap; 0 => 64 * table_slots          */
+  uint32_t hash_bits;            /* test hook: keep only the low hash_bits bits of the key
+                                    hash (0 = all 64) to force hash-collision runs        */
+  uint32_t reserved;
+} rg_kv_config;
+
+/* Store counters (host copy). */
+typedef struct rg_kv_stats {
+  uint64_t live_keys;        /* KVStore.data.len()                                     */
+  uint64_t version;          /* KVStore.version (store.rs:486-489)                     */
+  uint64_t total_operations; /* StoreStats.total_operations (store.rs:480-484)         */
+  uint64_t occupied_slots;   /* table slots holding a key (live or deleted)            */
+  uint64_t heap_used;        /* bytes of the key/value heap in use                     */
+  uint64_t batches;          /* rg_kv_apply calls                                      */
+  uint64_t ordered_batches;  /* batches applied on the exact in-order path (StoreFull
+                                reachable or a hash collision group too large)          */
+  uint64_t flags;            /* nonzero: capacity fault (table or heap full); the batch
+                                that raised it was not applied                          */
+  uint64_t last_path;        /* the last batch: 0 keyed replay, 1 ordered replay,
+                                2 refused (capacity fault)                              */
+} rg_kv_stats;
+
+int rg_kv_create(rg_kv** out, const rg_kv_config* cfg);
+int rg_kv_destroy(rg_kv* kv);
+const char* rg_kv_last_error(const rg_kv* kv);
+
+/* Which commands to apply: apply_mask[c] = 1 iff command c belongs to a slot whose
+ * decision is V1 (output plane 7 of an rg_phase_step over the same window).
+ * slot_cmd_off[n_slots + 1] = CSR offsets of each slot's batch in the command list.
+ * out_dev / stride_words / tile_words = the step's output buffer and its layout
+ * (rabia_gpu.h "Layout"). */
+int rg_kv_mark_applied_async(rg_kv* kv, const uint32_t* out_dev, uint64_t stride_words,
+                             uint32_t tile_words, uint64_t n_slots,
+                             const uint64_t* slot_cmd_off_dev, uint8_t* apply_mask_dev,
+                             void* stream);
+
+/* Apply n_cmds commands in total order. Command c's bytes are
+ * data_dev[cmd_off_dev[c] .. cmd_off_dev[c+1]). apply_mask_dev may be NULL (apply
+ * all). results_dev[c] receives the result code. Equivalent to calling
+ * KVStoreSMR::apply_command on each applied command in order. */
+int rg_kv_apply_async(rg_kv* kv, const uint8_t* data_dev, const uint64_t* cmd_off_dev,
+                      uint64_t n_cmds, const uint8_t* apply_mask_dev, uint8_t* results_dev,
+                      void* stream);
+
+/* Counters (synchronises the device). */
+int rg_kv_get_stats(rg_kv* kv, rg_kv_stats* out);
+
+/* get_all_data (store.rs / smr_impl.rs:97-104) as raw arrays: copies the table
+ * (hashes[table_slots], entries[table_slots][4] = {key_off, val_off, version,
+ * key_len | val_len << 32}; version 0 = not live) and heap[heap_used] to host
+ * buffers of at least those sizes. Synchronous. */
+int rg_kv_dump(rg_kv* kv, uint64_t* hashes, uint64_t* entries, uint8_t* heap, uint64_t heap_cap);
+int rg_kv_table_slots(const rg_kv* kv, uint64_t* out);
+
+/* Synthetic C4 commands: n_cmds bincode KVOperations (Set 85 %, Get 10 %, Delete 3 %,
+ * Exists 2 %) over `key_space` keys "k<decimal>" (16-byte keys) with 32-byte values,
+ * written to data_dev (capacity data_cap bytes) with offsets cmd_off_dev[n_cmds + 1]. */
+int rg_kv_trace_async(rg_kv* kv, uint64_t seed, uint64_t n_cmds, uint64_t key_space,
+                      uint8_t* data_dev, uint64_t data_cap, uint64_t* cmd_off_dev, void* stream);
+
+int rg_kv_sync(rg_kv* kv, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RABIA_KV_H */

@@ -16,6 +16,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 LIB_PATH = os.path.join(PKG, "lib", "librabia_gpu.so")
 HEADER = os.path.join(ROOT, "include", "rabia_gpu.h")
+HEADERS = [HEADER, os.path.join(ROOT, "include", "rabia_kv.h")]
 
 u32, u64, i32, vp = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32, ctypes.c_void_p
 
@@ -47,6 +48,23 @@ class RgEngineState(ctypes.Structure):
                 ("steps", u64)]
 
 
+class RgKvConfig(ctypes.Structure):
+    _fields_ = [("max_keys", u64), ("max_value_size", u64), ("enable_notifications", u32),
+                ("device", i32), ("table_slots", u64), ("heap_bytes", u64), ("hash_bits", u32),
+                ("reserved", u32)]
+
+
+KV_STATS_FIELDS = ["live_keys", "version", "total_operations", "occupied_slots", "heap_used",
+                   "batches", "ordered_batches", "flags", "last_path"]
+
+
+class RgKvStats(ctypes.Structure):
+    _fields_ = [(f, u64) for f in KV_STATS_FIELDS]
+
+    def as_dict(self):
+        return {f: int(getattr(self, f)) for f in KV_STATS_FIELDS}
+
+
 _SIGS = {
     "rg_abi_version": (ctypes.c_int, []),
     "rg_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
@@ -72,6 +90,17 @@ _SIGS = {
     "rg_unpack_planes": (ctypes.c_int, [vp, u32, u64, u64, vp]),
     "rg_planar_to_tiled": (ctypes.c_int, [vp, u32, u64, u64, u32, vp]),
     "rg_tiled_to_planar": (ctypes.c_int, [vp, u32, u64, u32, u64, vp]),
+    # kvstore apply (include/rabia_kv.h)
+    "rg_kv_create": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.POINTER(RgKvConfig)]),
+    "rg_kv_destroy": (ctypes.c_int, [vp]),
+    "rg_kv_last_error": (ctypes.c_char_p, [vp]),
+    "rg_kv_mark_applied_async": (ctypes.c_int, [vp, vp, u64, u32, u64, vp, vp, vp]),
+    "rg_kv_apply_async": (ctypes.c_int, [vp, vp, vp, u64, vp, vp, vp]),
+    "rg_kv_get_stats": (ctypes.c_int, [vp, ctypes.POINTER(RgKvStats)]),
+    "rg_kv_dump": (ctypes.c_int, [vp, vp, vp, vp, u64]),
+    "rg_kv_table_slots": (ctypes.c_int, [vp, ctypes.POINTER(u64)]),
+    "rg_kv_trace_async": (ctypes.c_int, [vp, u64, u64, u64, vp, u64, vp, vp]),
+    "rg_kv_sync": (ctypes.c_int, [vp, vp]),
     # diagnostics (include/rabia_gpu_debug.h)
     "rg_debug_set": (ctypes.c_int, [vp, u32]),
     "rg_debug_stamps": (ctypes.c_int, [vp, vp, u64]),
@@ -82,10 +111,13 @@ _lib = None
 
 
 def header_symbols() -> list[str]:
-    """Every function declared in include/rabia_gpu.h."""
-    with open(HEADER) as f:
-        text = f.read()
-    return sorted(set(re.findall(r"^\s*(?:[\w\s\*]+?)\b(rg_\w+)\s*\(", text, re.M)))
+    """Every function declared in include/rabia_gpu.h and include/rabia_kv.h."""
+    names = set()
+    for h in HEADERS:
+        with open(h) as f:
+            text = f.read()
+        names |= set(re.findall(r"^\s*(?:[\w\s\*]+?)\b(rg_\w+)\s*\(", text, re.M))
+    return sorted(names)
 
 
 def load():
@@ -122,5 +154,12 @@ class RabiaGpuError(RuntimeError):
 def check(rc: int, ctx=None):
     if rc != RG_OK:
         msg = load().rg_last_error(ctx)
+        raise RabiaGpuError(rc, msg.decode() if msg else "")
+    return rc
+
+
+def check_kv(rc: int, kv=None):
+    if rc != RG_OK:
+        msg = load().rg_kv_last_error(kv)
         raise RabiaGpuError(rc, msg.decode() if msg else "")
     return rc

@@ -15,9 +15,10 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB_DIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIB_DIR, "librabia_gpu.so")
-SOURCES = [os.path.join(CSRC, "rabia_gpu.hip")]
+SOURCES = [os.path.join(CSRC, "rabia_gpu.hip"), os.path.join(CSRC, "rg_kv.hip")]
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("rg_common.h", "rg_kernels.h")] + [
-    os.path.join(ROOT, "include", "rabia_gpu.h"), os.path.join(ROOT, "include", "rabia_gpu_debug.h")]
+    os.path.join(ROOT, "include", "rabia_gpu.h"), os.path.join(ROOT, "include", "rabia_gpu_debug.h"),
+    os.path.join(ROOT, "include", "rabia_kv.h")]
 ARCH = "gfx950"
 
 
