@@ -1,0 +1,105 @@
+#!/usr/bin/env python3
+"""C4 pipeline timing (BASELINE.json configs[3]): 7 replicas x 2^22 slots with per-replica
+proposal digests, one REF phase sweep, then the kvstore apply of the V1-decided slots'
+batches (one bincode KVOperation per slot, device-generated).
+
+Stages, all device-resident on one stream, timed with HIP events per stage:
+  digest  rg_digest_majority_async (exchange: state = some digest held by >= q replicas)
+  phase   rg_phase_step_async (REF, planar layout)
+  mark    rg_kv_mark_applied_async (commands of V1 slots)
+  apply   rg_kv_apply_async (decode, sort, keyed replay / commit)
+Prints one JSON object. Not the driver's bench line (bench.py is): C4 is a parity
+config; this records where its time goes. cpu_baseline = oracle/kvstore_ref.py on a
+bounded sample of the same commands (1 thread).
+usage: python tools/bench_c4.py [--slots-log2 22] [--reps 5]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from rabia_amd import _native as N  # noqa: E402
+from rabia_amd.engine import PhaseEvaluator  # noqa: E402
+from rabia_amd.kvstore import DeviceKVStore, KVStoreConfig  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--slots-log2", type=int, default=22)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--key-space-log2", type=int, default=20)
+    ap.add_argument("--cpu-sample", type=int, default=200_000)
+    a = ap.parse_args()
+    n, S = 7, 1 << a.slots_log2
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    sp = stream.cuda_stream
+    stride = ((S + 127) // 128) * 4
+    ev = PhaseEvaluator(n, self_lane=n - 1, mode="ref", seed=42)
+    votes = torch.empty((4 * n + 1) * stride, dtype=torch.int32, device="cuda")
+    out = torch.empty(8 * stride, dtype=torch.int32, device="cuda")
+    digests = torch.empty(n * S, dtype=torch.int64, device="cuda")
+    ev.trace_generate_async(N.RG_TRACE_AGREE90, 5, 1, S, stride, votes.data_ptr(), sp)
+    ev.digest_trace_async(5, 1, S, S, digests.data_ptr(), sp)
+    slot_off = torch.arange(S + 1, dtype=torch.int64, device="cuda")  # one command per slot
+    cmd_data = torch.empty(68 * S, dtype=torch.uint8, device="cuda")
+    cmd_off = torch.empty(S + 1, dtype=torch.int64, device="cuda")
+    mask = torch.empty(S, dtype=torch.uint8, device="cuda")
+    res = torch.empty(S, dtype=torch.uint8, device="cuda")
+    ks = 1 << a.key_space_log2
+    times = {k: [] for k in ("digest", "phase", "mark", "apply")}
+    applied = []
+    for rep in range(a.reps + 1):
+        with DeviceKVStore(KVStoreConfig(max_keys=4 * ks)) as kv:
+            kv.trace_async(rep, S, ks, cmd_data.data_ptr(), cmd_data.numel(), cmd_off.data_ptr(), sp)
+            stream.synchronize()
+            evs = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+            evs[0].record(stream)
+            ev.digest_majority_async(digests.data_ptr(), S, votes.data_ptr() + 4 * 4 * n * stride, S, sp)
+            evs[1].record(stream)
+            ev.phase_step_async(votes.data_ptr(), out.data_ptr(), S, stride, slot_base=1, stream=sp)
+            evs[2].record(stream)
+            kv.mark_applied_async(out.data_ptr(), stride, 0, S, slot_off.data_ptr(), mask.data_ptr(), sp)
+            evs[3].record(stream)
+            kv.apply_async(cmd_data.data_ptr(), cmd_off.data_ptr(), S, mask.data_ptr(), res.data_ptr(), sp)
+            evs[4].record(stream)
+            stream.synchronize()
+            if rep:
+                for k, i in zip(times, range(4)):
+                    times[k].append(evs[i].elapsed_time(evs[i + 1]) * 1000.0)
+                st = kv.stats()
+                applied.append(int((mask.cpu().numpy() != 0).sum()))
+    med = {k: float(np.median(v)) for k, v in times.items()}
+    total_us = sum(med.values())
+    n_applied = int(np.median(applied))
+    # CPU baseline: the sequential restatement on a bounded sample of the same commands
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import kvstore_ref as R
+    m = min(a.cpu_sample, S)
+    d = cmd_data.cpu().numpy().tobytes()
+    o = cmd_off.cpu().numpy()
+    blobs = [d[o[i]:o[i + 1]] for i in range(m)]
+    t0 = time.perf_counter()
+    R.KVStoreRef(max_keys=4 * ks).apply_commands(blobs)
+    cpu_s = time.perf_counter() - t0
+    print(json.dumps({
+        "workload": f"C4: n={n}, 2^{a.slots_log2} slots, agree90 votes + per-replica digests, REF sweep, "
+                    f"1 KVOperation per slot over 2^{a.key_space_log2} keys (85% Set)",
+        "stage_us_median": med, "total_us": total_us,
+        "applied_commands": n_applied, "apply_commands_per_s": n_applied / (med["apply"] * 1e-6),
+        "slots_per_s_end_to_end": S / (total_us * 1e-6),
+        "store": st,
+        "cpu_baseline": {"value": m / cpu_s, "unit": "commands/s", "cores": 1, "kind": "port",
+                         "sample": f"{m} commands through oracle/kvstore_ref.py (sequential dict replay)"},
+    }, indent=1))
+
+
+if __name__ == "__main__":
+    main()
