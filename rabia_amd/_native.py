@@ -16,7 +16,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 LIB_PATH = os.path.join(PKG, "lib", "librabia_gpu.so")
 HEADER = os.path.join(ROOT, "include", "rabia_gpu.h")
-HEADERS = [HEADER, os.path.join(ROOT, "include", "rabia_kv.h")]
+HEADERS = [HEADER] + [os.path.join(ROOT, "include", h) for h in ("rabia_kv.h", "rabia_ingest.h")]
 
 u32, u64, i32, vp = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32, ctypes.c_void_p
 
@@ -46,6 +46,14 @@ class RgStepResult(ctypes.Structure):
 class RgEngineState(ctypes.Structure):
     _fields_ = [("rng_next", u64), ("last_committed", u64), ("commit_watermark", u64),
                 ("steps", u64)]
+
+
+class RgIngestConfig(ctypes.Structure):
+    _fields_ = [("n_replicas", u32), ("tile_words", u32), ("device", i32), ("reserved", u32),
+                ("members", (ctypes.c_uint8 * 16) * 16)]
+
+
+INGEST_STATS = ["r1", "r2", "superseded", "other", "outside", "invalid", "sender", "malformed"]
 
 
 class RgKvConfig(ctypes.Structure):
@@ -101,6 +109,11 @@ _SIGS = {
     "rg_kv_table_slots": (ctypes.c_int, [vp, ctypes.POINTER(u64)]),
     "rg_kv_trace_async": (ctypes.c_int, [vp, u64, u64, u64, vp, u64, vp, vp]),
     "rg_kv_sync": (ctypes.c_int, [vp, vp]),
+    # vote ingestion (include/rabia_ingest.h)
+    "rg_ingest_create": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.POINTER(RgIngestConfig)]),
+    "rg_ingest_destroy": (ctypes.c_int, [vp]),
+    "rg_ingest_last_error": (ctypes.c_char_p, [vp]),
+    "rg_ingest_votes_async": (ctypes.c_int, [vp, vp, vp, vp, u64, u64, vp, u64, u64, u64, vp, vp]),
     # diagnostics (include/rabia_gpu_debug.h)
     "rg_debug_set": (ctypes.c_int, [vp, u32]),
     "rg_debug_stamps": (ctypes.c_int, [vp, vp, u64]),
@@ -154,6 +167,13 @@ class RabiaGpuError(RuntimeError):
 def check(rc: int, ctx=None):
     if rc != RG_OK:
         msg = load().rg_last_error(ctx)
+        raise RabiaGpuError(rc, msg.decode() if msg else "")
+    return rc
+
+
+def check_ingest(rc: int, h=None):
+    if rc != RG_OK:
+        msg = load().rg_ingest_last_error(h)
         raise RabiaGpuError(rc, msg.decode() if msg else "")
     return rc
 

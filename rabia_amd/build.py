@@ -15,10 +15,10 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB_DIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIB_DIR, "librabia_gpu.so")
-SOURCES = [os.path.join(CSRC, "rabia_gpu.hip"), os.path.join(CSRC, "rg_kv.hip")]
+SOURCES = [os.path.join(CSRC, f) for f in ("rabia_gpu.hip", "rg_kv.hip", "rg_ingest.hip")]
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("rg_common.h", "rg_kernels.h")] + [
     os.path.join(ROOT, "include", "rabia_gpu.h"), os.path.join(ROOT, "include", "rabia_gpu_debug.h"),
-    os.path.join(ROOT, "include", "rabia_kv.h")]
+    os.path.join(ROOT, "include", "rabia_kv.h"), os.path.join(ROOT, "include", "rabia_ingest.h")]
 ARCH = "gfx950"
 
 
@@ -37,23 +37,38 @@ def needs_build() -> bool:
 
 
 def build(force: bool = False, resource_usage: bool = False, verbose: bool = False) -> str:
+    """Compile each translation unit to an object in parallel (hipcc -c), then link."""
     if not force and not needs_build() and not resource_usage:
         return LIB
-    os.makedirs(LIB_DIR, exist_ok=True)
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-result", "-I", os.path.join(ROOT, "include"), "-o", LIB + ".tmp",
-           *SOURCES]
+    obj_dir = os.path.join(LIB_DIR, "obj")
+    os.makedirs(obj_dir, exist_ok=True)
+    base = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result",
+            "-I", os.path.join(ROOT, "include")]
     if resource_usage:
-        cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
-    proc = subprocess.run(cmd, capture_output=True, text=True)
+        base.insert(1, "-Rpass-analysis=kernel-resource-usage")
+    objs, procs = [], []
+    for src in SOURCES:
+        obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
+        objs.append(obj)
+        cmd = base + ["-c", "-o", obj, src]
+        procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)))
+    err_text = ""
+    for cmd, proc in procs:
+        out, err = proc.communicate()
+        err_text += err
+        if proc.returncode != 0:
+            sys.stderr.write(out + err)
+            raise RuntimeError(f"hipcc failed ({proc.returncode}): {' '.join(cmd)}")
+    link = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB + ".tmp", *objs]
+    proc = subprocess.run(link, capture_output=True, text=True)
     if proc.returncode != 0:
         sys.stderr.write(proc.stdout + proc.stderr)
-        raise RuntimeError(f"hipcc failed ({proc.returncode}): {' '.join(cmd)}")
+        raise RuntimeError(f"hipcc link failed ({proc.returncode}): {' '.join(link)}")
     os.replace(LIB + ".tmp", LIB)
-    if verbose and proc.stderr:
-        sys.stderr.write(proc.stderr)
+    if verbose and err_text:
+        sys.stderr.write(err_text)
     if resource_usage:
-        print_resource_usage(proc.stderr)
+        print_resource_usage(err_text)
     return LIB
 
 
