@@ -56,6 +56,11 @@ def parse():
     ap.add_argument("--cpu-sample-windows", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_c2.json"))
+    ap.add_argument("--config", choices=["c2", "c5"], default="c2",
+                    help="c2: the headline (weak scaling, per-shard results exchanged); c5: 9 replicas x "
+                         "2^26 slots per step split over the ranks (strong scaling) with the decision "
+                         "bitmaps all-gathered every step")
+    ap.add_argument("--c5-windows", type=int, default=64, help="C5: 2^20-slot windows per step, all ranks")
     return ap.parse_args()
 
 
@@ -87,6 +92,108 @@ def load_pmc(path: str, n: int, slots: int):
     return None
 
 
+def run_c5(a, world, rank, local, dist):
+    """C5 (BASELINE.json configs[4]): 9 replicas, a 2^26-slot window per step split into
+    equal contiguous shards (one per rank), REF sweep, then the streaming exchange: every
+    rank extracts its committed + V1 bitmaps and all-gathers them and its step result
+    (RCCL over xGMI) on the collective stream while the next step computes. After the
+    timed loop the gathered rows are folded into the global commit watermark
+    (rabia_amd/shard.py:combine) and checked against the per-shard counts."""
+    from rabia_amd import shard
+    n, T = 9, a.tile_words
+    total = a.c5_windows * WINDOW
+    start, S = shard.shard_range(total, world, rank, align=32 * (T or 4))
+    assert S * world == total, "C5 needs equal shards"
+    nw = S // 32
+    stride = T if T else ((S + 127) // 128) * 4
+    in_words = ((nw + T - 1) // T) * (4 * n + 1) * T if T else (4 * n + 1) * stride
+    out_words = ((nw + T - 1) // T) * 8 * T if T else 8 * stride
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    sp = stream.cuda_stream
+    ev = PhaseEvaluator(n, self_lane=n - 1, mode="ref", seed=42 + rank, device=local, tile_words=T)
+    sets = []
+    for i in range(a.sets):
+        votes = torch.empty(in_words, dtype=torch.int32, device="cuda")
+        out = torch.empty(out_words, dtype=torch.int32, device="cuda")
+        ev.trace_generate_async(N.RG_TRACE_AGREE90, 1000 * rank + i, 1 + start, S, stride, votes.data_ptr(), sp)
+        sets.append((votes, out))
+    n_total = a.warmup + a.steps
+    res_dev = torch.zeros((n_total, 10), dtype=torch.int64, device="cuda")
+    gathered = torch.zeros((n_total, world, 10), dtype=torch.int64, device="cuda")
+    bm = torch.zeros((n_total, 2, nw), dtype=torch.int32, device="cuda")
+    bm_all = torch.zeros((n_total, world, 2, nw), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    works = []
+
+    def step(t):
+        votes, out = sets[t % a.sets]
+        base = 1 + t * total
+        ev.phase_step_async(votes.data_ptr(), out.data_ptr(), S, stride, slot_base=base + start,
+                            result_ptr=res_dev[t].data_ptr(), stream=sp)
+        ev.decision_bitmap_async(out.data_ptr(), S, stride, bm[t, 0].data_ptr(), bm[t, 1].data_ptr(), sp)
+        if dist is not None:
+            works.append(dist.all_gather_into_tensor(gathered[t], res_dev[t], async_op=True))
+            works.append(dist.all_gather_into_tensor(bm_all[t], bm[t], async_op=True))
+
+    for t in range(a.warmup):
+        step(t)
+    for w in works:
+        w.wait()
+    works.clear()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_begin, t_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t_begin.record(stream)
+    for k in range(a.steps):
+        step(a.warmup + k)
+    for w in works:
+        w.wait()
+    t_end.record(stream)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    total_ms = t_begin.elapsed_time(t_end)
+    res = res_dev.cpu().numpy().view(np.uint64)
+    if int(res[:, 9].max()) != 0:
+        raise RuntimeError("device-side protocol fault flagged in a step result")
+    g = gathered.cpu().numpy().view(np.uint64) if dist is not None else res[:, None, :]
+    b_all = bm_all.cpu().numpy().view(np.uint32) if dist is not None else bm.cpu().numpy().view(np.uint32)[:, None]
+    decided = 0
+    for t in range(a.warmup, n_total):  # global commit per step, checked against the bitmaps
+        rows = [shard.row_result(g[t, r]) for r in range(world)]
+        starts = [shard.shard_range(total, world, r, align=32 * (T or 4))[0] for r in range(world)]
+        gc = shard.combine(rows, [1 + t * total + s_ for s_ in starts], [S] * world, 1 + t * total, 1 + t * total)
+        pop = int(np.unpackbits(b_all[t, :, 0].view(np.uint8)).sum())
+        assert pop == gc.n_decided, (pop, gc.n_decided)
+        decided += gc.n_decided
+    tm = torch.tensor([total_ms], dtype=torch.float64, device="cuda")
+    if dist is not None:
+        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+    total_ms = float(tm[0])
+    if rank == 0:
+        bitmap_bytes = 2 * nw * 4 * world
+        line = {
+            "metric": "consensus slots decided/sec (9 replicas, 2^26 slots per step, bitmap all-gather)",
+            "value": decided / (total_ms / 1000.0),
+            "unit": "slots decided/s",
+            "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": total_ms / a.steps,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": "u32 bit-sliced 2-bit vote codes (integer only)",
+            "data": "synthetic (seeded agree90 vote trace generated on device)",
+            "config": {"workload": f"C5: {n} replicas x {total} slots per step, REF sweep, committed + V1 "
+                                   f"bitmaps ({bitmap_bytes} B per step in all) and step results all-gathered "
+                                   f"every step, overlapped with the next step",
+                       "replicas": n, "slots_per_step": total, "slots_per_gpu": S,
+                       "layout": f"slot-tiled {T}" if T else "planar", "parallelism": f"slot-shard x{world}"},
+        }
+        print(json.dumps(line), flush=True)
+    ev.close()
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -97,6 +204,11 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if a.config == "c5":
+        run_c5(a, world, rank, local, dist)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
     n, G = a.replicas, a.windows
     S = G * WINDOW
     T = a.tile_words

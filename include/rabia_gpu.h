@@ -158,6 +158,12 @@ int rg_digest_majority_async(rg_ctx* ctx, const uint64_t* digests_dev,
 int rg_coin_async(rg_ctx* ctx, uint64_t slot_base, uint64_t n_slots, uint64_t phase,
                   uint32_t* out_dev, void* stream);
 
+/* Decision bitmaps of a step's output buffer (layout as the context's): committed
+ * (output plane 6) and V1/apply (plane 7) as contiguous bit arrays of
+ * ceil(n_slots/32) words each — the per-shard payload of the multi-GPU exchange. */
+int rg_decision_bitmap_async(rg_ctx* ctx, const uint32_t* out_dev, uint64_t n_slots, uint64_t stride_words,
+                             uint32_t* committed_dev, uint32_t* v1_dev, void* stream);
+
 /* StdRng::seed_from_u64(seed).next_u64() draws first..first+count-1 (random access;
  * the stream the REF mode consumes, engine.rs:461-604). */
 int rg_ref_draws_async(rg_ctx* ctx, uint64_t first, uint64_t count, uint64_t* out_dev,

@@ -470,6 +470,21 @@ int rg_coin_async(rg_ctx* ctx, uint64_t slot_base, uint64_t n_slots, uint64_t ph
   return RG_OK;
 }
 
+int rg_decision_bitmap_async(rg_ctx* ctx, const uint32_t* out_dev, uint64_t n_slots, uint64_t stride_words,
+                             uint32_t* committed_dev, uint32_t* v1_dev, void* stream) {
+  if (!ctx || !out_dev || !committed_dev || !v1_dev || n_slots == 0)
+    return fail(ctx, RG_EINVAL, "rg_decision_bitmap: bad argument");
+  const uint64_t n_words = (n_slots + 31) / 32;
+  Layout lout;
+  uint64_t need;
+  if (int rc = make_layout(ctx, kOutPlanes, n_words, stride_words, &lout, &need, "rg_decision_bitmap")) return rc;
+  RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
+  hipLaunchKernelGGL(bitmap_kernel, dim3((uint32_t)((n_words + 255) / 256)), dim3(256), 0,
+                     pick_stream(ctx, stream), out_dev, lout, n_words, committed_dev, v1_dev);
+  RG_HIP(ctx, hipGetLastError());
+  return RG_OK;
+}
+
 int rg_ref_draws_async(rg_ctx* ctx, uint64_t first, uint64_t count, uint64_t* out_dev, void* stream) {
   if (!ctx || !out_dev || count == 0) return fail(ctx, RG_EINVAL, "rg_ref_draws: bad argument");
   RG_HIP(ctx, hipSetDevice(ctx->cfg.device));

@@ -853,6 +853,17 @@ __global__ void coin_kernel(Key key, uint64_t stream, uint64_t phase, uint64_t s
   out[w] = coin_word(key, stream, phase, slot_base + 32 * w, cur, blk) & valid_mask(w, n_words, n_slots);
 }
 
+// Decision bitmaps of a step's output (planes 6 committed, 7 V1/apply) as two
+// contiguous bit arrays: what the multi-GPU exchange all-gathers.
+__global__ void bitmap_kernel(const uint32_t* out, Layout lout, uint64_t n_words, uint32_t* committed,
+                              uint32_t* v1) {
+  const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= n_words) return;
+  const uint64_t b = lout.base(w);
+  committed[w] = out[b + 6 * lout.pstride];
+  v1[w] = out[b + 7 * lout.pstride];
+}
+
 __global__ void draws_kernel(Key key, uint64_t first, uint64_t count, unsigned long long* out) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= count) return;

@@ -261,6 +261,10 @@ class PhaseEvaluator:
         N.check(self.lib.rg_coin_async(self.ctx, slot_base, n_slots, phase, out_ptr, stream or None),
                 self.ctx)
 
+    def decision_bitmap_async(self, out_ptr, n_slots, stride, committed_ptr, v1_ptr, stream=0):
+        N.check(self.lib.rg_decision_bitmap_async(self.ctx, out_ptr, n_slots, stride, committed_ptr, v1_ptr,
+                                                  stream or None), self.ctx)
+
     def ref_draws_async(self, first, count, out_ptr, stream=0):
         N.check(self.lib.rg_ref_draws_async(self.ctx, first, count, out_ptr, stream or None), self.ctx)
 
