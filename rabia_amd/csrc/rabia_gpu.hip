@@ -350,7 +350,9 @@ int rg_phase_step_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_de
   const uint64_t tile_words = (uint64_t)cfg_block(cfg) * cfg_words(cfg, n);
   const uint64_t n_tiles = (n_words + tile_words - 1) / tile_words;
   if (int rc = ensure_tiles(ctx, n_tiles, false)) return rc;
-  if (++ctx->seq >= (1u << 31)) {  // tags wrap: start a fresh epoch on zeroed granules
+  // Statistics granules carry 12 bits of seq and look-back granules 31: start a
+  // fresh epoch on zeroed granules whenever either wraps.
+  if (++ctx->seq >= (1u << 31) || (ctx->seq & 0xFFFu) == 0) {
     if (int rc = ensure_tiles(ctx, n_tiles, true)) return rc;
     ctx->seq = 2 - (ctx->seq & 1u);  // keep the record-ring parity
   }

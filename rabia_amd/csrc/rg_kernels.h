@@ -268,19 +268,27 @@ __device__ __forceinline__ uint32_t lookback_exclusive(unsigned long long* statu
 }
 
 // ---- per-tile statistics -> granules; the last tile reduces them ------------
-// Per tile, kStatGranules 8-B granules {tag = seq : 32 | value : 32}:
-//   0 n_decided, 1 n_v1, 2 n_pending_r1, 3 n_draws,
-//   4 (largest V1 slot offset in the tile that commit_phase accepts) + 1, 0 = none,
-//   5 smallest undecided slot offset in the tile, ~0 = none.
-// One lane writes them with 8-B agent-scope stores; the tile with the last
-// tile index polls and folds them. No per-tile atomics on shared words: thousands of
-// same-address atomics per launch serialise at the memory side.
-constexpr int kStatGranules = 8;
+// Per tile, two 8-B granules written with agent-scope stores by one lane:
+//   g0 = tag:13 | n_decided:17 | n_v1:17 | n_pending_r1:17
+//   g1 = tag:13 | n_draws:17 | (largest V1 slot offset commit_phase accepts) + 1 (0 = none):17
+//             | smallest undecided slot offset (0x1FFFF = none):17
+// (a tile holds <= 65536 slots, so every field fits 17 bits). tag = 0x1000 |
+// (seq & 0xFFF) is never 0, and the host zeroes the array whenever seq & 0xFFF
+// wraps, so a granule from an earlier launch never carries the current tag. The
+// tile with the last index polls and folds every tile's pair (all loads of a
+// thread's tiles in flight at once). No per-tile atomics on shared words:
+// thousands of same-address atomics per launch serialise at the memory side.
+constexpr int kStatGranules = 2;
 constexpr uint32_t kSpinLimit = 1u << 24;
+constexpr uint32_t kStatNone = 0x1FFFFu;
 
 struct TileStats {
   uint32_t dec, v1, pend, draws, max_off1, min_off;
 };
+
+__device__ __forceinline__ unsigned long long stat_tag(uint32_t seq) {
+  return (unsigned long long)(0x1000u | (seq & 0xFFFu)) << 51;
+}
 
 __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
 #pragma unroll
@@ -298,27 +306,33 @@ __device__ __forceinline__ uint32_t wave_min32(uint32_t v) {
   return v;
 }
 
+// Three 21-bit sums packed in one u64 (per-wave values <= 8192, per-tile <= 65536).
 template <int BLOCK>
 __device__ __forceinline__ TileStats block_reduce_stats(TileStats s, int lane, int wave) {
   constexpr int WAVES = BLOCK / 64;
-  __shared__ uint32_t red[WAVES][6];
-  s.dec = wave_sum32(s.dec);
-  s.v1 = wave_sum32(s.v1);
-  s.pend = wave_sum32(s.pend);
-  s.draws = wave_sum32(s.draws);
-  s.max_off1 = wave_max32(s.max_off1);
-  s.min_off = wave_min32(s.min_off);
+  __shared__ unsigned long long red[WAVES][3];
+  unsigned long long packed = (unsigned long long)s.dec | ((unsigned long long)s.v1 << 21) |
+                              ((unsigned long long)s.pend << 42);
+  packed = wave_sum64(packed);
+  const uint32_t draws = wave_sum32(s.draws);
+  const uint32_t mx = wave_max32(s.max_off1), mn = wave_min32(s.min_off);
   if (lane == 0) {
-    red[wave][0] = s.dec; red[wave][1] = s.v1; red[wave][2] = s.pend;
-    red[wave][3] = s.draws; red[wave][4] = s.max_off1; red[wave][5] = s.min_off;
+    red[wave][0] = packed;
+    red[wave][1] = draws;
+    red[wave][2] = ((unsigned long long)mn << 32) | mx;
   }
   lds_barrier();
   TileStats r{0, 0, 0, 0, 0, ~0u};
 #pragma unroll
   for (int w = 0; w < WAVES; w++) {
-    r.dec += red[w][0]; r.v1 += red[w][1]; r.pend += red[w][2]; r.draws += red[w][3];
-    r.max_off1 = red[w][4] > r.max_off1 ? red[w][4] : r.max_off1;
-    r.min_off = red[w][5] < r.min_off ? red[w][5] : r.min_off;
+    const unsigned long long x = red[w][0];
+    r.dec += (uint32_t)(x & 0x1FFFFFu);
+    r.v1 += (uint32_t)((x >> 21) & 0x1FFFFFu);
+    r.pend += (uint32_t)(x >> 42);
+    r.draws += (uint32_t)red[w][1];
+    const uint32_t wmx = (uint32_t)red[w][2], wmn = (uint32_t)(red[w][2] >> 32);
+    r.max_off1 = wmx > r.max_off1 ? wmx : r.max_off1;
+    r.min_off = wmn < r.min_off ? wmn : r.min_off;
   }
   return r;
 }
@@ -355,44 +369,57 @@ template <bool IS_REF, int BLOCK, int W>
 __device__ __forceinline__ void finish_tile(const StepParams& p, Record* rec, TileStats ts,
                                             uint32_t tile, int tid, int lane, int wave) {
   constexpr uint64_t kTileSlots = (uint64_t)BLOCK * W * 32;
+  constexpr int kBatch = 8;  // tiles per thread with loads in flight together
   const TileStats b = block_reduce_stats<BLOCK>(ts, lane, wave);
-  const unsigned long long tag = (unsigned long long)p.seq << 32;
+  const unsigned long long tag = stat_tag(p.seq);
   if (tid == 0) {
     unsigned long long* g = p.stats + (uint64_t)tile * kStatGranules;
-    atomic_store_agent(g + 0, tag | b.dec);
-    atomic_store_agent(g + 1, tag | b.v1);
-    atomic_store_agent(g + 2, tag | b.pend);
-    atomic_store_agent(g + 3, tag | b.draws);
-    atomic_store_agent(g + 4, tag | b.max_off1);
-    atomic_store_agent(g + 5, tag | b.min_off);
+    const uint32_t mn = b.min_off == ~0u ? kStatNone : b.min_off;
+    atomic_store_agent(g + 0, tag | ((unsigned long long)b.pend << 34) | ((unsigned long long)b.v1 << 17) | b.dec);
+    atomic_store_agent(g + 1, tag | ((unsigned long long)mn << 34) | ((unsigned long long)b.max_off1 << 17) | b.draws);
   }
   if (tile != p.n_tiles - 1) return;
 
   unsigned long long v[7] = {0, 0, 0, 0, 0, ~0ull, 0};  // dec v1 pend draws max(id+1) min(id) fault
-  for (uint32_t i = tid; i < p.n_tiles; i += BLOCK) {
-    unsigned long long* g = p.stats + (uint64_t)i * kStatGranules;
-    unsigned long long gv[6];
+  constexpr unsigned long long kTagMask = ~0ull << 51;
+  for (uint32_t i0 = tid; i0 < p.n_tiles; i0 += kBatch * BLOCK) {
+    unsigned long long g[kBatch][2];
 #pragma unroll
-    for (int k = 0; k < 6; k++) gv[k] = atomic_load_agent(g + k);  // all in flight at once
+    for (int k = 0; k < kBatch; k++) {
+      const uint32_t i = i0 + (uint32_t)k * BLOCK;
+      const unsigned long long* gp = p.stats + (uint64_t)i * kStatGranules;
+      g[k][0] = i < p.n_tiles ? atomic_load_agent(const_cast<unsigned long long*>(gp)) : tag;
+      g[k][1] = i < p.n_tiles ? atomic_load_agent(const_cast<unsigned long long*>(gp) + 1) : tag;
+    }
     uint32_t spins = 0;
     for (;;) {
       bool ready = true;
 #pragma unroll
-      for (int k = 0; k < 6; k++) ready &= (uint32_t)(gv[k] >> 32) == p.seq;
+      for (int k = 0; k < kBatch; k++) ready &= ((g[k][0] & kTagMask) == tag) & ((g[k][1] & kTagMask) == tag);
       if (ready) break;
       if (++spins > kSpinLimit) { v[6] = 2; break; }
       __builtin_amdgcn_s_sleep(2);
 #pragma unroll
-      for (int k = 0; k < 6; k++)
-        if ((uint32_t)(gv[k] >> 32) != p.seq) gv[k] = atomic_load_agent(g + k);
+      for (int k = 0; k < kBatch; k++) {
+        const uint32_t i = i0 + (uint32_t)k * BLOCK;
+        unsigned long long* gp = p.stats + (uint64_t)i * kStatGranules;
+        if ((g[k][0] & kTagMask) != tag) g[k][0] = atomic_load_agent(gp);
+        if ((g[k][1] & kTagMask) != tag) g[k][1] = atomic_load_agent(gp + 1);
+      }
     }
-    uint32_t x[6];
 #pragma unroll
-    for (int k = 0; k < 6; k++) x[k] = (uint32_t)gv[k];
-    const unsigned long long tb = p.slot_base + (unsigned long long)i * kTileSlots;
-    v[0] += x[0]; v[1] += x[1]; v[2] += x[2]; v[3] += x[3];
-    if (x[4] && tb + x[4] > v[4]) v[4] = tb + x[4];
-    if (x[5] != ~0u && tb + x[5] < v[5]) v[5] = tb + x[5];
+    for (int k = 0; k < kBatch; k++) {
+      const uint32_t i = i0 + (uint32_t)k * BLOCK;
+      if (i >= p.n_tiles) continue;
+      const uint32_t dec = (uint32_t)(g[k][0] & kStatNone), v1 = (uint32_t)((g[k][0] >> 17) & kStatNone);
+      const uint32_t pend = (uint32_t)((g[k][0] >> 34) & kStatNone);
+      const uint32_t draws = (uint32_t)(g[k][1] & kStatNone), mx = (uint32_t)((g[k][1] >> 17) & kStatNone);
+      const uint32_t mn = (uint32_t)((g[k][1] >> 34) & kStatNone);
+      const unsigned long long tb = p.slot_base + (unsigned long long)i * kTileSlots;
+      v[0] += dec; v[1] += v1; v[2] += pend; v[3] += draws;
+      if (mx && tb + mx > v[4]) v[4] = tb + mx;
+      if (mn != kStatNone && tb + mn < v[5]) v[5] = tb + mn;
+    }
   }
   block_reduce_totals<BLOCK>(v, lane, wave);
   stamp(p, tile, 5, tid);

@@ -66,17 +66,12 @@ def run(variant, k):
 
 variants = {
     "big": {"tiled": True, "diag": 1 << 8},
-    "la512": {"tiled": True, "diag": (6 << 8) | (512 << 16)},
-    "la256": {"tiled": True, "diag": (6 << 8) | (256 << 16)},
-    "la1024": {"tiled": True, "diag": (6 << 8) | (1024 << 16)},
-    "la_mid1024": {"tiled": True, "diag": (7 << 8) | (1024 << 16)},
+    "big_nofin": {"tiled": True, "diag": 2 | (1 << 8)},
     "t_probe": {"tiled": True, "probe": True},
     "big_s28": {"tiled": True, "diag": 1 << 8, "slots": 1 << 28},
-    "la512_s28": {"tiled": True, "diag": (6 << 8) | (512 << 16), "slots": 1 << 28},
-    "la1024_s28": {"tiled": True, "diag": (6 << 8) | (1024 << 16), "slots": 1 << 28},
-    "la2048_s28": {"tiled": True, "diag": (6 << 8) | (2048 << 16), "slots": 1 << 28},
-    "la_mid2048_s28": {"tiled": True, "diag": (7 << 8) | (2048 << 16), "slots": 1 << 28},
+    "big_nofin_s28": {"tiled": True, "diag": 2 | (1 << 8), "slots": 1 << 28},
     "t_probe_s28": {"tiled": True, "probe": True, "slots": 1 << 28},
+    "auto_1M": {"tiled": True, "slots": 1 << 20},
 }
 times = {k: [] for k in variants}
 for r in range(8):
