@@ -142,14 +142,19 @@ __device__ __forceinline__ void load_words(const uint32_t* p, uint32_t (&v)[W]) 
   }
 }
 
+// Output planes are written once and not read by this launch: non-temporal stores.
 template <int W>
-__device__ __forceinline__ void store_words(uint32_t* p, const uint32_t (&v)[W]) {
+__device__ __forceinline__ void store_words_nt(uint32_t* p, const uint32_t (&v)[W]) {
   if constexpr (W == 4) {
-    *reinterpret_cast<uint4*>(p) = make_uint4(v[0], v[1], v[2], v[3]);
+    u32x4 x;
+    x.x = v[0]; x.y = v[1]; x.z = v[2]; x.w = v[3];
+    __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(p));
   } else if constexpr (W == 2) {
-    *reinterpret_cast<uint2*>(p) = make_uint2(v[0], v[1]);
+    u32x2 x;
+    x.x = v[0]; x.y = v[1];
+    __builtin_nontemporal_store(x, reinterpret_cast<u32x2*>(p));
   } else {
-    *p = v[0];
+    __builtin_nontemporal_store(v[0], p);
   }
 }
 
@@ -665,7 +670,7 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
   if (active) {
     uint32_t* ob = p.out + p.lout.base(w0);
 #pragma unroll
-    for (int pl = 0; pl < kOutPlanes; pl++) store_words<W>(ob + pl * p.lout.pstride, o[pl]);
+    for (int pl = 0; pl < kOutPlanes; pl++) store_words_nt<W>(ob + pl * p.lout.pstride, o[pl]);
   }
   stamp(p, tile, 3, tid);
   if (p.diag & 2u) return;
@@ -821,7 +826,7 @@ __global__ __launch_bounds__(BLOCK, 4) void wmvc_step_kernel(StepParams p) {
   if (active) {
     uint32_t* ob = p.out + p.lout.base(w0);
 #pragma unroll
-    for (int pl = 0; pl < kOutPlanes; pl++) store_words<W>(ob + pl * p.lout.pstride, o[pl]);
+    for (int pl = 0; pl < kOutPlanes; pl++) store_words_nt<W>(ob + pl * p.lout.pstride, o[pl]);
   }
   uint32_t vm_all[W], dv1[W];
 #pragma unroll
