@@ -158,6 +158,24 @@ int rg_digest_majority_async(rg_ctx* ctx, const uint64_t* digests_dev,
 int rg_coin_async(rg_ctx* ctx, uint64_t slot_base, uint64_t n_slots, uint64_t phase,
                   uint32_t* out_dev, void* stream);
 
+/* Own round-1 votes for received proposals, in message order (REF mode):
+ * RabiaEngine::handle_propose -> determine_round1_vote / randomized_vote
+ * (engine.rs:380-481). phase_ids_dev[m], values_dev[m] (StateValue code) of
+ * proposal m; votes_dev[m] receives the vote code to send back (3 = phase id
+ * outside [slot_base, slot_base + n_slots)). track_proposals = 1: the window's
+ * PhaseData exist and record proposed_value in proposed_dev (2 planar planes of
+ * stride_words, lo/hi bit of the code, 3 = none; updated in place): a slot's first
+ * proposal takes randomized_vote (V0: StdRng draw < P70 -> V0 else VQuestion; V1:
+ * draw < P80 -> V1 else VQuestion; VQuestion: no draw), later ones vote the
+ * proposed value if equal, else VQuestion. track_proposals = 0 restates the
+ * reference as it runs (phases are never created, state.rs:166-185): every
+ * proposal takes randomized_vote; proposed_dev / n_slots / slot_base are ignored.
+ * Draws come from the engine stream in message order and advance rng_next. */
+int rg_round1_votes_async(rg_ctx* ctx, const uint64_t* phase_ids_dev, const uint8_t* values_dev,
+                          uint64_t n_props, uint32_t* proposed_dev, uint64_t stride_words,
+                          uint64_t n_slots, uint64_t slot_base, uint32_t track_proposals,
+                          uint8_t* votes_dev, void* stream);
+
 /* Decision bitmaps of a step's output buffer (layout as the context's): committed
  * (output plane 6) and V1/apply (plane 7) as contiguous bit arrays of
  * ceil(n_slots/32) words each — the per-shard payload of the multi-GPU exchange. */

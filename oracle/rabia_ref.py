@@ -115,6 +115,42 @@ def round2_vote_for_question(c0, c1, u):
     return V1 if u < P_INT[0.8] else V0
 
 
+def round1_votes(seed, rng_base, props, proposed, slot_base, track=True):
+    """Own round-1 votes for received proposals, in message order —
+    RabiaEngine::handle_propose (engine.rs:380-422) -> determine_round1_vote
+    (engine.rs:424-452) -> randomized_vote (engine.rs:454-481).
+    props: list of (phase_id, proposed value code); proposed: mutable list of the
+    window's PhaseData.proposed_value codes (NONE = unset), updated in place as
+    handle_propose does (engine.rs:400-404). track=False restates the reference as
+    it runs (phases never created, update_phase a no-op: state.rs:166-185): every
+    proposal takes randomized_vote. Returns (votes, draws consumed); vote NONE =
+    phase outside the window."""
+    key = seed_from_u64(seed)
+    k = rng_base
+    votes = []
+    for phase, value in props:
+        existing = NONE
+        if track:
+            off = phase - slot_base
+            if not 0 <= off < len(proposed):
+                votes.append(NONE)
+                continue
+            existing = proposed[off]
+        if existing != NONE:
+            votes.append(value if existing == value else VQ)
+            continue
+        if value == VQ:
+            vote = VQ
+        else:
+            u = ref_draw(key, k)
+            k += 1
+            vote = value if u < P_INT[0.7 if value == V0 else 0.8] else VQ
+        votes.append(vote)
+        if track:
+            proposed[phase - slot_base] = value
+    return votes, k - rng_base
+
+
 def coin(coin_key, epoch, slot, phase):
     """Common coin (build-defined)."""
     b = chacha_block(coin_key, ((phase - 1) << 40) | (slot >> 9), epoch | (1 << 63), 12)

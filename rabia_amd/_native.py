@@ -90,6 +90,7 @@ _SIGS = {
     "rg_coin_async": (ctypes.c_int, [vp, u64, u64, u64, vp, vp]),
     "rg_ref_draws_async": (ctypes.c_int, [vp, u64, u64, vp, vp]),
     "rg_decision_bitmap_async": (ctypes.c_int, [vp, vp, u64, u64, vp, vp, vp]),
+    "rg_round1_votes_async": (ctypes.c_int, [vp, vp, vp, u64, vp, u64, u64, u64, u32, vp, vp]),
     "rg_trace_generate_async": (ctypes.c_int, [vp, ctypes.c_int, u64, u64, u64, u64, vp, vp]),
     "rg_digest_trace_async": (ctypes.c_int, [vp, u64, u64, u64, u64, vp, vp]),
     "rg_wmvc_cluster_async": (ctypes.c_int, [vp, vp, u64, u64, u64, u64, u32, vp, vp, vp]),

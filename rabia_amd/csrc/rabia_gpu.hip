@@ -38,6 +38,11 @@ struct rg_ctx {
   uint32_t diag = 0;
   unsigned long long* dbg = nullptr;
   uint64_t dbg_cap = 0;
+  uint32_t* r1v_cells = nullptr;   // round-1 votes: per-slot claim cells (0xFFFFFFFF)
+  uint64_t r1v_cells_cap = 0;
+  uint32_t* r1v_blocks = nullptr;  // per-block draw counts / offsets
+  uint64_t r1v_blocks_cap = 0;
+  unsigned long long* r1v_base = nullptr;
   unsigned long long* cluster_part = nullptr;  // [blocks][kClusterStats]
   unsigned long long* cluster_stats = nullptr;  // [kClusterStats]
   std::string err;
@@ -285,6 +290,9 @@ int rg_destroy(rg_ctx* ctx) {
   (void)hipFree(ctx->lookback);
   (void)hipFree(ctx->stats);
   (void)hipFree(ctx->dbg);
+  (void)hipFree(ctx->r1v_cells);
+  (void)hipFree(ctx->r1v_blocks);
+  (void)hipFree(ctx->r1v_base);
   (void)hipFree(ctx->cluster_part);
   (void)hipFree(ctx->cluster_stats);
   (void)hipFree(ctx->d_votes);
@@ -483,6 +491,68 @@ int rg_decision_bitmap_async(rg_ctx* ctx, const uint32_t* out_dev, uint64_t n_sl
   RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
   hipLaunchKernelGGL(bitmap_kernel, dim3((uint32_t)((n_words + 255) / 256)), dim3(256), 0,
                      pick_stream(ctx, stream), out_dev, lout, n_words, committed_dev, v1_dev);
+  RG_HIP(ctx, hipGetLastError());
+  return RG_OK;
+}
+
+int rg_round1_votes_async(rg_ctx* ctx, const uint64_t* phase_ids_dev, const uint8_t* values_dev, uint64_t n_props,
+                          uint32_t* proposed_dev, uint64_t stride_words, uint64_t n_slots, uint64_t slot_base,
+                          uint32_t track_proposals, uint8_t* votes_dev, void* stream) {
+  if (!ctx) return fail(nullptr, RG_EINVAL, "rg_round1_votes: null context");
+  if (ctx->cfg.mode != RG_MODE_REF) return fail(ctx, RG_EINVAL, "rg_round1_votes: REF mode only (engine.rs:424-481)");
+  if (n_props == 0) return RG_OK;
+  if (!phase_ids_dev || !values_dev || !votes_dev || (track_proposals && (!proposed_dev || !n_slots)))
+    return fail(ctx, RG_EINVAL, "rg_round1_votes: null buffer");
+  if (n_props > (1ull << 31)) return fail(ctx, RG_EINVAL, "rg_round1_votes: more than 2^31 proposals");
+  if (track_proposals && (stride_words < (n_slots + 31) / 32))
+    return fail(ctx, RG_EINVAL, "rg_round1_votes: stride_words < ceil(n_slots/32)");
+  RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
+  const uint32_t blocks = (uint32_t)((n_props + kR1vBlock - 1) / kR1vBlock);
+  if ((track_proposals && n_slots > ctx->r1v_cells_cap) || blocks > ctx->r1v_blocks_cap || !ctx->r1v_base) {
+    RG_HIP(ctx, hipDeviceSynchronize());
+    if (track_proposals && n_slots > ctx->r1v_cells_cap) {
+      (void)hipFree(ctx->r1v_cells);
+      ctx->r1v_cells = nullptr;
+      ctx->r1v_cells_cap = 0;
+      RG_HIP(ctx, hipMalloc(&ctx->r1v_cells, n_slots * 4));
+      RG_HIP(ctx, hipMemset(ctx->r1v_cells, 0xFF, n_slots * 4));
+      ctx->r1v_cells_cap = n_slots;
+    }
+    if (blocks > ctx->r1v_blocks_cap) {
+      (void)hipFree(ctx->r1v_blocks);
+      ctx->r1v_blocks = nullptr;
+      ctx->r1v_blocks_cap = 0;
+      RG_HIP(ctx, hipMalloc(&ctx->r1v_blocks, (uint64_t)blocks * 4));
+      ctx->r1v_blocks_cap = blocks;
+    }
+    if (!ctx->r1v_base) RG_HIP(ctx, hipMalloc(&ctx->r1v_base, 8));
+    RG_HIP(ctx, hipDeviceSynchronize());
+  }
+  R1vArgs a;
+  a.phase_ids = phase_ids_dev;
+  a.values = values_dev;
+  a.n = n_props;
+  a.n_slots = track_proposals ? n_slots : 0;
+  a.slot_base = slot_base;
+  a.stride = stride_words;
+  a.proposed = proposed_dev;
+  a.cells = ctx->r1v_cells;
+  a.block_draws = ctx->r1v_blocks;
+  a.base = ctx->r1v_base;
+  a.state = ctx->state;
+  a.votes = votes_dev;
+  a.key = ctx->ref_key;
+  a.track = track_proposals ? 1u : 0u;
+  if (!track_proposals) {  // every proposal is "first": no window, all phase ids accepted
+    a.slot_base = 0;
+    a.n_slots = ~0ull;
+  }
+  hipStream_t s = pick_stream(ctx, stream);
+  hipLaunchKernelGGL(r1v_claim_kernel, dim3(blocks), dim3(kR1vBlock), 0, s, a);
+  hipLaunchKernelGGL(r1v_count_kernel, dim3(blocks), dim3(kR1vBlock), 0, s, a);
+  hipLaunchKernelGGL(r1v_scan_kernel, dim3(1), dim3(1024), 0, s, a, blocks);
+  hipLaunchKernelGGL(r1v_vote_kernel, dim3(blocks), dim3(kR1vBlock), 0, s, a);
+  hipLaunchKernelGGL(r1v_reset_kernel, dim3(blocks), dim3(kR1vBlock), 0, s, a);
   RG_HIP(ctx, hipGetLastError());
   return RG_OK;
 }

@@ -896,6 +896,154 @@ __global__ void bitmap_kernel(const uint32_t* out, Layout lout, uint64_t n_words
   v1[w] = out[b + 7 * lout.pstride];
 }
 
+// ---- own round-1 votes for received proposals (engine.rs:380-481) -------------
+// determine_round1_vote: a slot whose PhaseData already holds a proposed value
+// votes that value if the proposal matches it, VQuestion otherwise; the first
+// proposal of a slot (no proposed value yet) takes randomized_vote: V0 -> one
+// StdRng draw, V0 iff u < P70, else VQuestion; V1 -> V1 iff u < P80, else
+// VQuestion; VQuestion -> VQuestion without a draw. Draws are consumed in message
+// order from the engine's stream (the context's rng_next). `track` = 0 restates
+// the reference as it runs today (phases are never created, update_phase is a
+// no-op, state.rs:166-185), so every proposal takes randomized_vote.
+constexpr uint64_t kP70 = 0xB333333333333000ull;  // (0.7 * 2^64) as u64
+constexpr int kR1vBlock = 256;
+
+struct R1vArgs {
+  const uint64_t* phase_ids;
+  const uint8_t* values;
+  uint64_t n, n_slots, slot_base, stride;
+  uint32_t* proposed;       // 2 planar planes (lo, hi), code 3 = none
+  uint32_t* cells;          // [n_slots] first message index per slot (0xFFFFFFFF = none)
+  uint32_t* block_draws;    // [blocks] draws per block, then exclusive offsets
+  unsigned long long* base; // [1] rng_next at the start of the batch
+  DevState* state;
+  uint8_t* votes;
+  Key key;
+  uint32_t track;
+};
+
+__device__ __forceinline__ uint32_t proposed_code(const R1vArgs& a, uint64_t off) {
+  const uint32_t w = off >> 5, b = off & 31u;
+  return ((a.proposed[w] >> b) & 1u) | (((a.proposed[a.stride + w] >> b) & 1u) << 1);
+}
+
+// 1: the first message of each slot without a proposed value claims the slot
+__global__ void r1v_claim_kernel(R1vArgs a) {
+  const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= a.n || !a.track) return;
+  const uint64_t ph = a.phase_ids[m];
+  if (ph < a.slot_base || ph - a.slot_base >= a.n_slots) return;
+  const uint64_t off = ph - a.slot_base;
+  if (proposed_code(a, off) == 3u) atomicMin(a.cells + off, (uint32_t)m);
+}
+
+__device__ __forceinline__ bool r1v_draws(const R1vArgs& a, uint64_t m, bool* first, uint64_t* off) {
+  const uint64_t ph = a.phase_ids[m];
+  *first = false;
+  if (ph < a.slot_base || ph - a.slot_base >= a.n_slots) return false;
+  *off = ph - a.slot_base;
+  *first = !a.track || a.cells[*off] == (uint32_t)m;  // claimed only if no proposal before
+  return *first && a.values[m] <= 1;
+}
+
+// 2: draws per block
+__global__ __launch_bounds__(kR1vBlock) void r1v_count_kernel(R1vArgs a) {
+  const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool first = false, d = false;
+  uint64_t off = 0;
+  if (m < a.n) d = r1v_draws(a, m, &first, &off);
+  const int c = __syncthreads_count(d);
+  if (threadIdx.x == 0) a.block_draws[blockIdx.x] = (uint32_t)c;
+}
+
+// 3: one workgroup: exclusive offsets of the block counts; the batch's draws are
+// taken from the engine stream here (rng_next advances by the total)
+__global__ __launch_bounds__(1024) void r1v_scan_kernel(R1vArgs a, uint32_t blocks) {
+  __shared__ unsigned long long s_sum[1024];
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = (blocks + 1023) / 1024, lo = t * per, hi = lo + per < blocks ? lo + per : blocks;
+  unsigned long long sum = 0;
+  for (uint32_t b = lo; b < hi; b++) sum += a.block_draws[b];
+  s_sum[t] = sum;
+  __syncthreads();
+  for (uint32_t o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele scan
+    const unsigned long long v = t >= o ? s_sum[t - o] : 0;
+    __syncthreads();
+    s_sum[t] += v;
+    __syncthreads();
+  }
+  unsigned long long run = s_sum[t] - sum;
+  for (uint32_t b = lo; b < hi; b++) {
+    const uint32_t c = a.block_draws[b];
+    a.block_draws[b] = (uint32_t)run;
+    run += c;
+  }
+  if (t == 1023) {
+    const unsigned long long r0 = a.state->rng_next;
+    *a.base = r0;
+    a.state->rng_next = r0 + s_sum[1023];
+  }
+}
+
+// 4: votes, proposed values, cell reset
+__global__ __launch_bounds__(kR1vBlock) void r1v_vote_kernel(R1vArgs a) {
+  __shared__ uint32_t s_w[kR1vBlock / 64];
+  const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  bool first = false, d = false;
+  uint64_t off = 0;
+  if (m < a.n) d = r1v_draws(a, m, &first, &off);
+  const uint32_t incl = wave_incl_scan32(d ? 1u : 0u, lane);
+  if (lane == 63) s_w[wave] = incl;
+  __syncthreads();
+  uint32_t before = 0;
+  for (int w = 0; w < wave; w++) before += s_w[w];
+  if (m >= a.n) return;
+  const uint64_t ph = a.phase_ids[m];
+  const uint32_t val = a.values[m];
+  uint8_t vote;
+  if (ph < a.slot_base || ph - a.slot_base >= a.n_slots) {
+    vote = 3;                                          // not in this window
+  } else if (first) {
+    if (d) {
+      const unsigned long long k = *a.base + a.block_draws[blockIdx.x] + before + incl - 1;
+      uint32_t blk[16];
+      chacha_block<12>(a.key, k >> 3, 0, blk);
+      const uint32_t ws = (uint32_t)(k & 7u) * 2u;
+      const unsigned long long u =
+          (unsigned long long)select16(blk, ws) | ((unsigned long long)select16(blk, ws + 1) << 32);
+      vote = (uint8_t)((u < (val == 0 ? kP70 : kP80)) ? val : 2u);  // engine.rs:454-481
+    } else {
+      vote = 2;                                        // VQuestion proposal
+    }
+    if (a.track) {                                     // phase.proposed_value = Some(value)
+      const uint32_t bit = 1u << (off & 31);
+      uint32_t* lo = a.proposed + (off >> 5);
+      uint32_t* hi = lo + a.stride;
+      if (val & 1u) atomicOr(lo, bit); else atomicAnd(lo, ~bit);
+      if (val & 2u) atomicOr(hi, bit); else atomicAnd(hi, ~bit);
+    }
+  } else {
+    // a proposal already recorded for the slot: before this batch, or by this
+    // batch's first message for the slot (engine.rs:430-441)
+    // (cells[] is set only for slots without a proposal before the batch, and only
+    // first messages write the proposed planes, so neither read races a write)
+    const uint32_t c = a.cells[off];
+    const uint32_t cur = c != 0xFFFFFFFFu ? (uint32_t)a.values[c] : proposed_code(a, off);
+    vote = (uint8_t)(cur == val ? val : 2u);
+  }
+  a.votes[m] = vote;
+}
+
+// 5: re-arm the claim cells touched by this batch
+__global__ void r1v_reset_kernel(R1vArgs a) {
+  const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= a.n || !a.track) return;
+  const uint64_t ph = a.phase_ids[m];
+  if (ph < a.slot_base || ph - a.slot_base >= a.n_slots) return;
+  a.cells[ph - a.slot_base] = 0xFFFFFFFFu;
+}
+
 __global__ void draws_kernel(Key key, uint64_t first, uint64_t count, unsigned long long* out) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= count) return;

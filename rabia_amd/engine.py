@@ -261,6 +261,13 @@ class PhaseEvaluator:
         N.check(self.lib.rg_coin_async(self.ctx, slot_base, n_slots, phase, out_ptr, stream or None),
                 self.ctx)
 
+    def round1_votes_async(self, phase_ids_ptr, values_ptr, n_props, proposed_ptr, stride, n_slots, slot_base,
+                           track, votes_ptr, stream=0):
+        """Own round-1 votes for received proposals (determine_round1_vote, engine.rs:424-481)."""
+        N.check(self.lib.rg_round1_votes_async(self.ctx, phase_ids_ptr, values_ptr, n_props, proposed_ptr or None,
+                                               stride, n_slots, slot_base, 1 if track else 0, votes_ptr,
+                                               stream or None), self.ctx)
+
     def decision_bitmap_async(self, out_ptr, n_slots, stride, committed_ptr, v1_ptr, stream=0):
         N.check(self.lib.rg_decision_bitmap_async(self.ctx, out_ptr, n_slots, stride, committed_ptr, v1_ptr,
                                                   stream or None), self.ctx)
