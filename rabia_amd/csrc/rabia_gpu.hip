@@ -112,7 +112,10 @@ struct Disp {
   }
   static void digest(uint32_t grid, hipStream_t s, const uint64_t* dg, uint64_t ds, uint32_t* out,
                      uint64_t n, uint32_t q) {
-    hipLaunchKernelGGL((digest_kernel<N>), dim3(grid), dim3(kBlock), 0, s, dg, ds, out, n, q);
+    if ((reinterpret_cast<uintptr_t>(dg) & 15u) == 0 && (ds & 1u) == 0)  // rows 16-B aligned
+      hipLaunchKernelGGL((digest_kernel<N, true>), dim3(grid), dim3(kBlock), 0, s, dg, ds, out, n, q);
+    else
+      hipLaunchKernelGGL((digest_kernel<N, false>), dim3(grid), dim3(kBlock), 0, s, dg, ds, out, n, q);
   }
   static void cluster(uint32_t grid, hipStream_t s, const uint32_t* st, uint64_t stride, uint64_t n_slots,
                       uint64_t base, uint32_t q, uint32_t fp1, Key key, uint64_t cs, uint64_t dseed,

@@ -841,37 +841,82 @@ __global__ __launch_bounds__(BLOCK, 4) void wmvc_step_kernel(StepParams p) {
 
 // ============================================================================
 // Exchange stage: digest majority (weak_mvc.ivy:109-128). One wave = 128 slots:
-// lane l owns slots l and 64+l, so each u64 load instruction is 512 contiguous B.
+// lane l owns slots 2l and 2l+1 and reads them with one 16-B non-temporal load
+// per replica (1 KiB per wave instruction, all N in flight); the two per-lane
+// majority bits are bit-interleaved into the wave's 128-slot mask. When the
+// digest rows are not 16-B aligned, lane l owns slots l and 64+l (8-B loads).
 // ============================================================================
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ unsigned long long spread32(uint32_t x) {
+  unsigned long long v = x;
+  v = (v | (v << 16)) & 0x0000FFFF0000FFFFull;
+  v = (v | (v << 8)) & 0x00FF00FF00FF00FFull;
+  v = (v | (v << 4)) & 0x0F0F0F0F0F0F0F0Full;
+  v = (v | (v << 2)) & 0x3333333333333333ull;
+  v = (v | (v << 1)) & 0x5555555555555555ull;
+  return v;
+}
+
 template <int N>
+__device__ __forceinline__ bool digest_major(const uint64_t (&d)[N], uint32_t q) {
+  bool st = false;
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < N; j++) c += (d[j] == d[i]) ? 1u : 0u;
+    st |= (d[i] != 0) && (c >= q);
+  }
+  return st;
+}
+
+template <int N, bool VEC>
 __global__ __launch_bounds__(kBlock) void digest_kernel(const uint64_t* __restrict__ dg,
                                                         uint64_t dstride, uint32_t* out,
                                                         uint64_t n_slots, uint32_t q) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t s0 = ((uint64_t)blockIdx.x * kWaves + wave) * 128;
   if (s0 >= n_slots) return;
-  unsigned long long masks[2];
+  unsigned long long lo, hi;
+  if constexpr (VEC) {
+    const uint64_t s = s0 + 2 * lane;
+    uint64_t d0[N], d1[N];
+    if (s + 1 < n_slots) {
 #pragma unroll
-  for (int h = 0; h < 2; h++) {
-    const uint64_t s = s0 + 64 * h + lane;
-    const bool valid = s < n_slots;
-    uint64_t d[N];
+      for (int j = 0; j < N; j++) {
+        const u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(dg + (uint64_t)j * dstride + s));
+        d0[j] = x.x;
+        d1[j] = x.y;
+      }
+    } else {
 #pragma unroll
-    for (int j = 0; j < N; j++) d[j] = valid ? dg[(uint64_t)j * dstride + s] : 0ull;
-    bool st = false;
-#pragma unroll
-    for (int i = 0; i < N; i++) {
-      uint32_t c = 0;
-#pragma unroll
-      for (int j = 0; j < N; j++) c += (d[j] == d[i]) ? 1u : 0u;
-      st |= (d[i] != 0) && (c >= q);
+      for (int j = 0; j < N; j++) {
+        d0[j] = s < n_slots ? dg[(uint64_t)j * dstride + s] : 0ull;
+        d1[j] = 0ull;
+      }
     }
-    masks[h] = __ballot(st && valid);
+    const unsigned long long ev = __ballot(digest_major<N>(d0, q) && s < n_slots);
+    const unsigned long long od = __ballot(digest_major<N>(d1, q) && s + 1 < n_slots);
+    lo = spread32((uint32_t)ev) | (spread32((uint32_t)od) << 1);
+    hi = spread32((uint32_t)(ev >> 32)) | (spread32((uint32_t)(od >> 32)) << 1);
+  } else {
+    unsigned long long masks[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const uint64_t s = s0 + 64 * h + lane;
+      const bool valid = s < n_slots;
+      uint64_t d[N];
+#pragma unroll
+      for (int j = 0; j < N; j++) d[j] = valid ? dg[(uint64_t)j * dstride + s] : 0ull;
+      masks[h] = __ballot(digest_major<N>(d, q) && valid);
+    }
+    lo = masks[0];
+    hi = masks[1];
   }
   if (lane == 0) {
     *reinterpret_cast<uint4*>(out + s0 / 32) =
-        make_uint4((uint32_t)masks[0], (uint32_t)(masks[0] >> 32), (uint32_t)masks[1],
-                   (uint32_t)(masks[1] >> 32));
+        make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
   }
 }
 

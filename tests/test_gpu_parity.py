@@ -228,9 +228,10 @@ def test_digest_majority(oracle, golden, n):
     if n in (5, 7):
         g = golden(f"digest_n{n}.npz")
         cases.append((g["digests"], g["state"]))
+    for S_ in (131074, 100003):  # even stride: 16-B vector path; odd: 8-B path
+        d = oracle.digest_trace(n, 4, 1, S_)
+        cases.append((d, oracle.digest_majority(d, n // 2 + 1)))
     S = 100003
-    d = oracle.digest_trace(n, 4, 1, S)
-    cases.append((d, oracle.digest_majority(d, n // 2 + 1)))
     for dg, exp in cases:
         S = dg.shape[1]
         stride = ((S + 127) // 128) * 4
