@@ -43,6 +43,8 @@ struct rg_ctx {
   uint32_t* r1v_blocks = nullptr;  // per-block draw counts / offsets
   uint64_t r1v_blocks_cap = 0;
   unsigned long long* r1v_base = nullptr;
+  uint32_t* cluster_coins = nullptr;            // [phases][n_words] common-coin table
+  uint64_t cluster_coins_cap = 0;               // words
   unsigned long long* cluster_part = nullptr;  // [blocks][kClusterStats]
   unsigned long long* cluster_stats = nullptr;  // [kClusterStats]
   std::string err;
@@ -123,6 +125,13 @@ struct Disp {
     hipLaunchKernelGGL((wmvc_cluster_kernel<N>), dim3(grid), dim3(256), 0, s, st, stride, n_slots, base, q, fp1,
                        key, cs, dseed, maxp, info, part);
   }
+  static void cluster_lc(uint32_t grid, hipStream_t s, const uint32_t* st, uint64_t stride, uint64_t n_slots,
+                         uint64_t base, uint32_t q, uint32_t fp1, Key key, uint64_t cs, uint64_t dseed,
+                         uint32_t maxp, uint32_t* info, unsigned long long* part, const uint32_t* coins,
+                         uint32_t coin_phases, uint64_t chunk) {
+    hipLaunchKernelGGL((wmvc_cluster_lc_kernel<N>), dim3(grid), dim3(256), 0, s, st, stride, n_slots, base, q, fp1,
+                       key, cs, dseed, maxp, info, part, coins, coin_phases, chunk);
+  }
 };
 
 using ClusterLaunch = void (*)(uint32_t, hipStream_t, const uint32_t*, uint64_t, uint64_t, uint64_t, uint32_t,
@@ -140,6 +149,10 @@ const StepLaunch kRefLaunch[17] = RG_TABLE(ref);
 const StepLaunch kWmvcLaunch[17] = RG_TABLE(wmvc);
 const DigestLaunch kDigestLaunch[17] = RG_TABLE(digest);
 const ClusterLaunch kClusterLaunch[17] = RG_TABLE(cluster);
+using ClusterLcLaunch = void (*)(uint32_t, hipStream_t, const uint32_t*, uint64_t, uint64_t, uint64_t, uint32_t,
+                                 uint32_t, Key, uint64_t, uint64_t, uint32_t, uint32_t*, unsigned long long*,
+                                 const uint32_t*, uint32_t, uint64_t);
+const ClusterLcLaunch kClusterLcLaunch[17] = RG_TABLE(cluster_lc);
 
 hipStream_t pick_stream(rg_ctx* ctx, void* stream) {
   return stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
@@ -296,6 +309,7 @@ int rg_destroy(rg_ctx* ctx) {
   (void)hipFree(ctx->r1v_cells);
   (void)hipFree(ctx->r1v_blocks);
   (void)hipFree(ctx->r1v_base);
+  (void)hipFree(ctx->cluster_coins);
   (void)hipFree(ctx->cluster_part);
   (void)hipFree(ctx->cluster_stats);
   (void)hipFree(ctx->d_votes);
@@ -615,9 +629,25 @@ int rg_wmvc_cluster_async(rg_ctx* ctx, const uint32_t* states_dev, uint64_t stri
     RG_HIP(ctx, hipMalloc(&ctx->cluster_stats, kClusterStats * 8));
   }
   hipStream_t s = pick_stream(ctx, stream);
-  kClusterLaunch[ctx->cfg.n_replicas](grid, s, states_dev, stride_words, n_slots, slot_base, ctx->q, ctx->fp1,
-                                      ctx->coin_key, ctx->coin_stream, delivery_seed, max_phases, info_dev,
-                                      ctx->cluster_part);
+  // coin bits of the first phases precomputed (one ChaCha12 block per 512 slots and
+  // phase instead of one per lane and phase); later phases (rare) compute inline
+  const uint32_t coin_phases = max_phases < 16 ? max_phases : 16;
+  const uint64_t n_words = (n_slots + 31) / 32;
+  if (coin_phases * n_words > ctx->cluster_coins_cap) {
+    RG_HIP(ctx, hipDeviceSynchronize());
+    (void)hipFree(ctx->cluster_coins);
+    ctx->cluster_coins = nullptr;
+    ctx->cluster_coins_cap = 0;
+    RG_HIP(ctx, hipMalloc(&ctx->cluster_coins, coin_phases * n_words * 4));
+    ctx->cluster_coins_cap = coin_phases * n_words;
+  }
+  const uint64_t groups = ((n_words + 15) / 16) * coin_phases;
+  hipLaunchKernelGGL(coin_table_kernel, dim3((uint32_t)((groups + 255) / 256)), dim3(256), 0, s, ctx->coin_key,
+                     ctx->coin_stream, slot_base, n_slots, coin_phases, ctx->cluster_coins);
+  const uint64_t chunk = (n_slots + grid - 1) / grid;
+  kClusterLcLaunch[ctx->cfg.n_replicas](grid, s, states_dev, stride_words, n_slots, slot_base, ctx->q, ctx->fp1,
+                                        ctx->coin_key, ctx->coin_stream, delivery_seed, max_phases, info_dev,
+                                        ctx->cluster_part, ctx->cluster_coins, coin_phases, chunk);
   unsigned long long* dst = stats_dev ? reinterpret_cast<unsigned long long*>(stats_dev) : ctx->cluster_stats;
   hipLaunchKernelGGL(cluster_stats_kernel, dim3(1), dim3(64), 0, s, ctx->cluster_part, grid, dst);
   RG_HIP(ctx, hipGetLastError());

@@ -1195,7 +1195,9 @@ __device__ __forceinline__ uint32_t heard_mask(uint64_t dseed, uint64_t slot, ui
   const uint64_t h = mix64(cluster_key(dseed, phase, round, r) + slot);
   uint32_t avail = ((1u << N) - 1u) & ~(1u << r);
   uint32_t mask = 1u << r;
-  for (uint32_t i = 0; i + 1 < q; i++) {
+#pragma unroll
+  for (uint32_t i = 0; i + 1 < (uint32_t)N; i++) {  // unrolled: span is a constant, % is a mul-shift
+    if (i + 1 >= q) break;
     const uint32_t span = N - 1 - i;
     const uint32_t k = (uint32_t)((h >> (6 * i)) & 63u) % span;
     uint32_t a = avail;
@@ -1286,6 +1288,159 @@ __global__ __launch_bounds__(256) void wmvc_cluster_kernel(const uint32_t* state
     unsigned long long v = 0;
     for (int w = 0; w < 4; w++) v = k == 3 ? (red[w][k] > v ? red[w][k] : v) : v + red[w][k];
     partials[(uint64_t)blockIdx.x * kClusterStats + k] = v;  // plain stores: folded by the next launch
+  }
+}
+
+// Common-coin table for the cluster kernel: coin bits of phases 1..P for the
+// window's slots, [P][n_words]; one thread per 512-slot group (16 words) computes
+// the one or two ChaCha12 blocks that cover it (the same bits as coin_kernel).
+__global__ void coin_table_kernel(Key key, uint64_t stream, uint64_t slot_base, uint64_t n_slots,
+                                  uint32_t phases, uint32_t* tab) {
+  const uint64_t n_words = (n_slots + 31) / 32, n_groups = (n_words + 15) / 16;
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_groups * phases) return;
+  const uint64_t g = t % n_groups, phase = t / n_groups + 1;
+  const uint64_t id0 = slot_base + 512 * g;  // first slot id of the group
+  uint32_t a[16], b[16];
+  chacha_block<12>(key, ((phase - 1) << 40) | (id0 >> 9), stream, a);
+  const uint32_t sh = (uint32_t)(id0 & 511u);
+  if (sh) chacha_block<12>(key, ((phase - 1) << 40) | ((id0 >> 9) + 1), stream, b);
+  else
+#pragma unroll
+    for (int k = 0; k < 16; k++) b[k] = 0;
+  for (uint32_t k = 0; k < 16; k++) {
+    const uint64_t w = 16 * g + k;
+    if (w >= n_words) break;
+    // bits [sh + 32k, sh + 32k + 32) of the 1024-bit concatenation a|b
+    const uint32_t bit = sh + 32 * k, wi = bit >> 5, bo = bit & 31u;
+    const uint32_t lo = wi < 16 ? select16(a, wi) : select16(b, wi - 16);
+    const uint32_t hi = (wi + 1) < 16 ? select16(a, wi + 1) : select16(b, (wi + 1 - 16) & 15u);
+    const uint32_t v = bo ? ((lo >> bo) | (hi << (32 - bo))) : lo;
+    tab[(phase - 1) * n_words + w] = v & valid_mask(w, n_words, n_slots);
+  }
+}
+
+// Lane-compacted cluster kernel: each workgroup owns a contiguous chunk of slots;
+// a lane whose slot terminated takes the next slot of the chunk (wave-aggregated
+// LDS counter), so a wave never idles on its slowest slot (phases per slot vary
+// 1..max). Coins come from coin_table_kernel for phases <= coin_phases.
+template <int N>
+__global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* states, uint64_t stride,
+                                                              uint64_t n_slots, uint64_t slot_base, uint32_t q,
+                                                              uint32_t fp1, Key ckey, uint64_t coin_stream,
+                                                              uint64_t dseed, uint32_t max_phases, uint32_t* info,
+                                                              unsigned long long* partials, const uint32_t* coin_tab,
+                                                              uint32_t coin_phases, uint64_t chunk) {
+  constexpr uint32_t kAll = (1u << N) - 1u;
+  __shared__ unsigned long long s_next;
+  const uint64_t n_words = (n_slots + 31) / 32;
+  const uint64_t c0 = (uint64_t)blockIdx.x * chunk;
+  const uint64_t c1 = c0 + chunk < n_slots ? c0 + chunk : n_slots;
+  if (threadIdx.x == 0) s_next = c0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  unsigned long long acc[kClusterStats] = {0, 0, 0, 0, 0, 0, 0, 0};
+  bool active = false;
+  uint64_t s = 0, id = 0;
+  uint32_t st = 0, decided = 0, decv = 0, p = 0, first = 0, coins = 0;
+  for (;;) {
+    const unsigned long long idle = __ballot(!active);
+    if (idle) {
+      const uint32_t cnt = (uint32_t)__builtin_popcountll(idle);
+      const int leader = __builtin_ctzll(idle);
+      unsigned long long base = 0;
+      if (lane == leader) base = atomicAdd(&s_next, (unsigned long long)cnt);
+      base = __shfl(base, leader, 64);
+      if (!active) {
+        const uint32_t rank = (uint32_t)__builtin_popcountll(idle & ((1ull << lane) - 1ull));
+        const uint64_t ns = base + rank;
+        if (ns < c1) {
+          s = ns;
+          id = slot_base + s;
+          st = 0;
+#pragma unroll
+          for (int r = 0; r < N; r++) st |= ((states[(uint64_t)r * stride + s / 32] >> (s & 31)) & 1u) << r;
+          decided = decv = first = coins = 0;
+          p = 1;
+          active = true;
+        }
+      }
+    }
+    if (!__ballot(active)) break;
+    if (!active) continue;
+    // ---- one phase of every replica of slot s (same rules as wmvc_cluster_kernel)
+    uint32_t v1 = 0, vq = 0;
+#pragma unroll
+    for (int r = 0; r < N; r++) {
+      const uint32_t h = heard_mask<N>(dseed, id, p, 1, r, q);
+      const uint32_t c1r = __builtin_popcount(h & st), c0r = __builtin_popcount(h & ~st);
+      if (c1r >= q) v1 |= 1u << r;
+      else if (c0r < q) vq |= 1u << r;
+    }
+    uint32_t nst = 0;
+    int coin = -1;
+#pragma unroll
+    for (int r = 0; r < N; r++) {
+      const uint32_t h = heard_mask<N>(dseed, id, p, 2, r, q);
+      const uint32_t c1r = __builtin_popcount(h & v1), cq = __builtin_popcount(h & vq);
+      const uint32_t c0r = q - c1r - cq;
+      int nv = c0r >= fp1 ? 0 : (c1r >= fp1 ? 1 : -1);
+      if (nv >= 0 && !((decided >> r) & 1u)) {
+        decided |= 1u << r;
+        decv |= (uint32_t)nv << r;
+        if (!first) first = p;
+      }
+      if (nv < 0) {
+        if (c0r > 0) nv = 0;
+        else if (c1r > 0) nv = 1;
+        else {
+          if (coin < 0) {
+            if (p <= coin_phases) {
+              coin = (int)((coin_tab[(uint64_t)(p - 1) * n_words + s / 32] >> (s & 31)) & 1u);
+            } else {
+              uint32_t blk[16];
+              chacha_block<12>(ckey, ((uint64_t)(p - 1) << 40) | (id >> 9), coin_stream, blk);
+              coin = (int)((select16(blk, (uint32_t)(id >> 5) & 15u) >> (id & 31)) & 1u);
+            }
+            coins++;
+          }
+          nv = coin;
+        }
+      }
+      if ((decided >> r) & 1u) nv = (int)((decv >> r) & 1u);
+      nst |= (uint32_t)nv << r;
+    }
+    st = nst;
+    const bool all = decided == kAll;
+    if (all || p >= max_phases) {
+      const uint32_t phases = all ? p : 0u;
+      const uint32_t dec = all ? (decv & 1u) : kCodeNone;
+      info[s] = dec | (phases << 8) | (first << 16) | (coins << 24);
+      acc[0] += all;
+      acc[1] += dec == kCodeV1;
+      acc[2] += phases;
+      acc[3] = phases > acc[3] ? phases : acc[3];
+      acc[4] += coins;
+      acc[5] += first;
+      acc[6] += 1;
+      active = false;
+    } else {
+      p++;
+    }
+  }
+  __shared__ unsigned long long red[4][kClusterStats];
+  const int wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < kClusterStats; k++) acc[k] = k == 3 ? wave_max64(acc[k]) : wave_sum64(acc[k]);
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < kClusterStats; k++) red[wave][k] = acc[k];
+  __syncthreads();
+  if (threadIdx.x < kClusterStats) {
+    const int k = threadIdx.x;
+    unsigned long long v = 0;
+    for (int w = 0; w < 4; w++) v = k == 3 ? (red[w][k] > v ? red[w][k] : v) : v + red[w][k];
+    partials[(uint64_t)blockIdx.x * kClusterStats + k] = v;
   }
 }
 
