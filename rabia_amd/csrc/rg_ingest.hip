@@ -317,6 +317,9 @@ int rg_ingest_votes_async(rg_ingest* g, const uint8_t* msgs_dev, const uint64_t*
     g->cells_cap = 0;
     ING_HIP(g, hipMalloc(&g->cells, cells * 4));
     ING_HIP(g, hipMemset(g->cells, 0, cells * 4));
+    // hipMemset runs on the null stream, which does not order against the
+    // non-blocking launch stream: finish it before the parse kernel claims cells.
+    ING_HIP(g, hipDeviceSynchronize());
     g->cells_cap = cells;
   }
   if (n_msgs > g->msg_cap) {

@@ -66,10 +66,10 @@ def run(variant, k):
 
 variants = {
     "big": {"tiled": True, "diag": 1 << 8},
-    "big_ntst": {"tiled": True, "diag": 8 | (1 << 8)},
+    "big_no_lookback": {"tiled": True, "diag": 1 | (1 << 8)},
     "t_probe": {"tiled": True, "probe": True},
     "big_s28": {"tiled": True, "diag": 1 << 8, "slots": 1 << 28},
-    "big_ntst_s28": {"tiled": True, "diag": 8 | (1 << 8), "slots": 1 << 28},
+    "big_no_lookback_s28": {"tiled": True, "diag": 1 | (1 << 8), "slots": 1 << 28},
     "t_probe_s28": {"tiled": True, "probe": True, "slots": 1 << 28},
     "auto_1M": {"tiled": True, "slots": 1 << 20},
 }
