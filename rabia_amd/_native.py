@@ -14,7 +14,7 @@ import re
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
-LIB_PATH = os.path.join(PKG, "lib", "librabia_gpu.so")
+LIB_PATH = os.environ.get("RABIA_GPU_LIB") or os.path.join(PKG, "lib", "librabia_gpu.so")  # override: A/B runs
 HEADER = os.path.join(ROOT, "include", "rabia_gpu.h")
 HEADERS = [HEADER] + [os.path.join(ROOT, "include", h) for h in ("rabia_kv.h", "rabia_ingest.h")]
 
@@ -136,7 +136,7 @@ def header_symbols() -> list[str]:
 
 
 def load():
-    """Load librabia_gpu.so (building it first if the sources are newer)."""
+    """Load librabia_gpu.so (building it first if it is missing)."""
     global _lib
     if _lib is not None:
         return _lib

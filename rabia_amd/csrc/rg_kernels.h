@@ -311,31 +311,37 @@ __device__ __forceinline__ uint32_t wave_min32(uint32_t v) {
   return v;
 }
 
-// Three 21-bit sums packed in one u64 (per-wave values <= 8192, per-tile <= 65536).
+// The four sums travel as 16-bit fields of one u64 through ONE wave reduction
+// (a wave covers 64 * W * 32 <= 65535 slots, so no field overflows). The two
+// offsets need no reduction: a thread's offsets are relative to the tile and
+// threads own ascending word ranges, so the block maximum of max_off1 is the
+// value of the highest thread that has one, and the minimum of min_off that of
+// the lowest (a ballot plus a uniform readlane per wave, then the same pick
+// across waves).
 template <int BLOCK>
 __device__ __forceinline__ TileStats block_reduce_stats(TileStats s, int lane, int wave) {
   constexpr int WAVES = BLOCK / 64;
-  __shared__ unsigned long long red[WAVES][3];
-  unsigned long long packed = (unsigned long long)s.dec | ((unsigned long long)s.v1 << 21) |
-                              ((unsigned long long)s.pend << 42);
+  __shared__ unsigned long long red[WAVES][2];
+  unsigned long long packed = (unsigned long long)s.dec | ((unsigned long long)s.v1 << 16) |
+                              ((unsigned long long)s.pend << 32) | ((unsigned long long)s.draws << 48);
   packed = wave_sum64(packed);
-  const uint32_t draws = wave_sum32(s.draws);
-  const uint32_t mx = wave_max32(s.max_off1), mn = wave_min32(s.min_off);
+  const unsigned long long hmx = __ballot(s.max_off1 != 0u), hmn = __ballot(s.min_off != ~0u);
+  const uint32_t mx = hmx ? __builtin_amdgcn_readlane(s.max_off1, 63 - __builtin_clzll(hmx)) : 0u;
+  const uint32_t mn = hmn ? __builtin_amdgcn_readlane(s.min_off, __builtin_ctzll(hmn)) : ~0u;
   if (lane == 0) {
     red[wave][0] = packed;
-    red[wave][1] = draws;
-    red[wave][2] = ((unsigned long long)mn << 32) | mx;
+    red[wave][1] = ((unsigned long long)mn << 32) | mx;
   }
   lds_barrier();
   TileStats r{0, 0, 0, 0, 0, ~0u};
 #pragma unroll
   for (int w = 0; w < WAVES; w++) {
     const unsigned long long x = red[w][0];
-    r.dec += (uint32_t)(x & 0x1FFFFFu);
-    r.v1 += (uint32_t)((x >> 21) & 0x1FFFFFu);
-    r.pend += (uint32_t)(x >> 42);
-    r.draws += (uint32_t)red[w][1];
-    const uint32_t wmx = (uint32_t)red[w][2], wmn = (uint32_t)(red[w][2] >> 32);
+    r.dec += (uint32_t)(x & 0xFFFFu);
+    r.v1 += (uint32_t)((x >> 16) & 0xFFFFu);
+    r.pend += (uint32_t)((x >> 32) & 0xFFFFu);
+    r.draws += (uint32_t)(x >> 48);
+    const uint32_t wmx = (uint32_t)red[w][1], wmn = (uint32_t)(red[w][1] >> 32);
     r.max_off1 = wmx > r.max_off1 ? wmx : r.max_off1;
     r.min_off = wmn < r.min_off ? wmn : r.min_off;
   }
@@ -375,6 +381,7 @@ __device__ __forceinline__ void finish_tile(const StepParams& p, Record* rec, Ti
                                             uint32_t tile, int tid, int lane, int wave) {
   constexpr uint64_t kTileSlots = (uint64_t)BLOCK * W * 32;
   constexpr int kBatch = 8;  // tiles per thread with loads in flight together
+  static_assert(64 * W * 32 <= 0xFFFF, "per-wave sums must fit the 16-bit packed fields");
   const TileStats b = block_reduce_stats<BLOCK>(ts, lane, wave);
   const unsigned long long tag = stat_tag(p.seq);
   if (tid == 0) {
