@@ -14,3 +14,11 @@ import json
 for v in ("new","old"):
     print(v, [round(json.load(open(f"gpurun_out/ab/{v}_{i}.json"))["roofline"]["kernel_avg_us"],1) for i in (1,2,3)])
 P
+timeout -k 10 120 python tools/latency_1m.py > gpurun_out/ab/lat_new.json || exit 1
+RABIA_GPU_LIB=$PWD/rabia_amd/lib/ab/librabia_gpu_old.so timeout -k 10 120 python tools/latency_1m.py > gpurun_out/ab/lat_old.json || exit 1
+python - <<'P'
+import json
+for v in ("new", "old"):
+    d = json.load(open(f"gpurun_out/ab/lat_{v}.json"))["us_per_launch_median"]
+    print("1M", v, {k: d[k] for k in ("auto", "auto_no_lookback", "auto_no_stats")})
+P
