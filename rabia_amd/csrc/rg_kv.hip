@@ -33,7 +33,15 @@
 namespace {
 
 constexpr uint64_t kEmpty = 0;
-constexpr uint64_t kInvalidKey = ~0ull;    // sort key of commands that are not applied
+constexpr uint64_t kInvalidKey = ~0ull;    // full hash of commands that are not applied
+// Sort key: a 31-bit bucket of the full hash (equal hashes -> equal buckets), so the
+// radix sort runs 4 digit passes instead of 8; commands that are not applied get
+// kInvalidBucket and sort last. A bucket run may hold several hashes: the walkers
+// already split runs into keys by comparing key bytes, and look each key up with
+// its own full hash.
+constexpr uint64_t kInvalidBucket = 0xFFFFFFFFull;
+constexpr int kSortBits = 32;
+__device__ __forceinline__ uint64_t hash_bucket(uint64_t h) { return (h ^ (h >> 32)) & 0x7FFFFFFFull; }
 constexpr uint32_t kMaxKeyLen = 256;       // store.rs:467
 constexpr int kBlock = 256;
 constexpr int kMaxRunKeys = 8;             // distinct keys per hash run on the keyed path
@@ -132,7 +140,7 @@ __device__ bool bytes_eq(const uint8_t* a, const uint8_t* b, uint32_t n) {
 // ---- 1 decode ----------------------------------------------------------------
 __global__ void kv_decode_kernel(const uint8_t* __restrict__ data, const uint64_t* __restrict__ off,
                                  uint64_t n, const uint8_t* __restrict__ mask, uint64_t max_value, uint64_t hmask,
-                                 KvOp* __restrict__ ops, uint64_t* __restrict__ sort_key,
+                                 KvOp* __restrict__ ops, uint64_t* __restrict__ sort_key, uint64_t* __restrict__ full_hash,
                                  uint32_t* __restrict__ sort_idx, uint8_t* __restrict__ results) {
   const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= n) return;
@@ -177,7 +185,8 @@ __global__ void kv_decode_kernel(const uint8_t* __restrict__ data, const uint64_
     }
   }
   ops[c] = op;
-  sort_key[c] = key;
+  sort_key[c] = key == kInvalidKey ? kInvalidBucket : hash_bucket(key);
+  full_hash[c] = key;
   sort_idx[c] = (uint32_t)c;
   if (op.status != kPending) results[c] = (uint8_t)op.status;
 }
@@ -227,7 +236,8 @@ struct StoreView {
 struct BatchView {
   const uint8_t* data;
   const KvOp* ops;
-  const uint64_t* skey;   // sorted hashes
+  const uint64_t* skey;   // sorted hash buckets
+  const uint64_t* hfull;  // full key hash per command index
   const uint32_t* sidx;   // command index per sorted position
   uint64_t n;
   uint8_t* results;
@@ -315,7 +325,7 @@ __global__ __launch_bounds__(kBlock) void kv_walk_kernel(BatchView b, StoreView 
   const bool go = !COMMIT || st.ctr->mode == 0;
   if (go && i < b.n) {
     const uint64_t h = b.skey[i];
-    if (h != kInvalidKey && (i == 0 || b.skey[i - 1] != h)) {
+    if (h != kInvalidBucket && (i == 0 || b.skey[i - 1] != h)) {
       uint64_t end = i + 1;
       while (end < b.n && b.skey[end] == h) end++;
       uint64_t need = 0, heap_pos = COMMIT ? st.ctr->batch_base + b.heap_off[i] : 0;
@@ -324,8 +334,9 @@ __global__ __launch_bounds__(kBlock) void kv_walk_kernel(BatchView b, StoreView 
         if (b.done[first]) continue;
         if (++keys > kMaxRunKeys) { acc[kPOverflow] = 1; break; }
         const KvOp lead = b.ops[b.sidx[first]];
+        const uint64_t hl = b.hfull[b.sidx[first]];
         const uint8_t* kp = b.data + lead.key_off;
-        const int64_t slot = table_find(st.hashes, st.ent, st.heap, st.mask, h, kp, lead.key_len);
+        const int64_t slot = table_find(st.hashes, st.ent, st.heap, st.mask, hl, kp, lead.key_len);
         const KeyOutcome o = replay_key<COMMIT>(b, st, first, end, lead, slot, true);
         acc[kPOps] += o.n_ops;
         acc[kPVersion] += o.n_version;
@@ -340,7 +351,7 @@ __global__ __launch_bounds__(kBlock) void kv_walk_kernel(BatchView b, StoreView 
         if (COMMIT) {
           int64_t s = slot;
           if (new_slot) {
-            s = table_claim(st.hashes, st.mask, h);
+            s = table_claim(st.hashes, st.mask, hl);
             if (s < 0) { atomicOr(&st.ctr->flags, kFaultTable); continue; }
             uint8_t* dst = st.heap + heap_pos;
             for (uint32_t k = 0; k < lead.key_len; k++) dst[k] = kp[k];
@@ -550,7 +561,7 @@ struct rg_kv {
   // per-batch scratch
   uint64_t cap_cmds = 0;
   KvOp* ops = nullptr;
-  uint64_t *key_a = nullptr, *key_b = nullptr, *need = nullptr, *heap_off = nullptr;
+  uint64_t *key_a = nullptr, *key_b = nullptr, *hfull = nullptr, *need = nullptr, *heap_off = nullptr;
   uint32_t *idx_a = nullptr, *idx_b = nullptr;
   uint8_t* done = nullptr;
   unsigned long long* part = nullptr;
@@ -580,10 +591,10 @@ StoreView view(rg_kv* kv) {
 }
 
 void free_scratch(rg_kv* kv) {
-  (void)hipFree(kv->ops); (void)hipFree(kv->key_a); (void)hipFree(kv->key_b);
+  (void)hipFree(kv->ops); (void)hipFree(kv->key_a); (void)hipFree(kv->key_b); (void)hipFree(kv->hfull);
   (void)hipFree(kv->need); (void)hipFree(kv->heap_off); (void)hipFree(kv->idx_a);
   (void)hipFree(kv->idx_b); (void)hipFree(kv->done); (void)hipFree(kv->part); (void)hipFree(kv->tmp);
-  kv->ops = nullptr; kv->key_a = kv->key_b = kv->need = kv->heap_off = nullptr;
+  kv->ops = nullptr; kv->key_a = kv->key_b = kv->hfull = kv->need = kv->heap_off = nullptr;
   kv->idx_a = kv->idx_b = nullptr; kv->done = nullptr; kv->part = nullptr; kv->tmp = nullptr;
   kv->cap_cmds = 0; kv->tmp_bytes = 0;
 }
@@ -598,6 +609,7 @@ int ensure_scratch(rg_kv* kv, uint64_t n) {
   KV_HIP(kv, hipMalloc(&kv->ops, cap * sizeof(KvOp)));
   KV_HIP(kv, hipMalloc(&kv->key_a, cap * 8));
   KV_HIP(kv, hipMalloc(&kv->key_b, cap * 8));
+  KV_HIP(kv, hipMalloc(&kv->hfull, cap * 8));
   KV_HIP(kv, hipMalloc(&kv->need, cap * 8));
   KV_HIP(kv, hipMalloc(&kv->heap_off, cap * 8));
   KV_HIP(kv, hipMalloc(&kv->idx_a, cap * 4));
@@ -606,7 +618,7 @@ int ensure_scratch(rg_kv* kv, uint64_t n) {
   KV_HIP(kv, hipMalloc(&kv->part, blocks * kPCount * 8));
   size_t t1 = 0, t2 = 0;
   KV_HIP(kv, hipcub::DeviceRadixSort::SortPairs(nullptr, t1, kv->key_a, kv->key_b, kv->idx_a, kv->idx_b,
-                                                  (int)cap, 0, 64, kv->stream));
+                                                  (int)cap, 0, kSortBits, kv->stream));
   KV_HIP(kv, hipcub::DeviceScan::ExclusiveSum(nullptr, t2, kv->need, kv->heap_off, (int)cap, kv->stream));
   kv->tmp_bytes = t1 > t2 ? t1 : t2;
   KV_HIP(kv, hipMalloc(&kv->tmp, kv->tmp_bytes));
@@ -710,13 +722,13 @@ int rg_kv_apply_async(rg_kv* kv, const uint8_t* data_dev, const uint64_t* cmd_of
   hipLaunchKernelGGL(kv_decode_kernel, dim3(blocks), dim3(kBlock), 0, s, data_dev, cmd_off_dev, n_cmds,
                      apply_mask_dev, kv->cfg.max_value_size,
                      kv->cfg.hash_bits && kv->cfg.hash_bits < 64 ? (1ull << kv->cfg.hash_bits) - 1 : ~0ull,
-                     kv->ops, kv->key_a, kv->idx_a, results_dev);
+                     kv->ops, kv->key_a, kv->hfull, kv->idx_a, results_dev);
   KV_HIP(kv, hipGetLastError());
   size_t tb = kv->tmp_bytes;
   KV_HIP(kv, hipcub::DeviceRadixSort::SortPairs(kv->tmp, tb, kv->key_a, kv->key_b, kv->idx_a, kv->idx_b,
-                                                  (int)n_cmds, 0, 64, s));
+                                                  (int)n_cmds, 0, kSortBits, s));
   KV_HIP(kv, hipMemsetAsync(kv->done, 0, n_cmds, s));
-  BatchView b{data_dev, kv->ops, kv->key_b, kv->idx_b, n_cmds, results_dev, kv->done, kv->need,
+  BatchView b{data_dev, kv->ops, kv->key_b, kv->hfull, kv->idx_b, n_cmds, results_dev, kv->done, kv->need,
               kv->heap_off, kv->part};
   const StoreView st = view(kv);
   hipLaunchKernelGGL(kv_walk_kernel<false>, dim3(blocks), dim3(kBlock), 0, s, b, st);
@@ -727,7 +739,7 @@ int rg_kv_apply_async(rg_kv* kv, const uint8_t* data_dev, const uint64_t* cmd_of
                      kv->heap_off, n_cmds);
   KV_HIP(kv, hipMemsetAsync(kv->done, 0, n_cmds, s));
   hipLaunchKernelGGL(kv_walk_kernel<true>, dim3(blocks), dim3(kBlock), 0, s, b, st);
-  hipLaunchKernelGGL(kv_ordered_kernel, dim3(1), dim3(64), 0, s, data_dev, kv->ops, kv->key_a, n_cmds,
+  hipLaunchKernelGGL(kv_ordered_kernel, dim3(1), dim3(64), 0, s, data_dev, kv->ops, kv->hfull, n_cmds,
                      results_dev, st);
   hipLaunchKernelGGL(kv_finish_kernel, dim3(1), dim3(kBlock), 0, s, kv->ctr, kv->part, blocks);
   KV_HIP(kv, hipGetLastError());
