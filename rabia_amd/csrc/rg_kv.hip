@@ -131,10 +131,24 @@ __device__ bool utf8_valid(const uint8_t* p, uint64_t n) {
   return true;
 }
 
+// Key/value bytes sit at arbitrary byte offsets: compare and copy them 8 bytes at a
+// time through 1-byte-aligned u64 accesses (gfx950 global memory takes unaligned
+// dword accesses), then the tail byte by byte; nothing past the n bytes is touched.
+typedef uint64_t u64_unaligned __attribute__((aligned(1)));
+
 __device__ bool bytes_eq(const uint8_t* a, const uint8_t* b, uint32_t n) {
-  for (uint32_t i = 0; i < n; i++)
+  uint32_t i = 0;
+  for (; i + 8 <= n; i += 8)
+    if (*(const u64_unaligned*)(a + i) != *(const u64_unaligned*)(b + i)) return false;
+  for (; i < n; i++)
     if (a[i] != b[i]) return false;
   return true;
+}
+
+__device__ __forceinline__ void bytes_copy(uint8_t* dst, const uint8_t* src, uint32_t n) {
+  uint32_t i = 0;
+  for (; i + 8 <= n; i += 8) *(u64_unaligned*)(dst + i) = *(const u64_unaligned*)(src + i);
+  for (; i < n; i++) dst[i] = src[i];
 }
 
 // ---- 1 decode ----------------------------------------------------------------
@@ -354,7 +368,7 @@ __global__ __launch_bounds__(kBlock) void kv_walk_kernel(BatchView b, StoreView 
             s = table_claim(st.hashes, st.mask, hl);
             if (s < 0) { atomicOr(&st.ctr->flags, kFaultTable); continue; }
             uint8_t* dst = st.heap + heap_pos;
-            for (uint32_t k = 0; k < lead.key_len; k++) dst[k] = kp[k];
+            bytes_copy(dst, kp, lead.key_len);
             st.ent[s].key_off = heap_pos;
             st.ent[s].key_len = lead.key_len;
             heap_pos += kbytes;
@@ -364,7 +378,7 @@ __global__ __launch_bounds__(kBlock) void kv_walk_kernel(BatchView b, StoreView 
               const KvOp& sop = b.ops[o.last_set];
               const uint8_t* src = b.data + sop.val_off;
               uint8_t* dst = st.heap + heap_pos;
-              for (uint32_t k = 0; k < sop.val_len; k++) dst[k] = src[k];
+              bytes_copy(dst, src, sop.val_len);
               st.ent[s].val_off = heap_pos;
               st.ent[s].val_len = sop.val_len;
               heap_pos += vbytes;
@@ -443,14 +457,14 @@ __global__ void kv_ordered_kernel(const uint8_t* data, const KvOp* ops, const ui
         s = table_claim(st.hashes, st.mask, h);
         if (s < 0) { k->flags |= kFaultTable; break; }
         occ++;
-        for (uint32_t q = 0; q < op.key_len; q++) st.heap[top + q] = kp[q];
+        bytes_copy(st.heap + top, kp, op.key_len);
         st.ent[s].key_off = top;
         st.ent[s].key_len = op.key_len;
         st.ent[s].version = 0;
         top += op.key_len;
       }
       if (top + op.val_len > st.heap_cap) { k->flags |= kFaultHeap; break; }
-      for (uint32_t q = 0; q < op.val_len; q++) st.heap[top + q] = data[op.val_off + q];
+      bytes_copy(st.heap + top, data + op.val_off, op.val_len);
       st.ent[s].val_off = top;
       st.ent[s].val_len = op.val_len;
       top += op.val_len;
