@@ -40,6 +40,11 @@ constexpr uint64_t kInvalidKey = ~0ull;    // full hash of commands that are not
 // already split runs into keys by comparing key bytes, and look each key up with
 // its own full hash.
 constexpr uint64_t kInvalidBucket = 0xFFFFFFFFull;
+// Command bytes sit at arbitrary byte offsets: multi-byte fields, key compares and
+// copies go through 1-byte-aligned types (gfx950 global memory takes unaligned
+// dword accesses; little-endian like bincode's fixint encoding).
+typedef uint64_t u64_unaligned __attribute__((aligned(1)));
+typedef uint32_t u32_unaligned __attribute__((aligned(1)));
 constexpr int kSortBits = 32;
 __device__ __forceinline__ uint64_t hash_bucket(uint64_t h) { return (h ^ (h >> 32)) & 0x7FFFFFFFull; }
 constexpr uint32_t kMaxKeyLen = 256;       // store.rs:467
@@ -86,27 +91,28 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
 
 __device__ __forceinline__ uint64_t key_hash(const uint8_t* p, uint32_t n, uint64_t hmask) {
   uint64_t h = 0xcbf29ce484222325ull;  // FNV-1a 64, then a finaliser for the probe bits
-  for (uint32_t i = 0; i < n; i++) h = (h ^ p[i]) * 0x100000001b3ull;
+  uint32_t i = 0;
+  for (; i + 8 <= n; i += 8) {  // one 8-byte load, bytes folded in order from the register
+    uint64_t w = *(const u64_unaligned*)(p + i);
+#pragma unroll
+    for (int k = 0; k < 8; k++, w >>= 8) h = (h ^ (w & 0xFFu)) * 0x100000001b3ull;
+  }
+  for (; i < n; i++) h = (h ^ p[i]) * 0x100000001b3ull;
   h = fmix64(h ^ n) & hmask;
   if (h == kEmpty) h = 1;
   if (h == kInvalidKey) h = kInvalidKey - 1;
   return h;
 }
 
-__device__ __forceinline__ uint64_t ld_u64(const uint8_t* p) {
-  uint64_t v = 0;
-  for (int i = 7; i >= 0; i--) v = (v << 8) | p[i];
-  return v;
-}
-__device__ __forceinline__ uint32_t ld_u32(const uint8_t* p) {
-  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
-}
+__device__ __forceinline__ uint64_t ld_u64(const uint8_t* p) { return *(const u64_unaligned*)p; }
+__device__ __forceinline__ uint32_t ld_u32(const uint8_t* p) { return *(const u32_unaligned*)p; }
 
 // std::str::from_utf8 acceptance (no overlongs, no surrogates, <= U+10FFFF):
 // serde's String visitor rejects anything else, so bincode::deserialize fails.
 __device__ bool utf8_valid(const uint8_t* p, uint64_t n) {
   uint64_t i = 0;
   while (i < n) {
+    if (i + 8 <= n && (ld_u64(p + i) & 0x8080808080808080ull) == 0) { i += 8; continue; }  // 8 ASCII bytes
     const uint32_t c = p[i];
     if (c < 0x80) { i++; continue; }
     uint32_t need, lo = 0x80, hi = 0xBF;
@@ -132,9 +138,8 @@ __device__ bool utf8_valid(const uint8_t* p, uint64_t n) {
 }
 
 // Key/value bytes sit at arbitrary byte offsets: compare and copy them 8 bytes at a
-// time through 1-byte-aligned u64 accesses (gfx950 global memory takes unaligned
-// dword accesses), then the tail byte by byte; nothing past the n bytes is touched.
-typedef uint64_t u64_unaligned __attribute__((aligned(1)));
+// time through 1-byte-aligned u64 accesses, then the tail byte by byte; nothing past
+// the n bytes is touched.
 
 __device__ bool bytes_eq(const uint8_t* a, const uint8_t* b, uint32_t n) {
   uint32_t i = 0;
