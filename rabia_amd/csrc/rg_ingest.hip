@@ -29,6 +29,11 @@ struct Members {
   uint32_t n;
 };
 
+// Frames sit at arbitrary byte offsets: fields are read through 1-byte-aligned types
+// (gfx950 global memory takes unaligned dword accesses).
+typedef uint64_t u64_unaligned __attribute__((aligned(1)));
+typedef uint32_t u32_unaligned __attribute__((aligned(1)));
+
 struct Reader {
   const uint8_t* p;
   uint64_t len, pos;
@@ -39,15 +44,13 @@ struct Reader {
   }
   __device__ uint64_t u64() {
     if (!need(8)) return 0;
-    uint64_t v = 0;
-    for (int i = 7; i >= 0; i--) v = (v << 8) | p[pos + i];
+    const uint64_t v = *(const u64_unaligned*)(p + pos);  // bincode fixint: little-endian
     pos += 8;
     return v;
   }
   __device__ uint32_t u32() {
     if (!need(4)) return 0;
-    const uint32_t v = (uint32_t)p[pos] | ((uint32_t)p[pos + 1] << 8) | ((uint32_t)p[pos + 2] << 16) |
-                       ((uint32_t)p[pos + 3] << 24);
+    const uint32_t v = *(const u32_unaligned*)(p + pos);
     pos += 4;
     return v;
   }
