@@ -15,7 +15,8 @@
  *   Weak-MVC rounds + common coin (WMVC mode)  docs/weak_mvc.ivy:109-191
  *
  * Plain C types only (no HIP/torch types): streams are passed as `void*`
- * (a hipStream_t; NULL = the context's own stream). Every entry point returns
+ * (a hipStream_t; NULL = the context's own stream, a blocking stream: it orders
+ * with the legacy default stream, e.g. torch's default-stream fills). Every entry point returns
  * RG_OK (0) or a negative rg_status; rg_last_error() gives the text. No entry
  * point throws, retains a caller pointer past return, or falls back to the CPU:
  * without a usable gfx950 device rg_create fails with RG_ENODEV.
@@ -24,7 +25,9 @@
  *   V0 = 0, V1 = 1, VQuestion = 2, 3 = absent voter / None / pending.
  *
  * Layout: bit-sliced planes of 32-bit words; slot s of a
- * window is bit (s % 32) of word (s / 32). Plane pointers must be 16-B aligned.
+ * window is bit (s % 32) of word (s / 32). Plane pointers must be 16-B aligned;
+ * a step reads and writes whole 16-B groups (128 slots), so windows sharing a buffer
+ * start on 128-slot boundaries.
  * Two plane arrangements, chosen per context by rg_config.tile_words:
  *  - planar (tile_words = 0): plane p starts at p * stride_words; stride_words is
  *    a multiple of 4 and >= ceil(n_slots/32) (rg_plane_stride() gives the minimum);
@@ -51,7 +54,7 @@
 extern "C" {
 #endif
 
-#define RG_ABI_VERSION 2
+#define RG_ABI_VERSION 3
 #define RG_MAX_REPLICAS 16
 #define RG_OUT_PLANES 8
 
@@ -146,6 +149,36 @@ int rg_phase_step(rg_ctx* ctx, const uint32_t* votes_host, uint32_t* out_host,
                   uint64_t n_slots, uint64_t stride_words, uint64_t slot_base,
                   uint64_t phase, uint64_t max_phase, rg_step_result* result_host);
 int rg_last_result(rg_ctx* ctx, rg_step_result* out_host);
+
+/* ---- Sharded REF: ONE engine (one StdRng stream, engine.rs:59-62) over a window
+ * split into contiguous shards, one per GPU. Draw k of shard r is
+ * the engine's draw  rng_next + (VQ slots of shards 0..r-1) + k  — ascending slot
+ * order over the whole window, as one evaluator (engine.rs:567-611). Per window:
+ *  1. every shard: rg_phase_step_shard_async — evaluates its slots with draws taken
+ *     at a provisional position (no cross-GPU wait), writes one 8-B draw record per
+ *     VQ slot (records_dev, capacity records_cap; n_slots always suffices) and its
+ *     row (rg_step_result): counts, extremes and n_draws of its NON-VQ slots;
+ *  2. exchange the rows (all-gather, rank order) -> rows_dev[n_shards];
+ *  3. every shard: rg_shard_fixup_async — re-draws its VQ slots at their global
+ *     positions, XOR-patches the output bits that change, and writes its final row
+ *     (VQ slots counted in; rng_next = the engine position after the window); the
+ *     context's rng_next advances past every shard's draws;
+ *  4. exchange the final rows; every shard: rg_shard_commit_async folds them into
+ *     the context's engine state (last_committed, contiguous watermark, steps),
+ *     leaving every rank's state equal to one evaluator's over the whole window.
+ * Steps (1) never wait on (2)-(4), so they pipeline: the output buffer of a window
+ * must not be reused before its fix-up ran. row_dev / result_dev may be NULL. */
+int rg_phase_step_shard_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev,
+                              uint64_t n_slots, uint64_t stride_words, uint64_t slot_base,
+                              uint64_t max_phase, uint64_t* records_dev, uint64_t records_cap,
+                              rg_step_result* row_dev, void* stream);
+int rg_shard_fixup_async(rg_ctx* ctx, uint32_t* out_dev, uint64_t n_slots, uint64_t stride_words,
+                         uint64_t slot_base, uint64_t max_phase, const uint64_t* records_dev,
+                         uint64_t records_cap, const rg_step_result* rows_dev, uint32_t shard,
+                         uint32_t n_shards, rg_step_result* row_dev, void* stream);
+int rg_shard_commit_async(rg_ctx* ctx, const rg_step_result* rows_dev, uint32_t n_shards,
+                          uint64_t window_base, uint64_t window_slots, rg_step_result* result_dev,
+                          void* stream);
 
 /* Exchange stage: state bit = 1 iff some proposal digest is held by >= quorum
  * replicas (weak_mvc.ivy:109-128). digests_dev = [n][digest_stride] u64 (0 = no

@@ -85,6 +85,9 @@ _SIGS = {
     "rg_get_state": (ctypes.c_int, [vp, ctypes.POINTER(RgEngineState)]),
     "rg_phase_step_async": (ctypes.c_int, [vp, vp, vp, u64, u64, u64, u64, u64, vp, vp]),
     "rg_phase_step": (ctypes.c_int, [vp, vp, vp, u64, u64, u64, u64, u64, ctypes.POINTER(RgStepResult)]),
+    "rg_phase_step_shard_async": (ctypes.c_int, [vp, vp, vp, u64, u64, u64, u64, vp, u64, vp, vp]),
+    "rg_shard_fixup_async": (ctypes.c_int, [vp, vp, u64, u64, u64, u64, vp, u64, vp, u32, u32, vp, vp]),
+    "rg_shard_commit_async": (ctypes.c_int, [vp, vp, u32, u64, u64, vp, vp]),
     "rg_last_result": (ctypes.c_int, [vp, ctypes.POINTER(RgStepResult)]),
     "rg_digest_majority_async": (ctypes.c_int, [vp, vp, u64, vp, u64, vp]),
     "rg_coin_async": (ctypes.c_int, [vp, u64, u64, u64, vp, vp]),
@@ -144,9 +147,12 @@ def load():
         import torch  # noqa: F401
     except Exception:  # pragma: no cover - torch is optional for the binding itself
         pass
-    if not os.path.exists(LIB_PATH):
+    if LIB_PATH == os.path.join(PKG, "lib", "librabia_gpu.so"):
         from . import build as _build
-        _build.build()
+        if _build.needs_build():  # missing, or older than one of its sources
+            _build.build()
+    elif not os.path.exists(LIB_PATH):
+        raise FileNotFoundError(f"RABIA_GPU_LIB={LIB_PATH} does not exist")
     lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
     for name, (res, args) in _SIGS.items():
         fn = getattr(lib, name)

@@ -15,7 +15,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB_DIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIB_DIR, "librabia_gpu.so")
-SOURCES = [os.path.join(CSRC, f) for f in ("rabia_gpu.hip", "rg_kv.hip", "rg_ingest.hip")]
+SOURCES = [os.path.join(CSRC, f) for f in ("rabia_gpu.hip", "rg_shard.hip", "rg_kv.hip", "rg_ingest.hip")]
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("rg_common.h", "rg_kernels.h")] + [
     os.path.join(ROOT, "include", "rabia_gpu.h"), os.path.join(ROOT, "include", "rabia_gpu_debug.h"),
     os.path.join(ROOT, "include", "rabia_kv.h"), os.path.join(ROOT, "include", "rabia_ingest.h")]

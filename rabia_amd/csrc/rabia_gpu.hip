@@ -18,6 +18,10 @@
 
 using namespace rg;
 
+namespace rg {
+void launch_ref_shard(int n, int block, int words, uint32_t grid, hipStream_t s, const StepParams& p);
+}
+
 struct rg_ctx {
   rg_config cfg{};
   uint32_t q = 0, fp1 = 0;
@@ -47,6 +51,7 @@ struct rg_ctx {
   uint64_t cluster_coins_cap = 0;               // words
   unsigned long long* cluster_part = nullptr;  // [blocks][kClusterStats]
   unsigned long long* cluster_stats = nullptr;  // [kClusterStats]
+  unsigned long long* fix_acc = nullptr;        // sharded REF fix-up accumulator [4]
   std::string err;
 };
 
@@ -74,7 +79,7 @@ int hip_fail(rg_ctx* ctx, hipError_t e, const char* what) {
 constexpr int wmax_for(int n) { return n <= 5 ? 4 : (n <= 10 ? 2 : 1); }
 
 // Tile shapes: {threads, words per thread}. Big tiles keep the per-launch count
-// of tile tickets and look-back hand-offs low on large windows; small tiles fill
+// of tiles and look-back hand-offs low on large windows; small tiles fill
 // the 256 CUs on single 2^20-slot windows.
 enum TileCfg { kCfgBig = 0, kCfgMid = 1, kCfgSmall = 2, kCfgBigW2 = 3, kCfgMidW2 = 4 };
 constexpr int cfg_block(int c) { return (c == kCfgBig || c == kCfgBigW2) ? 512 : (c == kCfgSmall ? 128 : 256); }
@@ -95,17 +100,17 @@ struct Disp {
   static void ref(int c, uint32_t grid, hipStream_t s, const StepParams& p) {
     if constexpr (N == 5) {  // diagnostic shapes (rg_debug_set force 4, 5): 2 words per thread
       if (c == kCfgBigW2) {
-        hipLaunchKernelGGL((ref_step_kernel<N, 2, 512>), dim3(grid), dim3(512), 0, s, p);
+        hipLaunchKernelGGL((ref_step_kernel<N, 2, 512, false>), dim3(grid), dim3(512), 0, s, p);
         return;
       }
       if (c == kCfgMidW2) {
-        hipLaunchKernelGGL((ref_step_kernel<N, 2, 256>), dim3(grid), dim3(256), 0, s, p);
+        hipLaunchKernelGGL((ref_step_kernel<N, 2, 256, false>), dim3(grid), dim3(256), 0, s, p);
         return;
       }
     }
-    if (c == kCfgBig) hipLaunchKernelGGL((ref_step_kernel<N, WM, 512>), dim3(grid), dim3(512), 0, s, p);
-    else if (c == kCfgMid) hipLaunchKernelGGL((ref_step_kernel<N, WM, 256>), dim3(grid), dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((ref_step_kernel<N, 1, 128>), dim3(grid), dim3(128), 0, s, p);
+    if (c == kCfgBig) hipLaunchKernelGGL((ref_step_kernel<N, WM, 512, false>), dim3(grid), dim3(512), 0, s, p);
+    else if (c == kCfgMid) hipLaunchKernelGGL((ref_step_kernel<N, WM, 256, false>), dim3(grid), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((ref_step_kernel<N, 1, 128, false>), dim3(grid), dim3(128), 0, s, p);
   }
   static void wmvc(int c, uint32_t grid, hipStream_t s, const StepParams& p) {
     if (c == kCfgBig) hipLaunchKernelGGL((wmvc_step_kernel<N, WM, 512>), dim3(grid), dim3(512), 0, s, p);
@@ -274,13 +279,13 @@ int rg_create(rg_ctx** out, const rg_config* cfg) {
   };
   hipError_t e;
   if ((e = hipSetDevice(cfg->device)) != hipSuccess) return bail(e, "hipSetDevice");
-  if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess)
+  if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamDefault)) != hipSuccess)
     return bail(e, "hipStreamCreate");
   if ((e = hipMalloc(&ctx->rec, 2 * sizeof(Record))) != hipSuccess) return bail(e, "hipMalloc(rec)");
   if ((e = hipMalloc(&ctx->state, sizeof(DevState))) != hipSuccess) return bail(e, "hipMalloc(state)");
   if ((e = hipMalloc(&ctx->result, sizeof(DevResult))) != hipSuccess) return bail(e, "hipMalloc(result)");
   Record recs[2] = {fresh_record(), fresh_record()};
-  DevState st{0, 0, 1, 0};  // PhaseIds start at 1 (state.rs:59-63)
+  DevState st{0, 0, 1, 0, 0};  // PhaseIds start at 1 (state.rs:59-63)
   DevResult res;
   std::memset(&res, 0, sizeof res);
   if ((e = hipMemcpy(ctx->rec, recs, sizeof recs, hipMemcpyHostToDevice)) != hipSuccess) return bail(e, "init rec");
@@ -312,6 +317,7 @@ int rg_destroy(rg_ctx* ctx) {
   (void)hipFree(ctx->cluster_coins);
   (void)hipFree(ctx->cluster_part);
   (void)hipFree(ctx->cluster_stats);
+  (void)hipFree(ctx->fix_acc);
   (void)hipFree(ctx->d_votes);
   (void)hipFree(ctx->d_out);
   (void)hipFree(ctx->d_user_result);
@@ -330,7 +336,7 @@ int rg_set_state(rg_ctx* ctx, const rg_engine_state* st) {
   if (!ctx || !st) return fail(ctx, RG_EINVAL, "rg_set_state: null argument");
   RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
   RG_HIP(ctx, hipDeviceSynchronize());
-  DevState s{st->rng_next, st->last_committed, st->commit_watermark, st->steps};
+  DevState s{st->rng_next, st->last_committed, st->commit_watermark, st->steps, 0};
   RG_HIP(ctx, hipMemcpy(ctx->state, &s, sizeof s, hipMemcpyHostToDevice));
   return RG_OK;
 }
@@ -348,10 +354,13 @@ int rg_get_state(rg_ctx* ctx, rg_engine_state* st) {
   return RG_OK;
 }
 
-int rg_phase_step_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, uint64_t n_slots,
-                        uint64_t stride_words, uint64_t slot_base, uint64_t phase, uint64_t max_phase,
-                        rg_step_result* result_dev, void* stream) {
+static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, uint64_t n_slots, uint64_t stride_words,
+              uint64_t slot_base, uint64_t phase, uint64_t max_phase, rg_step_result* result_dev, void* stream,
+              bool shard, uint64_t* records_dev, uint64_t records_cap) {
   if (!ctx) return fail(nullptr, RG_EINVAL, "rg_phase_step: null context");
+  if (shard && ctx->cfg.mode != RG_MODE_REF)
+    return fail(ctx, RG_EINVAL, "rg_phase_step_shard: REF mode only (WMVC coins are shard-invariant already)");
+  if (shard && !records_dev) return fail(ctx, RG_EINVAL, "rg_phase_step_shard: null records buffer");
   if (n_slots == 0) return fail(ctx, RG_EINVAL, "rg_phase_step: n_slots must be > 0");
   if (n_slots >= (1ull << 32)) return fail(ctx, RG_EINVAL, "rg_phase_step: n_slots must be < 2^32 per call");
   if (!votes_dev || !out_dev) return fail(ctx, RG_EINVAL, "rg_phase_step: null plane pointer");
@@ -370,7 +379,7 @@ int rg_phase_step_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_de
   if (int rc = make_layout(ctx, 4 * n + 1, n_words, stride_words, &lin, &need_in, "rg_phase_step")) return rc;
   if (int rc = make_layout(ctx, kOutPlanes, n_words, stride_words, &lout, &need_out, "rg_phase_step")) return rc;
   uint32_t force = (ctx->diag >> 8) & 7u;  // diagnostics: force a tile shape
-  if (force > 3 && (n != 5 || wmvc)) force = 0;
+  if (force > 3 && (n != 5 || wmvc || shard)) force = 0;
   const int cfg = force ? (int)force - 1 : pick_cfg(n, n_words);
   const uint64_t tile_words = (uint64_t)cfg_block(cfg) * cfg_words(cfg, n);
   const uint64_t n_tiles = (n_words + tile_words - 1) / tile_words;
@@ -406,6 +415,8 @@ int rg_phase_step_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_de
   p.n_tiles = (uint32_t)n_tiles;
   p.diag = ctx->diag & 0xffu;
   p.dbg = nullptr;
+  p.vq_rec = reinterpret_cast<unsigned long long*>(records_dev);
+  p.vq_cap = records_cap;
   if (ctx->diag & 4u) {
     if (ctx->dbg_cap < n_tiles * 8) {
       RG_HIP(ctx, hipDeviceSynchronize());
@@ -418,7 +429,76 @@ int rg_phase_step_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_de
     p.dbg = ctx->dbg;
   }
   hipStream_t s = pick_stream(ctx, stream);
-  (wmvc ? kWmvcLaunch : kRefLaunch)[n](cfg, (uint32_t)n_tiles, s, p);
+  if (shard) launch_ref_shard(n, cfg_block(cfg), cfg_words(cfg, n), (uint32_t)n_tiles, s, p);
+  else (wmvc ? kWmvcLaunch : kRefLaunch)[n](cfg, (uint32_t)n_tiles, s, p);
+  RG_HIP(ctx, hipGetLastError());
+  return RG_OK;
+}
+
+int rg_phase_step_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, uint64_t n_slots,
+                        uint64_t stride_words, uint64_t slot_base, uint64_t phase, uint64_t max_phase,
+                        rg_step_result* result_dev, void* stream) {
+  return step_impl(ctx, votes_dev, out_dev, n_slots, stride_words, slot_base, phase, max_phase, result_dev, stream,
+                   false, nullptr, 0);
+}
+
+int rg_phase_step_shard_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, uint64_t n_slots,
+                              uint64_t stride_words, uint64_t slot_base, uint64_t max_phase, uint64_t* records_dev,
+                              uint64_t records_cap, rg_step_result* row_dev, void* stream) {
+  return step_impl(ctx, votes_dev, out_dev, n_slots, stride_words, slot_base, 1, max_phase, row_dev, stream, true,
+                   records_dev, records_cap);
+}
+
+int rg_shard_fixup_async(rg_ctx* ctx, uint32_t* out_dev, uint64_t n_slots, uint64_t stride_words,
+                         uint64_t slot_base, uint64_t max_phase, const uint64_t* records_dev,
+                         uint64_t records_cap, const rg_step_result* rows_dev, uint32_t shard,
+                         uint32_t n_shards, rg_step_result* row_dev, void* stream) {
+  if (!ctx) return fail(nullptr, RG_EINVAL, "rg_shard_fixup: null context");
+  if (ctx->cfg.mode != RG_MODE_REF) return fail(ctx, RG_EINVAL, "rg_shard_fixup: REF mode only");
+  if (!out_dev || !records_dev || !rows_dev || n_shards == 0 || shard >= n_shards || n_slots == 0)
+    return fail(ctx, RG_EINVAL, "rg_shard_fixup: bad argument");
+  RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
+  const uint64_t n_words = (n_slots + 31) / 32;
+  Layout lout;
+  uint64_t need;
+  if (int rc = make_layout(ctx, kOutPlanes, n_words, stride_words, &lout, &need, "rg_shard_fixup")) return rc;
+  if (!ctx->fix_acc) RG_HIP(ctx, hipMalloc(&ctx->fix_acc, 4 * sizeof(unsigned long long)));
+  hipStream_t s = pick_stream(ctx, stream);
+  RG_HIP(ctx, hipMemsetAsync(ctx->fix_acc, 0, 3 * sizeof(unsigned long long), s));
+  RG_HIP(ctx, hipMemsetAsync(ctx->fix_acc + 3, 0xFF, sizeof(unsigned long long), s));
+  FixParams f;
+  f.rec = reinterpret_cast<const unsigned long long*>(records_dev);
+  f.rows = reinterpret_cast<const DevResult*>(rows_dev);
+  f.shard = shard;
+  f.n_shards = n_shards;
+  f.state = ctx->state;
+  f.out = out_dev;
+  f.lout = lout;
+  f.slot_base = slot_base;
+  f.max_phase = max_phase;
+  f.vq_cap = records_cap;
+  f.key = ctx->ref_key;
+  f.acc = ctx->fix_acc;
+  // one ChaCha12 block per thread per pass; the record count lives on the device,
+  // so the grid covers the largest possible count (all slots VQ) and strides
+  const uint64_t blocks_max = (records_cap < n_slots ? records_cap : n_slots) / 8 + 2;
+  const uint64_t g = (blocks_max + 255) / 256;
+  const uint32_t grid = (uint32_t)(g < 1024 ? g : 1024);
+  hipLaunchKernelGGL(shard_fixup_kernel, dim3(grid), dim3(256), 0, s, f);
+  hipLaunchKernelGGL(shard_fixup_finish_kernel, dim3(1), dim3(64), 0, s, f, ctx->result,
+                     reinterpret_cast<DevResult*>(row_dev));
+  RG_HIP(ctx, hipGetLastError());
+  return RG_OK;
+}
+
+int rg_shard_commit_async(rg_ctx* ctx, const rg_step_result* rows_dev, uint32_t n_shards, uint64_t window_base,
+                          uint64_t window_slots, rg_step_result* result_dev, void* stream) {
+  if (!ctx) return fail(nullptr, RG_EINVAL, "rg_shard_commit: null context");
+  if (!rows_dev || n_shards == 0 || window_slots == 0) return fail(ctx, RG_EINVAL, "rg_shard_commit: bad argument");
+  RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
+  hipLaunchKernelGGL(shard_commit_kernel, dim3(1), dim3(64), 0, pick_stream(ctx, stream),
+                     reinterpret_cast<const DevResult*>(rows_dev), n_shards, window_base, window_slots, ctx->state,
+                     ctx->result, reinterpret_cast<DevResult*>(result_dev));
   RG_HIP(ctx, hipGetLastError());
   return RG_OK;
 }

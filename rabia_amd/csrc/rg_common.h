@@ -102,7 +102,6 @@ struct alignas(128) Line {
 // One per launch parity (seq & 1). The last tile of launch e resets record
 // (e+1)&1 for the next launch, so no host memset sits between steps.
 struct Record {
-  Line ticket;     // dynamic tile ticket (decoupled look-back needs dispatch order)
   Line error;      // device protocol fault bits
 };
 
@@ -111,7 +110,18 @@ struct DevState {
   unsigned long long last_committed;
   unsigned long long commit_watermark;
   unsigned long long steps;
+  // Sharded REF (rg_phase_step_shard_async): provisional stream position of this
+  // shard's draws, advanced by the shard's own VQ count only. Never read by the
+  // single-evaluator path; the fix-up re-draws at the global position.
+  unsigned long long shard_draws;
 };
+
+// Sharded REF draw record, one per VQ slot of a shard step, indexed by the slot's
+// local draw number: slot offset (low 32 bits) | info << 32 with
+//   info bits 0-1 (c1 vs c0 over R1: 0 tie, 1 c1 > c0, 2 c1 < c0),
+//   bits 2-3 decision code if the own round-2 vote is V0, bits 4-5 if it is V1,
+//   bit 6 the own vote the provisional draw gave.
+constexpr uint32_t kRecGt = 1u, kRecLt = 2u;
 
 struct DevResult {  // layout-identical to rg_step_result
   unsigned long long n_slots, n_decided, n_v1, n_pending_r1, n_draws;

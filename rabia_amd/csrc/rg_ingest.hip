@@ -280,7 +280,7 @@ int rg_ingest_create(rg_ingest** out, const rg_ingest_config* cfg) {
   std::memcpy(g->mem.id, cfg->members, sizeof(g->mem.id));
   g->mem.n = cfg->n_replicas;
   if (hipSetDevice(cfg->device) != hipSuccess ||
-      hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess) {
+      hipStreamCreateWithFlags(&g->stream, hipStreamDefault) != hipSuccess) {
     delete g;
     return ifail(nullptr, -2, "rg_ingest_create: stream creation failed");
   }

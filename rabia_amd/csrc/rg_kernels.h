@@ -51,7 +51,12 @@ struct StepParams {
   uint32_t diag;                  // diagnostic build switches (0 in production):
                                   //  1 skip the look-back wait, 2 skip finish_tile, 4 stamps
   unsigned long long* dbg;        // [n_tiles][8] s_memrealtime stamps when diag & 4
+  unsigned long long* vq_rec;     // sharded REF: draw records [vq_cap] (rg_common.h)
+  uint64_t vq_cap;
 };
+
+// finish_tile flavours
+constexpr int kFinRef = 0, kFinWmvc = 1, kFinShard = 2;
 
 __device__ __forceinline__ void stamp(const StepParams& p, uint32_t tile, int k, int tid) {
   if ((p.diag & 4u) && tid == 0) p.dbg[(uint64_t)tile * 8 + k] = __builtin_amdgcn_s_memrealtime();
@@ -376,7 +381,7 @@ __device__ __forceinline__ void block_reduce_totals(unsigned long long (&v)[7], 
 
 // Publish this tile's statistics; the tile with the last index folds every
 // tile's granules, advances the device engine state and writes the step result.
-template <bool IS_REF, int BLOCK, int W>
+template <int FIN, int BLOCK, int W>
 __device__ __forceinline__ void finish_tile(const StepParams& p, Record* rec, TileStats ts,
                                             uint32_t tile, int tid, int lane, int wave) {
   constexpr uint64_t kTileSlots = (uint64_t)BLOCK * W * 32;
@@ -444,15 +449,31 @@ __device__ __forceinline__ void finish_tile(const StepParams& p, Record* rec, Ti
   r.n_v1 = v[1];
   r.n_pending_r1 = v[2];
   r.n_draws = v[3];
-  unsigned long long lc = s.last_committed;          // commit_phase: monotonic max,
-  if (v[4] && v[4] - 1 > lc) lc = v[4] - 1;          // state.rs:77-99
   const unsigned long long end = p.slot_base + p.n_slots;
   const unsigned long long fu = v[5] < end ? v[5] : end;
+  if constexpr (FIN == kFinShard) {
+    // Shard row before the fix-up: VQ slots are not in the counts / extremes
+    // (their decisions wait for the global draw positions); draws advance only
+    // the provisional counter. The global engine state is left to the fix-up and
+    // rg_shard_commit (state.rs:65-103 over the whole window).
+    r.last_committed_max = v[4] ? v[4] - 1 : 0;
+    r.first_undecided = fu;
+    r.rng_next = s.shard_draws + r.n_draws;
+    r.commit_watermark = 0;
+    r.flags = err;
+    s.shard_draws = r.rng_next;
+    *p.state = s;
+    *p.result = r;
+    if (p.result_user) *p.result_user = r;
+    return;
+  }
+  unsigned long long lc = s.last_committed;          // commit_phase: monotonic max,
+  if (v[4] && v[4] - 1 > lc) lc = v[4] - 1;          // state.rs:77-99
   unsigned long long wm = s.commit_watermark;
   if (p.slot_base <= wm && wm < fu) wm = fu;
   r.last_committed_max = lc;
   r.first_undecided = fu;
-  r.rng_next = IS_REF ? s.rng_next + r.n_draws : s.rng_next;
+  r.rng_next = FIN == kFinRef ? s.rng_next + r.n_draws : s.rng_next;
   r.commit_watermark = wm;
   r.flags = err;
   s.rng_next = r.rng_next;
@@ -476,7 +497,6 @@ __device__ __forceinline__ bool tile_prologue(const StepParams& p, Record* rec, 
   }
   if (tid == 0 && tile == p.n_tiles - 1) {
     Record* nxt = p.rec + ((p.seq + 1) & 1u);
-    atomic_store_agent(&nxt->ticket.v, 0ull);
     atomic_store_agent(&nxt->error.v, 0ull);
   }
   return true;
@@ -514,7 +534,34 @@ __device__ __forceinline__ TileStats thread_stats(const uint32_t (&committed)[W]
 // Occupancy: 4 waves per SIMD (<= 128 VGPRs) so that at least two 512-thread or
 // four 256-thread tiles are resident per CU and one tile's look-back / stores
 // overlap another's loads.
-template <int N, int W, int BLOCK>
+// Decision code masks (lo, hi) of count_votes over the round-2 lanes of word i
+// (messages.rs:185-211; 3 = None): V0 0/0, V1 1/0, VQ 0/1, None 1/1.
+template <int N, int W>
+__device__ __forceinline__ void r2_decision(const uint32_t (&lo)[N][W], const uint32_t (&hi)[N][W], int i,
+                                            uint32_t q, uint32_t& dlo, uint32_t& dhi) {
+  constexpr int B = ctr_bits(N);
+  Ctr<B> c0, c1, cq;
+  ctr_zero(c0); ctr_zero(c1); ctr_zero(cq);
+#pragma unroll
+  for (int j = 0; j < N; j++) {
+    const uint32_t l = lo[j][i], h = hi[j][i];
+    ctr_add(c0, ~l & ~h);
+    ctr_add(c1, l & ~h);
+    ctr_add(cq, ~l & h);
+  }
+  const uint32_t d0 = ctr_ge(c0, q);
+  const uint32_t d1 = ~d0 & ctr_ge(c1, q);
+  const uint32_t dq = ~d0 & ~d1 & ctr_ge(cq, q);
+  const uint32_t dn = ~(d0 | d1 | dq);
+  dlo = d1 | dn;
+  dhi = dq | dn;
+}
+
+// SHARD = the sharded-REF flavour (rg_phase_step_shard_async): the draws come from
+// the shard's provisional stream position, every VQ slot also leaves a draw
+// record (its decision under both own votes) for rg_shard_fixup_async, and the
+// tile statistics leave the VQ slots out.
+template <int N, int W, int BLOCK, bool SHARD>
 __global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
   constexpr int B = ctr_bits(N);
   constexpr int WAVES = BLOCK / 64;
@@ -600,8 +647,10 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
   // ---- own round-2 vote (engine.rs:523-537; VQ -> one StdRng draw, 567-611).
   // The tile's draws are ONE contiguous index range [k_tile, k_tile + tile_total):
   // its ChaCha12 blocks are computed once, one per thread, and staged in LDS.
-  const unsigned long long k_tile = p.state->rng_next + s_excl;
-  unsigned long long k = k_tile + wave_off + incl - vq_count;
+  const unsigned long long k_base = SHARD ? p.state->shard_draws : p.state->rng_next;
+  const unsigned long long k_tile = k_base + s_excl;
+  const unsigned long long k_first = k_tile + wave_off + incl - vq_count;  // this thread's first draw
+  unsigned long long k = k_first;
   uint32_t own_lo[W], mq[W];
 #pragma unroll
   for (int i = 0; i < W; i++) {
@@ -639,6 +688,23 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
   }
 
   // ---- own vote joins round2_votes (engine.rs:540-542); decision (613-628)
+  uint32_t dlo[W], dhi[W], alo[W], ahi[W];
+  if constexpr (SHARD) {
+    // the decision under the other own vote, for the VQ slots' draw records
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      if (j == p.self_lane) {
+#pragma unroll
+        for (int i = 0; i < W; i++) {
+          const uint32_t l = r2lo[j][i], h = r2hi[j][i];
+          r2lo[j][i] = (l & pend[i]) | ((own_lo[i] ^ r1vq[i]) & ~pend[i]);
+          r2hi[j][i] = h & pend[i];
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < W; i++) r2_decision<N, W>(r2lo, r2hi, i, p.q, alo[i], ahi[i]);
+  }
 #pragma unroll
   for (int j = 0; j < N; j++) {
     if (j == p.self_lane) {
@@ -649,41 +715,227 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
       }
     }
   }
+#pragma unroll
+  for (int i = 0; i < W; i++) r2_decision<N, W>(r2lo, r2hi, i, p.q, dlo[i], dhi[i]);
   uint32_t o[kOutPlanes][W];
 #pragma unroll
   for (int i = 0; i < W; i++) {
-    Ctr<B> c0, c1, cq;
-    ctr_zero(c0); ctr_zero(c1); ctr_zero(cq);
-#pragma unroll
-    for (int j = 0; j < N; j++) {
-      const uint32_t lo = r2lo[j][i], hi = r2hi[j][i];
-      ctr_add(c0, ~lo & ~hi);
-      ctr_add(c1, lo & ~hi);
-      ctr_add(cq, ~lo & hi);
-    }
-    const uint32_t d0 = ctr_ge(c0, p.q);
-    const uint32_t d1 = ~d0 & ctr_ge(c1, p.q);
-    const uint32_t dq = ~d0 & ~d1 & ctr_ge(cq, p.q);
-    const uint32_t dn = ~(d0 | d1 | dq);
+    const uint32_t d1 = dlo[i] & ~dhi[i];
+    const uint32_t dc = ~dhi[i];  // V0 or V1
     o[0][i] = (r1v1[i] | pend[i]) & vm[i];
     o[1][i] = (r1vq[i] | pend[i]) & vm[i];
     o[2][i] = (own_lo[i] | pend[i]) & vm[i];
     o[3][i] = pend[i];
-    o[4][i] = (d1 | dn) & vm[i];
-    o[5][i] = (dq | dn) & vm[i];
-    o[6][i] = (d0 | d1) & vm[i];   // set_decision: committed iff not VQuestion
-    o[7][i] = d1 & vm[i];          // V1: apply_batch + commit_phase
+    o[4][i] = dlo[i] & vm[i];
+    o[5][i] = dhi[i] & vm[i];
+    o[6][i] = dc & vm[i];   // set_decision: committed iff not VQuestion
+    o[7][i] = d1 & vm[i];   // V1: apply_batch + commit_phase
   }
   if (active) {
     uint32_t* ob = p.out + p.lout.base(w0);
 #pragma unroll
     for (int pl = 0; pl < kOutPlanes; pl++) store_words_nt<W>(ob + pl * p.lout.pstride, o[pl]);
   }
+  if constexpr (SHARD) {
+    // draw records, indexed by local draw number (ascending slot order)
+    unsigned long long kr = k_first - k_base;
+#pragma unroll
+    for (int i = 0; i < W; i++) {
+      uint32_t m = r1vq[i];
+      while (m) {
+        const int b = __builtin_ctz(m);
+        m &= m - 1;
+        const uint32_t own = (own_lo[i] >> b) & 1u;
+        const uint32_t dp = ((dlo[i] >> b) & 1u) | (((dhi[i] >> b) & 1u) << 1);
+        const uint32_t da = ((alo[i] >> b) & 1u) | (((ahi[i] >> b) & 1u) << 1);
+        const uint32_t d_v0 = own ? da : dp, d_v1 = own ? dp : da;
+        const uint32_t cls = ((c1gt[i] >> b) & 1u) ? kRecGt : (((c1lt[i] >> b) & 1u) ? kRecLt : 0u);
+        const uint32_t info = cls | (d_v0 << 2) | (d_v1 << 4) | (own << 6);
+        const uint32_t off = (uint32_t)(32u * (w0 + i) + b);
+        if (kr < p.vq_cap) p.vq_rec[kr] = ((unsigned long long)info << 32) | off;
+        kr++;
+      }
+    }
+  }
   stamp(p, tile, 3, tid);
   if (p.diag & 2u) return;
-  const TileStats ts = thread_stats<W>(o[6], o[7], pend, vm, vq_count, w0, tw0, p);
-  finish_tile<true, BLOCK, W>(p, rec, ts, tile, tid, lane, wave);
+  uint32_t st_dec[W], st_v1[W], st_vm[W];
+#pragma unroll
+  for (int i = 0; i < W; i++) {  // SHARD: VQ slots are counted by the fix-up
+    const uint32_t keep = SHARD ? ~r1vq[i] : ~0u;
+    st_dec[i] = o[6][i] & keep;
+    st_v1[i] = o[7][i] & keep;
+    st_vm[i] = vm[i] & keep;
+  }
+  const TileStats ts = thread_stats<W>(st_dec, st_v1, pend, st_vm, vq_count, w0, tw0, p);
+  finish_tile<SHARD ? kFinShard : kFinRef, BLOCK, W>(p, rec, ts, tile, tid, lane, wave);
   stamp(p, tile, 4, tid);
+}
+
+// ============================================================================
+// Sharded REF: one engine (one StdRng stream) over a window split into
+// contiguous shards, one per GPU. Draw k of shard r sits at global
+// stream position  rng_next(window start) + VQ slots of shards 0..r-1 + k
+// (ascending slot order over the whole window, engine.rs:567-611). The step ran
+// with a provisional position; the fix-up re-draws every VQ slot of the shard at
+// its global position from its draw record, XOR-patches the output bits that
+// change (own round-2 vote; decision, committed, V1 planes) and counts the VQ
+// slots into the shard's statistics. One thread per ChaCha12 block (8 draws),
+// grid-stride; one atomic per changed (plane, word) run of a thread.
+// ============================================================================
+struct FixParams {
+  const unsigned long long* rec;  // [vq_cap] draw records of this shard's step
+  const DevResult* rows;          // [n_shards] step rows of every shard, rank order
+  uint32_t shard, n_shards;
+  DevState* state;
+  uint32_t* out;
+  Layout lout;
+  uint64_t slot_base, max_phase, vq_cap;
+  Key key;
+  unsigned long long* acc;        // [4] decided, V1, max V1 id + 1, min undecided id
+};
+
+__device__ __forceinline__ void fix_flush(const FixParams& f, uint64_t w, const uint32_t (&x)[5]) {
+  constexpr int kPl[5] = {2, 4, 5, 6, 7};
+  const uint64_t base = f.lout.base(w);
+#pragma unroll
+  for (int i = 0; i < 5; i++)
+    if (x[i]) atomicXor(f.out + base + (uint64_t)kPl[i] * f.lout.pstride, x[i]);
+}
+
+static __global__ __launch_bounds__(256) void shard_fixup_kernel(FixParams f) {
+  const unsigned long long n = f.rows[f.shard].n_draws;
+  unsigned long long pre = 0;
+  for (uint32_t r = 0; r < f.shard; r++) pre += f.rows[r].n_draws;
+  const unsigned long long g0 = f.state->rng_next + pre;  // global position of local draw 0
+  const unsigned long long nn = n < f.vq_cap ? n : f.vq_cap;
+  const unsigned long long b_first = g0 >> 3, b_end = nn ? ((g0 + nn - 1) >> 3) + 1 : b_first;
+  unsigned long long dec = 0, v1 = 0, mx = 0, mn = ~0ull;
+  for (unsigned long long b = b_first + (unsigned long long)blockIdx.x * 256 + threadIdx.x; b < b_end;
+       b += (unsigned long long)gridDim.x * 256) {
+    uint32_t x[16];
+    chacha_block<12>(f.key, b, 0, x);
+    const unsigned long long lo = (b << 3) > g0 ? (b << 3) - g0 : 0;
+    const unsigned long long hi = ((b + 1) << 3) - g0 < nn ? ((b + 1) << 3) - g0 : nn;
+    uint64_t cur = ~0ull;
+    uint32_t xm[5] = {0, 0, 0, 0, 0};
+    for (unsigned long long k = lo; k < hi; k++) {
+      const unsigned long long r = f.rec[k];
+      const uint32_t off = (uint32_t)r, info = (uint32_t)(r >> 32);
+      const uint32_t ws = (uint32_t)((g0 + k) & 7u) * 2u;
+      const unsigned long long u =
+          (unsigned long long)select16(x, ws) | ((unsigned long long)select16(x, ws + 1) << 32);
+      const uint32_t cls = info & 3u;
+      const uint32_t own = cls == kRecGt ? (u < kP90) : (cls == kRecLt ? (u >= kP90) : (u < kP80));
+      const uint32_t prov = (info >> 6) & 1u;
+      const uint32_t d = own ? (info >> 4) & 3u : (info >> 2) & 3u;
+      const uint32_t dp = prov ? (info >> 4) & 3u : (info >> 2) & 3u;
+      const unsigned long long id = f.slot_base + off;
+      if (d <= kCodeV1) {
+        dec++;
+        if (d == kCodeV1) {
+          v1++;
+          if ((f.max_phase == 0 || id <= f.max_phase) && id + 1 > mx) mx = id + 1;
+        }
+      } else if (id < mn) {
+        mn = id;
+      }
+      if (own != prov) {
+        const uint64_t w = off >> 5;
+        if (w != cur) {
+          if (cur != ~0ull) fix_flush(f, cur, xm);
+          cur = w;
+          xm[0] = xm[1] = xm[2] = xm[3] = xm[4] = 0;
+        }
+        const uint32_t bit = 1u << (off & 31u), dd = d ^ dp;
+        xm[0] ^= bit;
+        xm[1] ^= (dd & 1u) ? bit : 0u;
+        xm[2] ^= (dd & 2u) ? bit : 0u;
+        xm[3] ^= ((d <= kCodeV1) != (dp <= kCodeV1)) ? bit : 0u;
+        xm[4] ^= ((d == kCodeV1) != (dp == kCodeV1)) ? bit : 0u;
+      }
+    }
+    if (cur != ~0ull) fix_flush(f, cur, xm);
+  }
+  __shared__ unsigned long long red[4][4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  dec = wave_sum64(dec);
+  v1 = wave_sum64(v1);
+  mx = wave_max64(mx);
+  mn = wave_min64(mn);
+  if (lane == 0) { red[wave][0] = dec; red[wave][1] = v1; red[wave][2] = mx; red[wave][3] = mn; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; w++) {
+      dec += red[w][0]; v1 += red[w][1];
+      mx = red[w][2] > mx ? red[w][2] : mx;
+      mn = red[w][3] < mn ? red[w][3] : mn;
+    }
+    if (dec) atomicAdd(f.acc + 0, dec);
+    if (v1) atomicAdd(f.acc + 1, v1);
+    if (mx) atomicMax(f.acc + 2, mx);
+    if (mn != ~0ull) atomicMin(f.acc + 3, mn);
+  }
+}
+
+// The shard's final row: VQ-slot counts and extremes folded in, the engine's
+// stream position advanced past the whole window's draws (every shard's).
+static __global__ void shard_fixup_finish_kernel(FixParams f, DevResult* row_ctx, DevResult* row_user) {
+  if (threadIdx.x != 0) return;
+  DevResult r = f.rows[f.shard];
+  unsigned long long total = 0;
+  for (uint32_t s = 0; s < f.n_shards; s++) total += f.rows[s].n_draws;
+  r.n_decided += f.acc[0];
+  r.n_v1 += f.acc[1];
+  if (f.acc[2] && f.acc[2] - 1 > r.last_committed_max) r.last_committed_max = f.acc[2] - 1;
+  if (f.acc[3] < r.first_undecided) r.first_undecided = f.acc[3];
+  if (r.n_draws > f.vq_cap) r.flags |= 8ull;  // records did not fit: the patch is incomplete
+  DevState s = *f.state;
+  s.rng_next += total;
+  r.rng_next = s.rng_next;
+  r.commit_watermark = 0;
+  *f.state = s;
+  *row_ctx = r;
+  if (row_user) *row_user = r;
+}
+
+// Fold the shards' final rows of one window into the engine state exactly as one
+// evaluator over the whole window: commit_phase max (state.rs:77-99), first
+// undecided = min over shards, contiguous watermark advance.
+static __global__ void shard_commit_kernel(const DevResult* rows, uint32_t n_shards, uint64_t window_base,
+                                    uint64_t window_slots, DevState* state, DevResult* res_ctx,
+                                    DevResult* res_user) {
+  if (threadIdx.x != 0) return;
+  DevState s = *state;
+  DevResult g;
+  g.n_slots = g.n_decided = g.n_v1 = g.n_pending_r1 = g.n_draws = g.flags = 0;
+  unsigned long long lc = s.last_committed;
+  const unsigned long long end = window_base + window_slots;
+  unsigned long long fu = end;
+  for (uint32_t r = 0; r < n_shards; r++) {
+    const DevResult& x = rows[r];
+    g.n_slots += x.n_slots;
+    g.n_decided += x.n_decided;
+    g.n_v1 += x.n_v1;
+    g.n_pending_r1 += x.n_pending_r1;
+    g.n_draws += x.n_draws;
+    g.flags |= x.flags;
+    if (x.last_committed_max > lc) lc = x.last_committed_max;
+    if (x.n_slots && x.first_undecided < fu) fu = x.first_undecided;
+  }
+  if (g.n_slots != window_slots) g.flags |= 16ull;  // the rows do not tile the window
+  unsigned long long wm = s.commit_watermark;
+  if (window_base <= wm && wm < fu) wm = fu;
+  g.last_committed_max = lc;
+  g.first_undecided = fu;
+  g.rng_next = s.rng_next;
+  g.commit_watermark = wm;
+  s.last_committed = lc;
+  s.commit_watermark = wm;
+  s.steps += 1;
+  *state = s;
+  *res_ctx = g;
+  if (res_user) *res_user = g;
 }
 
 // ============================================================================
@@ -713,7 +965,7 @@ __global__ __launch_bounds__(BLOCK, 4) void wmvc_step_kernel(StepParams p) {
   constexpr int B = ctr_bits(N);
   Record* rec = p.rec + (p.seq & 1u);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t tile = blockIdx.x;  // no cross-tile dependency: no ticket needed
+  const uint32_t tile = blockIdx.x;  // no cross-tile dependency
   if (!tile_prologue(p, rec, tile, tid)) return;
   const uint32_t tw0 = (uint32_t)tid * W;
   const uint64_t w0 = (uint64_t)tile * BLOCK * W + tw0;
@@ -843,7 +1095,7 @@ __global__ __launch_bounds__(BLOCK, 4) void wmvc_step_kernel(StepParams p) {
   }
   if (p.diag & 2u) return;
   const TileStats ts = thread_stats<W>(o[6], dv1, pend_w, vm_all, n_coin, w0, tw0, p);
-  finish_tile<false, BLOCK, W>(p, rec, ts, tile, tid, lane, wave);
+  finish_tile<kFinWmvc, BLOCK, W>(p, rec, ts, tile, tid, lane, wave);
 }
 
 // ============================================================================
@@ -927,7 +1179,7 @@ __global__ __launch_bounds__(kBlock) void digest_kernel(const uint64_t* __restri
   }
 }
 
-__global__ void coin_kernel(Key key, uint64_t stream, uint64_t phase, uint64_t slot_base,
+static __global__ void coin_kernel(Key key, uint64_t stream, uint64_t phase, uint64_t slot_base,
                             uint64_t n_slots, uint32_t* out) {
   const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t n_words = (n_slots + 31) / 32;
@@ -939,7 +1191,7 @@ __global__ void coin_kernel(Key key, uint64_t stream, uint64_t phase, uint64_t s
 
 // Decision bitmaps of a step's output (planes 6 committed, 7 V1/apply) as two
 // contiguous bit arrays: what the multi-GPU exchange all-gathers.
-__global__ void bitmap_kernel(const uint32_t* out, Layout lout, uint64_t n_words, uint32_t* committed,
+static __global__ void bitmap_kernel(const uint32_t* out, Layout lout, uint64_t n_words, uint32_t* committed,
                               uint32_t* v1) {
   const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= n_words) return;
@@ -980,7 +1232,7 @@ __device__ __forceinline__ uint32_t proposed_code(const R1vArgs& a, uint64_t off
 }
 
 // 1: the first message of each slot without a proposed value claims the slot
-__global__ void r1v_claim_kernel(R1vArgs a) {
+static __global__ void r1v_claim_kernel(R1vArgs a) {
   const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= a.n || !a.track) return;
   const uint64_t ph = a.phase_ids[m];
@@ -999,7 +1251,7 @@ __device__ __forceinline__ bool r1v_draws(const R1vArgs& a, uint64_t m, bool* fi
 }
 
 // 2: draws per block
-__global__ __launch_bounds__(kR1vBlock) void r1v_count_kernel(R1vArgs a) {
+static __global__ __launch_bounds__(kR1vBlock) void r1v_count_kernel(R1vArgs a) {
   const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool first = false, d = false;
   uint64_t off = 0;
@@ -1010,7 +1262,7 @@ __global__ __launch_bounds__(kR1vBlock) void r1v_count_kernel(R1vArgs a) {
 
 // 3: one workgroup: exclusive offsets of the block counts; the batch's draws are
 // taken from the engine stream here (rng_next advances by the total)
-__global__ __launch_bounds__(1024) void r1v_scan_kernel(R1vArgs a, uint32_t blocks) {
+static __global__ __launch_bounds__(1024) void r1v_scan_kernel(R1vArgs a, uint32_t blocks) {
   __shared__ unsigned long long s_sum[1024];
   const uint32_t t = threadIdx.x;
   const uint32_t per = (blocks + 1023) / 1024, lo = t * per, hi = lo + per < blocks ? lo + per : blocks;
@@ -1038,7 +1290,7 @@ __global__ __launch_bounds__(1024) void r1v_scan_kernel(R1vArgs a, uint32_t bloc
 }
 
 // 4: votes, proposed values, cell reset
-__global__ __launch_bounds__(kR1vBlock) void r1v_vote_kernel(R1vArgs a) {
+static __global__ __launch_bounds__(kR1vBlock) void r1v_vote_kernel(R1vArgs a) {
   __shared__ uint32_t s_w[kR1vBlock / 64];
   const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1088,7 +1340,7 @@ __global__ __launch_bounds__(kR1vBlock) void r1v_vote_kernel(R1vArgs a) {
 }
 
 // 5: re-arm the claim cells touched by this batch
-__global__ void r1v_reset_kernel(R1vArgs a) {
+static __global__ void r1v_reset_kernel(R1vArgs a) {
   const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= a.n || !a.track) return;
   const uint64_t ph = a.phase_ids[m];
@@ -1096,7 +1348,7 @@ __global__ void r1v_reset_kernel(R1vArgs a) {
   a.cells[ph - a.slot_base] = 0xFFFFFFFFu;
 }
 
-__global__ void draws_kernel(Key key, uint64_t first, uint64_t count, unsigned long long* out) {
+static __global__ void draws_kernel(Key key, uint64_t first, uint64_t count, unsigned long long* out) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= count) return;
   const uint64_t k = first + t;
@@ -1107,7 +1359,7 @@ __global__ void draws_kernel(Key key, uint64_t first, uint64_t count, unsigned l
 }
 
 // Synthetic traces, one thread per 32-slot word (restated in oracle/rabia_oracle.c:or_trace).
-__global__ void trace_kernel(int kind, int n, uint64_t seed, uint64_t slot_base, uint64_t n_slots,
+static __global__ void trace_kernel(int kind, int n, uint64_t seed, uint64_t slot_base, uint64_t n_slots,
                              Layout lay, uint32_t* planes) {
   const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t n_words = (n_slots + 31) / 32;
@@ -1167,7 +1419,7 @@ __global__ void trace_kernel(int kind, int n, uint64_t seed, uint64_t slot_base,
   planes[lay.base(w) + (uint64_t)(4 * n) * lay.pstride] = stw;
 }
 
-__global__ void digest_trace_kernel(int n, uint64_t seed, uint64_t slot_base, uint64_t n_slots,
+static __global__ void digest_trace_kernel(int n, uint64_t seed, uint64_t slot_base, uint64_t n_slots,
                                     uint64_t dstride, unsigned long long* dg) {
   const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n_slots) return;
@@ -1301,7 +1553,7 @@ __global__ __launch_bounds__(256) void wmvc_cluster_kernel(const uint32_t* state
 // Common-coin table for the cluster kernel: coin bits of phases 1..P for the
 // window's slots, [P][n_words]; one thread per 512-slot group (16 words) computes
 // the one or two ChaCha12 blocks that cover it (the same bits as coin_kernel).
-__global__ void coin_table_kernel(Key key, uint64_t stream, uint64_t slot_base, uint64_t n_slots,
+static __global__ void coin_table_kernel(Key key, uint64_t stream, uint64_t slot_base, uint64_t n_slots,
                                   uint32_t phases, uint32_t* tab) {
   const uint64_t n_words = (n_slots + 31) / 32, n_groups = (n_words + 15) / 16;
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1451,7 +1703,7 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
   }
 }
 
-__global__ void cluster_stats_kernel(const unsigned long long* partials, uint32_t nblocks, unsigned long long* out) {
+static __global__ void cluster_stats_kernel(const unsigned long long* partials, uint32_t nblocks, unsigned long long* out) {
   const int k = threadIdx.x;
   if (k >= kClusterStats) return;
   unsigned long long v = 0;
@@ -1463,7 +1715,7 @@ __global__ void cluster_stats_kernel(const unsigned long long* partials, uint32_
 }
 
 // Initial states of the adversarial cluster trace (restated in or_cluster_trace).
-__global__ void cluster_trace_kernel(int n, uint64_t seed, uint64_t slot_base, uint64_t n_slots, uint64_t stride,
+static __global__ void cluster_trace_kernel(int n, uint64_t seed, uint64_t slot_base, uint64_t n_slots, uint64_t stride,
                                      uint32_t* states) {
   const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t n_words = (n_slots + 31) / 32;

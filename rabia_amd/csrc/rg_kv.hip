@@ -683,7 +683,7 @@ int rg_kv_create(rg_kv** out, const rg_kv_config* cfg) {
     if (e != hipSuccess && !rc) rc = kfail(nullptr, e == hipErrorOutOfMemory ? -3 : -2, std::string(w) + ": " + hipGetErrorString(e));
   };
   chk(hipSetDevice(c.device), "hipSetDevice");
-  chk(hipStreamCreateWithFlags(&kv->stream, hipStreamNonBlocking), "hipStreamCreate");
+  chk(hipStreamCreateWithFlags(&kv->stream, hipStreamDefault), "hipStreamCreate");
   chk(hipMalloc(&kv->hashes, c.table_slots * 8), "hipMalloc(table)");
   chk(hipMalloc(&kv->ent, c.table_slots * sizeof(KvEntry)), "hipMalloc(entries)");
   chk(hipMalloc(&kv->heap, c.heap_bytes ? c.heap_bytes : 1), "hipMalloc(heap)");

@@ -253,6 +253,26 @@ class PhaseEvaluator:
                                              phase, max_phase, result_ptr or None, stream or None),
                 self.ctx)
 
+    # -- sharded REF: one engine over a window split across GPUs (shard.py) -----
+    def phase_step_shard_async(self, votes_ptr, out_ptr, n_slots, stride, slot_base, records_ptr, records_cap,
+                               row_ptr=0, max_phase=0, stream=0):
+        """Stage 1: this shard's slots at a provisional stream position + draw records."""
+        N.check(self.lib.rg_phase_step_shard_async(self.ctx, votes_ptr, out_ptr, n_slots, stride, slot_base,
+                                                   max_phase, records_ptr, records_cap, row_ptr or None,
+                                                   stream or None), self.ctx)
+
+    def shard_fixup_async(self, out_ptr, n_slots, stride, slot_base, records_ptr, records_cap, rows_ptr, shard,
+                          n_shards, row_ptr=0, max_phase=0, stream=0):
+        """Stage 3: re-draw this shard's VQ slots at their global stream positions."""
+        N.check(self.lib.rg_shard_fixup_async(self.ctx, out_ptr, n_slots, stride, slot_base, max_phase, records_ptr,
+                                              records_cap, rows_ptr, shard, n_shards, row_ptr or None,
+                                              stream or None), self.ctx)
+
+    def shard_commit_async(self, rows_ptr, n_shards, window_base, window_slots, result_ptr=0, stream=0):
+        """Stage 4: fold every shard's final row into this context's engine state."""
+        N.check(self.lib.rg_shard_commit_async(self.ctx, rows_ptr, n_shards, window_base, window_slots,
+                                               result_ptr or None, stream or None), self.ctx)
+
     def digest_majority_async(self, digests_ptr, digest_stride, state_ptr, n_slots, stream=0):
         N.check(self.lib.rg_digest_majority_async(self.ctx, digests_ptr, digest_stride, state_ptr,
                                                   n_slots, stream or None), self.ctx)

@@ -8,10 +8,15 @@ watermark, last_committed, counts) and, optionally, its decided bitmap; ranks
 all_gather them (RCCL over xGMI when the backend is "nccl") and fold them into
 the global commit view here.
 
-Results are shard-invariant in WMVC mode (the coin is keyed by the GLOBAL slot
-id). In REF mode each shard is its own engine with its own StdRng stream
-(sharded-KV instances); a single REF stream spanning shards would need the
-cross-shard VQ prefix.
+Results are shard-invariant in both modes. WMVC: the coin is keyed by the
+GLOBAL slot id. REF: every rank holds the SAME engine seed and the window's one
+StdRng stream (engine.rs:59-62) is consumed in ascending slot order across the
+shards: shard r's k-th VQ slot takes the draw at  rng_next + (VQ slots of shards
+< r) + k  (engine.rs:567-611). The device does it without a cross-GPU wait in the
+step (include/rabia_gpu.h, "Sharded REF"): step with provisional draw positions
++ draw records -> all_gather of the rows -> fix-up at the global positions ->
+all_gather of the final rows -> commit fold. `draw_bases` / `combine` below are the
+same algebra on the host.
 """
 from __future__ import annotations
 
@@ -68,6 +73,16 @@ def combine(results, starts, counts, slot_base: int, watermark_in: int, last_com
                         tot["n_draws"], lc, fu, wm, tot["flags"])
 
 
+def draw_bases(n_draws, rng_base: int):
+    """Global StdRng position of each shard's first draw: rng_base + the VQ slots of
+    the shards before it (exclusive prefix in rank order)."""
+    out, acc = [], int(rng_base)
+    for c in n_draws:
+        out.append(acc)
+        acc += int(c)
+    return out, acc
+
+
 def result_row(d: dict):
     return [int(d.get(k, 0)) for k in RESULT_FIELDS]
 
@@ -98,3 +113,49 @@ def exchange_bitmap(plane_tensor, group=None):
     out = torch.empty(world * src.numel(), dtype=src.dtype, device=src.device)
     dist.all_gather_into_tensor(out, src, group=group)
     return out.view((world,) + tuple(plane_tensor.shape))
+
+
+class ShardedRefStep:
+    """One rank's driver of the sharded REF window (include/rabia_gpu.h): the four
+    stages of one window on this rank's evaluator, the two row exchanges going
+    through torch.distributed (all_gather_into_tensor on device rows for "nccl";
+    host copies for "gloo"). Synchronous per window; bench.py pipelines the same
+    calls across windows."""
+
+    def __init__(self, ev, rank: int, world: int, n_slots_cap: int, group=None):
+        import torch
+        self.ev, self.rank, self.world, self.group = ev, rank, world, group
+        self.cap = int(n_slots_cap)
+        self.records = torch.empty(max(self.cap, 1), dtype=torch.int64, device="cuda")
+        self.row = torch.zeros(10, dtype=torch.int64, device="cuda")
+        self.fixed = torch.zeros(10, dtype=torch.int64, device="cuda")
+        self.result = torch.zeros(10, dtype=torch.int64, device="cuda")
+
+    def _gather(self, row):
+        import torch
+        import torch.distributed as dist
+        if self.world == 1:
+            return row.view(1, 10).clone()
+        if dist.get_backend(self.group) == "nccl":
+            return exchange_results(row, self.group)
+        got = exchange_results(row.cpu(), self.group)
+        return got.to(row.device)
+
+    def step(self, votes_ptr, out_ptr, n_slots, stride, shard_base, window_base, window_slots,
+             max_phase=0, stream=0):
+        """Evaluate this rank's shard [shard_base, shard_base + n_slots) of the window
+        [window_base, window_base + window_slots); returns the global step result."""
+        import torch
+        ev = self.ev
+        ev.phase_step_shard_async(votes_ptr, out_ptr, n_slots, stride, shard_base, self.records.data_ptr(),
+                                  self.cap, self.row.data_ptr(), max_phase, stream)
+        torch.cuda.synchronize()
+        rows = self._gather(self.row).contiguous()
+        ev.shard_fixup_async(out_ptr, n_slots, stride, shard_base, self.records.data_ptr(), self.cap,
+                             rows.data_ptr(), self.rank, self.world, self.fixed.data_ptr(), max_phase, stream)
+        torch.cuda.synchronize()
+        fixed = self._gather(self.fixed).contiguous()
+        ev.shard_commit_async(fixed.data_ptr(), self.world, window_base, window_slots, self.result.data_ptr(),
+                              stream)
+        torch.cuda.synchronize()
+        return row_result(self.result.cpu().numpy().view("uint64").tolist())

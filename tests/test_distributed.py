@@ -98,3 +98,74 @@ def test_two_rank_gloo_global_commit(oracle):
         assert g.commit_watermark == res["commit_watermark"]
         assert g.n_draws == res["n_draws"]
         np.testing.assert_array_equal(np.array(bits, np.uint8), out["committed"])
+
+
+def _ref_worker(rank, world, port, q):
+    """REF mode: every rank holds the SAME engine seed; the shard's draws start at
+    the global exclusive prefix of the shards' VQ counts (shard.draw_bases over an
+    all_gather), so the window consumes ONE StdRng stream in ascending slot order."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "tests"), root]
+    import oracle_lib as O
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n, S, base, rng0, seed = 5, 20_000, 1, 777, 42
+        r1, r2, _ = O.trace(0, n, 5, base, S)
+        start, count = shard.shard_range(S, world, rank)
+        sl = slice(start, start + count)
+        # the shard's VQ count does not depend on where its draws start
+        _, probe = O.ref_step(n, 3, 2, seed, 0, base + start, r1[sl], r2[sl], max_phase=S // 2, lc_in=5, wm_in=1)
+        counts = shard.exchange_results(torch.tensor([probe["n_draws"]], dtype=torch.int64)).view(-1).tolist()
+        bases, total = shard.draw_bases(counts, rng0)
+        out, res = O.ref_step(n, 3, 2, seed, bases[rank], base + start, r1[sl], r2[sl], max_phase=S // 2,
+                              lc_in=5, wm_in=1)
+        assert res["rng_next"] == bases[rank] + counts[rank]
+        rows = shard.exchange_results(torch.tensor(shard.result_row(res), dtype=torch.int64))
+        starts = [shard.shard_range(S, world, r)[0] for r in range(world)]
+        cnts = [shard.shard_range(S, world, r)[1] for r in range(world)]
+        g = shard.combine([shard.row_result(rw.tolist()) for rw in rows], starts, cnts, base, 1, 5)
+        width = max(cnts)
+        packed = np.zeros((5, width), np.uint8)
+        for i, k in enumerate(("r1", "r2own", "dec", "committed", "value")):
+            packed[i, :count] = out[k]
+        allp = shard.exchange_bitmap(torch.from_numpy(packed)).numpy()
+        full = {k: np.concatenate([allp[r][i][:cnts[r]] for r in range(world)])
+                for i, k in enumerate(("r1", "r2own", "dec", "committed", "value"))}
+        q.put((rank, g, total, {k: v.tolist() for k, v in full.items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ref_shards_one_stream_gloo(oracle, world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ref_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    import queue
+    got = []
+    while len(got) < world:
+        try:
+            got.append(q.get(timeout=1))
+        except queue.Empty:
+            assert all(p.is_alive() or p.exitcode == 0 for p in procs), "a rank died"
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    n, S = 5, 20_000
+    r1, r2, _ = oracle.trace(0, n, 5, 1, S)
+    exp, eres = oracle.ref_step(n, 3, 2, 42, 777, 1, r1, r2, max_phase=S // 2, lc_in=5, wm_in=1)
+    assert eres["n_draws"] > 0
+    for rank, g, total, full in got:
+        assert total == eres["rng_next"]
+        assert g.n_draws == eres["n_draws"] and g.n_decided == eres["n_decided"] and g.n_v1 == eres["n_v1"]
+        assert g.last_committed == eres["last_committed_max"]
+        assert g.first_undecided == eres["first_undecided"]
+        assert g.commit_watermark == eres["commit_watermark"]
+        for k in exp:
+            np.testing.assert_array_equal(np.array(full[k], np.uint8), exp[k], err_msg=k)

@@ -1,0 +1,292 @@
+"""Sharded REF on the GPU: ONE engine (one StdRng stream, engine.rs:59-62) over a
+window split into contiguous shards, each shard on its own context (= its own
+rank), must equal one evaluator over the whole window — outputs bit for bit, the
+step result, and the engine state (rng_next, last_committed, contiguous
+watermark) on every rank. The single evaluator is itself checked against the
+oracle (test_gpu_parity.py); here both are also compared with the oracle directly
+where it finishes in seconds.
+
+Stages per window (include/rabia_gpu.h "Sharded REF"): step with provisional draw
+positions + draw records -> rows exchanged -> fix-up at the global positions ->
+final rows exchanged -> commit fold. In one process the exchange is a stack of the
+ranks' device rows; test_two_process_gloo runs it across processes."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from rabia_amd import _native as N
+from rabia_amd import shard
+from rabia_amd.engine import PhaseEvaluator, decode_outputs, plane_stride
+
+pytestmark = pytest.mark.gpu
+
+RES_CMP = ["n_slots", "n_decided", "n_v1", "n_pending_r1", "n_draws", "last_committed_max",
+           "first_undecided", "rng_next", "commit_watermark", "flags"]
+
+
+def torch_cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def rows_of(t):
+    return [shard.row_result(r) for r in t.cpu().numpy().view(np.uint64).tolist()]
+
+
+def run_sharded(n, world, window_sizes, votes, out, stride, seed=42, self_lane=None, state=None, max_phase=0,
+                cap=None, aligned=128, keep=None):
+    """Every window's stage 1 on every shard first (provisional positions pile up,
+    as in the pipelined bench), then fix-ups and commits window by window."""
+    torch = torch_cuda()
+    self_lane = n // 2 if self_lane is None else self_lane
+    ctxs = [PhaseEvaluator(n, self_lane=self_lane, seed=seed) for _ in range(world)]
+    try:
+        for ev in ctxs:
+            if state:
+                ev.set_state(**state)
+        W = len(window_sizes)
+        rows = torch.zeros((W, world, 10), dtype=torch.int64, device="cuda")
+        fixed = torch.zeros((W, world, 10), dtype=torch.int64, device="cuda")
+        result = torch.zeros((W, world, 10), dtype=torch.int64, device="cuda")
+        recs, plan = [], []
+        for S in window_sizes:
+            for r in range(world):
+                c = cap if cap is not None else max(shard.shard_range(S, world, r, align=aligned)[1], 1)
+                recs.append(torch.zeros(max(c, 1), dtype=torch.int64, device="cuda"))
+        # torch fills on its own stream; the contexts' streams do not wait for it
+        torch.cuda.synchronize()
+        base, off = 1, 0
+        for w, S in enumerate(window_sizes):
+            parts = []
+            for r in range(world):
+                start, cnt = shard.shard_range(S, world, r, align=aligned)
+                c = cap if cap is not None else max(cnt, 1)
+                rec = recs[w * world + r]
+                parts.append((start, cnt, rec, c))
+                if cnt:
+                    w0 = (off + start) // 32
+                    ctxs[r].phase_step_shard_async(votes.data_ptr() + 4 * w0, out.data_ptr() + 4 * w0, cnt, stride,
+                                                   base + start, rec.data_ptr(), c, rows[w, r].data_ptr(),
+                                                   max_phase=max_phase)
+                else:  # an empty shard still reports a row
+                    rows[w, r, 6] = base + S
+                    torch.cuda.synchronize()
+            plan.append((base, off, S, parts))
+            base += S
+            off += ((S + 127) // 128) * 128
+        torch.cuda.synchronize()
+        for w, (base, off, S, parts) in enumerate(plan):
+            g = rows[w].contiguous()
+            for r, (start, cnt, rec, c) in enumerate(parts):
+                if cnt:
+                    w0 = (off + start) // 32
+                    ctxs[r].shard_fixup_async(out.data_ptr() + 4 * w0, cnt, stride, base + start, rec.data_ptr(), c,
+                                              g.data_ptr(), r, world, fixed[w, r].data_ptr(), max_phase=max_phase)
+                else:
+                    fixed[w, r] = rows[w, r]
+                    torch.cuda.synchronize()
+            torch.cuda.synchronize()
+            fg = fixed[w].contiguous()
+            for r in range(world):
+                ctxs[r].shard_commit_async(fg.data_ptr(), world, base, S, result[w, r].data_ptr())
+            torch.cuda.synchronize()
+        states = [ev.get_state() for ev in ctxs]
+        if keep is not None:
+            keep.extend(r.cpu().numpy().view(np.uint64) for r in recs)
+    finally:
+        for ev in ctxs:
+            ev.close()
+    return [rows_of(result[w]) for w in range(len(window_sizes))], states, rows_of(rows[0]), rows_of(fixed[0])
+
+
+def run_single(n, window_sizes, votes, out, stride, seed=42, self_lane=None, state=None, max_phase=0):
+    torch = torch_cuda()
+    self_lane = n // 2 if self_lane is None else self_lane
+    res = torch.zeros((len(window_sizes), 10), dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    with PhaseEvaluator(n, self_lane=self_lane, seed=seed) as ev:
+        if state:
+            ev.set_state(**state)
+        base, off = 1, 0
+        for w, S in enumerate(window_sizes):
+            w0 = off // 32
+            ev.phase_step_async(votes.data_ptr() + 4 * w0, out.data_ptr() + 4 * w0, S, stride, slot_base=base,
+                                max_phase=max_phase, result_ptr=res[w].data_ptr())
+            base += S
+            off += ((S + 127) // 128) * 128
+        ev.sync()
+        st = ev.get_state()
+    return rows_of(res), st
+
+
+def make_votes(n, window_sizes, kind=1, seed=7):
+    """Windows laid out back to back (each padded to 128 slots) in one planar buffer."""
+    torch = torch_cuda()
+    total = sum(((S + 127) // 128) * 128 for S in window_sizes)
+    stride = plane_stride(total)
+    votes = torch.zeros((4 * n + 1) * stride, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    with PhaseEvaluator(n) as ev:
+        base, off = 1, 0
+        for S in window_sizes:
+            ev.trace_generate_async(kind, seed, base, S, stride, votes.data_ptr() + 4 * (off // 32))
+            base += S
+            off += ((S + 127) // 128) * 128
+        ev.sync()
+    return votes, stride, total
+
+
+@pytest.mark.parametrize("n,world,sizes,kind", [
+    (5, 2, [300_007], 1),
+    (3, 4, [100_003, 777, 50_000], 0),
+    (9, 3, [1 << 20], 1),
+    (7, 5, [262_144, 131_071], 2),
+    (16, 2, [70_001], 0),
+])
+def test_sharded_equals_one_engine(oracle, n, world, sizes, kind):
+    torch = torch_cuda()
+    votes, stride, total = make_votes(n, sizes, kind)
+    out_s = torch.zeros(8 * stride, dtype=torch.int32, device="cuda")
+    out_1 = torch.zeros(8 * stride, dtype=torch.int32, device="cuda")
+    state = {"rng_next": 1234, "last_committed": 3, "commit_watermark": 1, "steps": 0}
+    mp = sum(sizes) * 2 // 3  # commit_phase refuses V1 slots above current_phase
+    res_s, st_s, _, _ = run_sharded(n, world, sizes, votes, out_s, stride, state=state, max_phase=mp)
+    res_1, st_1 = run_single(n, sizes, votes, out_1, stride, state=state, max_phase=mp)
+    assert torch.equal(out_s, out_1)
+    for w in range(len(sizes)):
+        for r in range(world):
+            assert {k: res_s[w][r][k] for k in RES_CMP} == {k: res_1[w][k] for k in RES_CMP}, (w, r)
+    for st in st_s:
+        assert st == st_1
+    # and the oracle over the whole concatenation of windows (one stream across them)
+    planes = out_s.view(8, stride).cpu().numpy().view(np.uint32)
+    got = decode_outputs(planes, total)
+    base, off, rng = 1, 0, 1234
+    lc = 3
+    for w, S in enumerate(sizes):
+        r1, r2, _ = oracle.trace(kind, n, 7, base, S)
+        exp, eres = oracle.ref_step(n, n // 2 + 1, n // 2, 42, rng, base, r1, r2, max_phase=mp, lc_in=lc,
+                                    wm_in=res_1[w - 1]["commit_watermark"] if w else 1)
+        for k in exp:
+            np.testing.assert_array_equal(got[k][off:off + S], exp[k], err_msg=f"window {w} {k}")
+        assert eres["rng_next"] == res_s[w][0]["rng_next"]
+        assert eres["commit_watermark"] == res_s[w][0]["commit_watermark"]
+        rng, lc = eres["rng_next"], eres["last_committed_max"]
+        base += S
+        off += ((S + 127) // 128) * 128
+
+
+def test_sharded_full_size_c5_shape():
+    """C5 shape (9 replicas x 2^26 slots) over 8 shards == one evaluator (device
+    results compared bit for bit; the single evaluator is oracle-checked elsewhere)."""
+    torch = torch_cuda()
+    n, S, world = 9, 1 << 26, 8
+    votes, stride, total = make_votes(n, [S], 1, seed=11)
+    out_s = torch.zeros(8 * stride, dtype=torch.int32, device="cuda")
+    res_s, st_s, rows, fixed = run_sharded(n, world, [S], votes, out_s, stride)
+    out_1 = torch.zeros(8 * stride, dtype=torch.int32, device="cuda")
+    res_1, st_1 = run_single(n, [S], votes, out_1, stride)
+    assert torch.equal(out_s, out_1)
+    for r in range(world):
+        assert {k: res_s[0][r][k] for k in RES_CMP} == {k: res_1[0][k] for k in RES_CMP}
+    assert all(st == st_1 for st in st_s)
+    assert sum(x["n_draws"] for x in rows) == res_1[0]["n_draws"] > 0
+    del votes
+
+
+def test_records_capacity_overflow_is_flagged():
+    torch = torch_cuda()
+    n, S = 5, 200_000
+    votes, stride, total = make_votes(n, [S], 0)
+    out = torch.zeros(8 * stride, dtype=torch.int32, device="cuda")
+    res, _, _, _ = run_sharded(n, 2, [S], votes, out, stride, cap=16)
+    assert res[0][0]["flags"] & 8
+
+
+def test_shard_argument_errors():
+    torch = torch_cuda()
+    buf = torch.zeros(1 << 16, dtype=torch.int32, device="cuda")
+    with PhaseEvaluator(5, mode="wmvc") as ev:
+        with pytest.raises(N.RabiaGpuError):
+            ev.phase_step_shard_async(buf.data_ptr(), buf.data_ptr(), 100, 4, 1, buf.data_ptr(), 100)
+    with PhaseEvaluator(5) as ev:
+        with pytest.raises(N.RabiaGpuError):
+            ev.phase_step_shard_async(buf.data_ptr(), buf.data_ptr(), 100, 4, 1, 0, 100)
+        with pytest.raises(N.RabiaGpuError):
+            ev.shard_fixup_async(buf.data_ptr(), 100, 4, 1, buf.data_ptr(), 100, buf.data_ptr(), 2, 2)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _rank(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "tests"), root]
+    import torch
+    import torch.distributed as dist
+    from rabia_amd import shard as SH
+    from rabia_amd.engine import PhaseEvaluator as PE, plane_stride as ps
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n, S = 5, 500_000
+        start, cnt = SH.shard_range(S, world, rank)
+        stride = ps(cnt)
+        votes = torch.zeros((4 * n + 1) * stride, dtype=torch.int32, device="cuda")
+        out = torch.zeros(8 * stride, dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        with PE(n, self_lane=2, seed=42) as ev:  # the same engine seed on every rank
+            ev.trace_generate_async(1, 9, 1 + start, cnt, stride, votes.data_ptr())
+            drv = SH.ShardedRefStep(ev, rank, world, cnt)
+            g = drv.step(votes.data_ptr(), out.data_ptr(), cnt, stride, 1 + start, 1, S)
+            st = ev.get_state()
+        planes = out.view(8, stride).cpu().numpy().view(np.uint32)
+        q.put((rank, g, st, planes.tobytes(), stride, start, cnt))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_process_gloo(oracle):
+    """Two ranks (processes) on the one GPU, rows exchanged over gloo: the folded
+    global result and every rank's state == the oracle's single engine."""
+    torch_cuda()
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    import queue
+    got = []
+    while len(got) < world:
+        try:
+            got.append(q.get(timeout=1))
+        except queue.Empty:
+            assert all(p.is_alive() or p.exitcode == 0 for p in procs), "a rank died"
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    n, S = 5, 500_000
+    r1, r2, _ = oracle.trace(1, n, 9, 1, S)
+    exp, eres = oracle.ref_step(n, 3, 2, 42, 0, 1, r1, r2)
+    for rank, g, st, raw, stride, start, cnt in sorted(got, key=lambda x: x[0]):
+        for k in ("n_slots", "n_decided", "n_v1", "n_pending_r1", "n_draws", "last_committed_max",
+                  "first_undecided", "rng_next", "commit_watermark"):
+            assert g[k] == eres[k], (rank, k)
+        assert st["rng_next"] == eres["rng_next"] and st["commit_watermark"] == eres["commit_watermark"]
+        assert st["last_committed"] == eres["last_committed_max"]
+        dec = decode_outputs(np.frombuffer(raw, np.uint32).reshape(8, stride), cnt)
+        for k in exp:
+            np.testing.assert_array_equal(dec[k], exp[k][start:start + cnt], err_msg=f"rank {rank} {k}")
