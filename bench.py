@@ -3,16 +3,22 @@
 
 Workload (BASELINE.json configs[1], "C2"): 5 replicas, windows of 2^20 slots,
 90%-agreement synthetic vote trace, REF single phase sweep. One bench "step" is
-one launch over `--windows` consecutive 2^20-slot windows (default 256: the
-steady-state streaming batch; --windows 1 is the single-sweep latency case and is
-also reported as `sweep_1m_us`). Inputs are generated on the device before the
-timed region and rotate over 3 buffer sets (> 2x the 256 MiB Infinity Cache) so
-every step reads from HBM.
+one launch over `--windows` consecutive 2^20-slot windows per GPU (default 256:
+the steady-state streaming batch; the single-window latency is reported as
+`sweep_1m_us`). Inputs are generated on the device before the timed region and
+rotate over 3 buffer sets (> 2x the 256 MiB Infinity Cache) so every step reads
+from HBM.
 
-Multi-GPU (torchrun, one rank per GPU): every rank is one slot shard with its own
-engine context (weak scaling); after each step the per-shard step results
-(commit watermark, last_committed, counts) are exchanged with an RCCL all_gather
-that overlaps the next step.
+Multi-GPU (torchrun, one rank per GPU): ONE engine — every rank holds the same
+StdRng seed — over a global window of world x (windows x 2^20) slots per step,
+rank r owning the r-th contiguous shard (weak scaling). The shard's REF step runs
+with provisional draw positions and leaves draw records; the shard rows are
+all-gathered over RCCL, each rank re-draws its VQ slots at their global stream
+positions (rg_shard_fixup_async), the final rows are all-gathered again and folded
+into every rank's engine state (rg_shard_commit_async). The exchange and fix-up
+run on a second stream, so the step kernels of later windows never wait for them.
+`--config c5`: 9 replicas x 2^26 slots per step split over the ranks (strong
+scaling), decided/V1 bitmaps all-gathered every step as well.
 
 Prints ONE JSON line on rank 0.
 """
@@ -22,6 +28,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -35,6 +42,7 @@ from rabia_amd.engine import PhaseEvaluator  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 WINDOW = 1 << 20
+SEED = 42  # RabiaConfig.randomization_seed of the one engine (integration_consensus.rs:404-408)
 
 
 def bytes_per_slot_ref(n: int) -> float:
@@ -53,32 +61,108 @@ def parse():
     ap.add_argument("--sets", type=int, default=3)
     ap.add_argument("--tile-words", type=int, default=1024,
                     help="slot-tiled plane layout (include/rabia_gpu.h); 0 = planar")
-    ap.add_argument("--cpu-sample-windows", type=int, default=8)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads of the all-core CPU baseline (0: OMP_NUM_THREADS, else min(cpus, 16))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_c2.json"))
     ap.add_argument("--config", choices=["c2", "c5"], default="c2",
-                    help="c2: the headline (weak scaling, per-shard results exchanged); c5: 9 replicas x "
-                         "2^26 slots per step split over the ranks (strong scaling) with the decision "
-                         "bitmaps all-gathered every step")
+                    help="c2: the headline (weak scaling); c5: 9 replicas x 2^26 slots per step split over the "
+                         "ranks (strong scaling) with the decision bitmaps all-gathered every step")
     ap.add_argument("--c5-windows", type=int, default=64, help="C5: 2^20-slot windows per step, all ranks")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="nccl = RCCL over xGMI; gloo = several ranks on one GPU (rehearsal only)")
     return ap.parse_args()
 
 
-def cpu_baseline(n: int, windows: int):
-    """Structure-faithful REF path (oracle/rabia_oracle.c:or_ref_structured: per-slot
-    NodeId->StateValue maps, one handler call per vote, PhaseData clone per read),
-    single thread, on `windows` x 2^20 slots of the same trace kind."""
+# ---------------------------------------------------------------------------
+# CPU baseline (rank 0, N = 1 only): the reference's Rust/Tokio path cannot run
+# here (no toolchain), so three C restatements of it are timed on this host:
+#   structure-faithful (per-slot NodeId->StateValue maps, one handler call per
+#   vote, PhaseData clone per read: oracle/rabia_oracle.c:or_ref_structured),
+#   1 thread and one independent engine instance per core; and the fast SoA
+#   path (oracle/rabia_cpu_soa.c: bit-sliced, 64 slots per op, OpenMP) on all
+#   cores over the same planes the GPU reads.
+# ---------------------------------------------------------------------------
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_threads(a) -> int:
+    if a.cpu_threads > 0:
+        return a.cpu_threads
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    return max(1, min(os.cpu_count() or 1, 16))
+
+
+def cpu_baseline(a, n: int, ev: PhaseEvaluator, stream) -> dict:
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
-    S = windows * WINDOW
-    r1, r2, _ = O.trace(1, n, 42, 1, S)
+    th = cpu_threads(a)
+    q, lane = n // 2 + 1, n - 1
+    # (1) structure-faithful, one thread
+    S1 = 4 * WINDOW
+    r1, r2, _ = O.trace(1, n, SEED, 1, S1)
     t0 = time.perf_counter()
-    _, res = O.ref_structured(n, n // 2 + 1, n - 1, 42, 0, 1, r1, r2)
-    dt = time.perf_counter() - t0
-    return {"value": res["n_decided"] / dt, "unit": "slots decided/s", "cores": 1, "kind": "port",
-            "sample": f"{S} slots ({windows} x 2^20 windows, agree90 trace, n={n}) through the "
-                      f"structure-faithful REF restatement (oracle/rabia_oracle.c:or_ref_structured), "
-                      f"1 thread, {dt:.2f} s"}
+    _, res = O.ref_structured(n, q, lane, SEED, 0, 1, r1, r2)
+    dt1 = time.perf_counter() - t0
+    sf1 = res["n_decided"] / dt1
+    # (2) structure-faithful, one engine instance per core (ctypes drops the GIL)
+    out = [0.0] * th
+
+    def inst(i):
+        t = time.perf_counter()
+        _, rr = O.ref_structured(n, q, lane, SEED + i, 0, 1, r1, r2)
+        out[i] = (rr["n_decided"], time.perf_counter() - t)
+
+    ts = [threading.Thread(target=inst, args=(i,)) for i in range(th)]
+    t0 = time.perf_counter()
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    dtp = time.perf_counter() - t0
+    sfp = sum(x[0] for x in out) / dtp
+    # (3) SoA all cores on the GPU's own planar planes (same trace kind/seed)
+    S3 = 256 * WINDOW  # the GPU step's size: 704 MB of planes, past the host's L3
+    stride = ((S3 + 127) // 128) * 4
+    planar = PhaseEvaluator(n, self_lane=lane, seed=SEED, tile_words=0)
+    votes = torch.empty((4 * n + 1) * stride, dtype=torch.int32, device="cuda")
+    planar.trace_generate_async(N.RG_TRACE_AGREE90, SEED, 1, S3, stride, votes.data_ptr(), stream.cuda_stream)
+    outp = torch.empty(8 * stride, dtype=torch.int32, device="cuda")
+    resd = torch.zeros(10, dtype=torch.int64, device="cuda")
+    planar.phase_step_async(votes.data_ptr(), outp.data_ptr(), S3, stride, 1, result_ptr=resd.data_ptr(),
+                            stream=stream.cuda_stream)
+    torch.cuda.synchronize()
+    host = votes.view(4 * n + 1, stride).cpu().numpy().view(np.uint32)
+    gpu_res = resd.cpu().numpy().view(np.uint64)
+    planar.close()
+    del votes, outp
+    times = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        _, sres = O.ref_step_soa(n, q, lane, SEED, 0, 1, host, stride, S3, threads=th)
+        times.append(time.perf_counter() - t0)
+    dt3 = float(np.median(times))
+    soa = sres["n_decided"] / dt3
+    # the CPU fast path and the GPU agree on the same planes (decided count, draws)
+    agree = int(gpu_res[1]) == sres["n_decided"] and int(gpu_res[4]) == sres["n_draws"]
+    return {"value": soa, "unit": "slots decided/s", "cores": th, "kind": "port",
+            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+            "sample": f"SoA all-core path (oracle/rabia_cpu_soa.c, {th} OpenMP threads) over {S3} slots "
+                      f"(256 x 2^20, agree90, n={n}, the GPU's planar planes), median of 5 = {dt3:.3f} s; "
+                      f"agrees with the GPU step on decided/draws: {agree}",
+            "structure_faithful_1t": {"value": sf1, "slots": S1, "seconds": dt1},
+            "structure_faithful_per_core": {"value": sfp, "instances": th, "slots_each": S1, "seconds": dtp},
+            "soa_all_cores": {"value": soa, "threads": th, "slots": S3, "seconds": dt3, "gpu_agrees": agree}}
 
 
 def load_pmc(path: str, n: int, slots: int):
@@ -92,214 +176,63 @@ def load_pmc(path: str, n: int, slots: int):
     return None
 
 
-def run_c5(a, world, rank, local, dist):
-    """C5 (BASELINE.json configs[4]): 9 replicas, a 2^26-slot window per step split into
-    equal contiguous shards (one per rank), REF sweep, then the streaming exchange: every
-    rank extracts its committed + V1 bitmaps and all-gathers them and its step result
-    (RCCL over xGMI) on the collective stream while the next step computes. After the
-    timed loop the gathered rows are folded into the global commit watermark
-    (rabia_amd/shard.py:combine) and checked against the per-shard counts."""
-    from rabia_amd import shard
-    n, T = 9, a.tile_words
-    total = a.c5_windows * WINDOW
-    start, S = shard.shard_range(total, world, rank, align=32 * (T or 4))
-    assert S * world == total, "C5 needs equal shards"
-    nw = S // 32
-    stride = T if T else ((S + 127) // 128) * 4
-    in_words = ((nw + T - 1) // T) * (4 * n + 1) * T if T else (4 * n + 1) * stride
-    out_words = ((nw + T - 1) // T) * 8 * T if T else 8 * stride
-    stream = torch.cuda.Stream()
-    torch.cuda.set_stream(stream)
-    sp = stream.cuda_stream
-    ev = PhaseEvaluator(n, self_lane=n - 1, mode="ref", seed=42 + rank, device=local, tile_words=T)
-    sets = []
-    for i in range(a.sets):
-        votes = torch.empty(in_words, dtype=torch.int32, device="cuda")
-        out = torch.empty(out_words, dtype=torch.int32, device="cuda")
-        ev.trace_generate_async(N.RG_TRACE_AGREE90, 1000 * rank + i, 1 + start, S, stride, votes.data_ptr(), sp)
-        sets.append((votes, out))
-    n_total = a.warmup + a.steps
-    res_dev = torch.zeros((n_total, 10), dtype=torch.int64, device="cuda")
-    gathered = torch.zeros((n_total, world, 10), dtype=torch.int64, device="cuda")
-    bm = torch.zeros((n_total, 2, nw), dtype=torch.int32, device="cuda")
-    bm_all = torch.zeros((n_total, world, 2, nw), dtype=torch.int32, device="cuda")
-    torch.cuda.synchronize()
-    works = []
-
-    def step(t):
-        votes, out = sets[t % a.sets]
-        base = 1 + t * total
-        ev.phase_step_async(votes.data_ptr(), out.data_ptr(), S, stride, slot_base=base + start,
-                            result_ptr=res_dev[t].data_ptr(), stream=sp)
-        ev.decision_bitmap_async(out.data_ptr(), S, stride, bm[t, 0].data_ptr(), bm[t, 1].data_ptr(), sp)
-        if dist is not None:
-            works.append(dist.all_gather_into_tensor(gathered[t], res_dev[t], async_op=True))
-            works.append(dist.all_gather_into_tensor(bm_all[t], bm[t], async_op=True))
-
-    for t in range(a.warmup):
-        step(t)
-    for w in works:
-        w.wait()
-    works.clear()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t_begin, t_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t_begin.record(stream)
-    for k in range(a.steps):
-        step(a.warmup + k)
-    for w in works:
-        w.wait()
-    t_end.record(stream)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    total_ms = t_begin.elapsed_time(t_end)
-    res = res_dev.cpu().numpy().view(np.uint64)
-    if int(res[:, 9].max()) != 0:
-        raise RuntimeError("device-side protocol fault flagged in a step result")
-    g = gathered.cpu().numpy().view(np.uint64) if dist is not None else res[:, None, :]
-    b_all = bm_all.cpu().numpy().view(np.uint32) if dist is not None else bm.cpu().numpy().view(np.uint32)[:, None]
-    decided = 0
-    for t in range(a.warmup, n_total):  # global commit per step, checked against the bitmaps
-        rows = [shard.row_result(g[t, r]) for r in range(world)]
-        starts = [shard.shard_range(total, world, r, align=32 * (T or 4))[0] for r in range(world)]
-        gc = shard.combine(rows, [1 + t * total + s_ for s_ in starts], [S] * world, 1 + t * total, 1 + t * total)
-        pop = int(np.unpackbits(b_all[t, :, 0].view(np.uint8)).sum())
-        assert pop == gc.n_decided, (pop, gc.n_decided)
-        decided += gc.n_decided
-    tm = torch.tensor([total_ms], dtype=torch.float64, device="cuda")
-    if dist is not None:
-        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
-    total_ms = float(tm[0])
-    if rank == 0:
-        bitmap_bytes = 2 * nw * 4 * world
-        line = {
-            "metric": "consensus slots decided/sec (9 replicas, 2^26 slots per step, bitmap all-gather)",
-            "value": decided / (total_ms / 1000.0),
-            "unit": "slots decided/s",
-            "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": total_ms / a.steps,
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
-            "dtype": "u32 bit-sliced 2-bit vote codes (integer only)",
-            "data": "synthetic (seeded agree90 vote trace generated on device)",
-            "config": {"workload": f"C5: {n} replicas x {total} slots per step, REF sweep, committed + V1 "
-                                   f"bitmaps ({bitmap_bytes} B per step in all) and step results all-gathered "
-                                   f"every step, overlapped with the next step",
-                       "replicas": n, "slots_per_step": total, "slots_per_gpu": S,
-                       "layout": f"slot-tiled {T}" if T else "planar", "parallelism": f"slot-shard x{world}"},
-        }
-        print(json.dumps(line), flush=True)
-    ev.close()
-
-
-def main():
-    a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    if a.config == "c5":
-        run_c5(a, world, rank, local, dist)
-        if dist is not None:
-            dist.destroy_process_group()
-        return
-    n, G = a.replicas, a.windows
-    S = G * WINDOW
-    T = a.tile_words
-    nw = S // 32
+def layout(n, S, T):
+    nw = (S + 31) // 32
     if T:  # slot-tiled: the planes of each T-word slot tile are contiguous
-        stride = T
-        in_words = ((nw + T - 1) // T) * (4 * n + 1) * T
-        out_words = ((nw + T - 1) // T) * 8 * T
-    else:
-        stride = ((S + 127) // 128) * 4
-        in_words, out_words = (4 * n + 1) * stride, 8 * stride
-    # A dedicated stream: the legacy default stream has handle 0, which the C ABI
-    # reads as "the context's own stream"; events must sit on the launch stream.
+        return T, ((nw + T - 1) // T) * (4 * n + 1) * T, ((nw + T - 1) // T) * 8 * T
+    stride = ((S + 127) // 128) * 4
+    return stride, (4 * n + 1) * stride, 8 * stride
+
+
+# ---------------------------------------------------------------------------
+# one GPU: the single evaluator
+# ---------------------------------------------------------------------------
+def run_single(a, n, S, label):
+    T = a.tile_words
+    stride, in_words, out_words = layout(n, S, T)
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
-    assert sp != 0
-
-    ev = PhaseEvaluator(n, self_lane=n - 1, mode="ref", seed=42 + rank, device=local, tile_words=T)
+    ev = PhaseEvaluator(n, self_lane=n - 1, mode="ref", seed=SEED, tile_words=T)
     sets = []
     for i in range(a.sets):
         votes = torch.empty(in_words, dtype=torch.int32, device="cuda")
         out = torch.empty(out_words, dtype=torch.int32, device="cuda")
-        ev.trace_generate_async(N.RG_TRACE_AGREE90, 1000 * rank + i, 1 + i * S, S, stride,
-                                votes.data_ptr(), sp)
+        ev.trace_generate_async(N.RG_TRACE_AGREE90, 1000 + i, 1 + i * S, S, stride, votes.data_ptr(), sp)
         sets.append((votes, out))
     n_total = a.warmup + a.steps
     res_dev = torch.zeros((n_total, 10), dtype=torch.int64, device="cuda")
-    gathered = torch.zeros((n_total, world, 10), dtype=torch.int64, device="cuda") if world > 1 else None
     torch.cuda.synchronize()
-
-    rank_base = 1 + rank * (1 << 40)  # disjoint slot-id range per shard
-    works = []
 
     def step(t, evs=None):
         votes, out = sets[t % a.sets]
         if evs is not None:
             evs[0].record(stream)
-        ev.phase_step_async(votes.data_ptr(), out.data_ptr(), S, stride,
-                            slot_base=rank_base + t * S, result_ptr=res_dev[t].data_ptr(), stream=sp)
+        ev.phase_step_async(votes.data_ptr(), out.data_ptr(), S, stride, slot_base=1 + t * S,
+                            result_ptr=res_dev[t].data_ptr(), stream=sp)
         if evs is not None:
             evs[1].record(stream)
-        if dist is not None:  # global commit exchange, overlapped with the next step
-            works.append(dist.all_gather_into_tensor(gathered[t], res_dev[t], async_op=True))
 
     for t in range(a.warmup):
         step(t)
     torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(a.steps)]
-    t_begin = torch.cuda.Event(enable_timing=True)
-    t_end = torch.cuda.Event(enable_timing=True)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    t_begin, t_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t_begin.record(stream)
     for k in range(a.steps):
         step(a.warmup + k, evs[k])
-    for w in works:
-        w.wait()
     t_end.record(stream)
     torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
     total_ms = t_begin.elapsed_time(t_end)
-    kern_ms = [b.elapsed_time(e) for b, e in evs]
+    kern_ms = float(np.mean([b.elapsed_time(e) for b, e in evs]))
     res = res_dev.cpu().numpy().view(np.uint64)
     if int(res[:, 9].max()) != 0:
         raise RuntimeError("device-side protocol fault flagged in a step result")
     timed = res[a.warmup:]
     assert (timed[:, 0] == S).all(), "a timed step did not complete"
-    decided_total = int(timed[:, 1].sum())
-    if dist is not None:  # every shard's step results arrived through the exchange
-        g = gathered.cpu().numpy().view(np.uint64)
-        assert (g[a.warmup:, :, 0] == S).all()
-
-    tmax = torch.tensor([total_ms, float(np.mean(kern_ms)), float(decided_total)], dtype=torch.float64,
-                        device="cuda")
-    if dist is not None:
-        t_all = tmax.clone()
-        dist.all_reduce(t_all[:2], op=dist.ReduceOp.MAX)
-        dec_all = tmax[2:].clone()
-        dist.all_reduce(dec_all, op=dist.ReduceOp.SUM)
-        total_ms, kavg_ms, decided_all = float(t_all[0]), float(t_all[1]), float(dec_all[0])
-    else:
-        kavg_ms, decided_all = float(np.mean(kern_ms)), float(decided_total)
-
-    # single-window (C2 one sweep) latency, untimed w.r.t. the headline
+    decided = int(timed[:, 1].sum())
     sweep_us = None
-    if rank == 0:
+    if label == "c2":  # single-window (C2 one sweep) latency, outside the headline
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         reps = 20
         e0.record(stream)
@@ -309,39 +242,188 @@ def main():
         e1.record(stream)
         torch.cuda.synchronize()
         sweep_us = e0.elapsed_time(e1) * 1000.0 / reps
+    return {"total_ms": total_ms, "kern_ms": kern_ms, "decided": decided, "sweep_us": sweep_us, "ev": ev,
+            "stream": stream}
 
+
+# ---------------------------------------------------------------------------
+# N GPUs: one engine over a window split into contiguous shards
+# ---------------------------------------------------------------------------
+def make_gather(dist, backend):
+    """all_gather of one row/bitmap per rank into out[world, ...], enqueued on the
+    current stream (RCCL); "gloo" is a one-GPU rehearsal through host copies."""
+    if backend == "nccl":
+        return lambda out, inp: dist.all_gather_into_tensor(out, inp, async_op=True).wait()
+
+    def gather(out, inp):
+        torch.cuda.current_stream().synchronize()
+        parts = [torch.empty_like(inp, device="cpu") for _ in range(out.shape[0])]
+        dist.all_gather(parts, inp.cpu())
+        out.copy_(torch.stack(parts))
+    return gather
+
+
+def run_sharded(a, n, S, window_slots, world, rank, dist, bitmaps):
+    T = a.tile_words
+    gather = make_gather(dist, a.backend)
+    stride, in_words, out_words = layout(n, S, T)
+    comp = torch.cuda.Stream()
+    fix = torch.cuda.Stream()
+    torch.cuda.set_stream(comp)
+    ev = PhaseEvaluator(n, self_lane=n - 1, mode="ref", seed=SEED, tile_words=T)  # one seed on every rank
+    cap = max(S // 8, 1 << 16)  # draw records per shard step (agree90: ~1 % of slots are VQ); overflow -> flags
+    sets = []
+    start = rank * S
+    for i in range(a.sets):
+        votes = torch.empty(in_words, dtype=torch.int32, device="cuda")
+        out = torch.empty(out_words, dtype=torch.int32, device="cuda")
+        rec = torch.empty(cap, dtype=torch.int64, device="cuda")
+        ev.trace_generate_async(N.RG_TRACE_AGREE90, 1000 + i, 1 + i * window_slots + start, S, stride,
+                                votes.data_ptr(), comp.cuda_stream)
+        sets.append((votes, out, rec))
+    n_total = a.warmup + a.steps
+    i64 = dict(dtype=torch.int64, device="cuda")
+    rows = torch.zeros((n_total, 10), **i64)
+    g_rows = torch.zeros((n_total, world, 10), **i64)
+    fixed = torch.zeros((n_total, 10), **i64)
+    g_fixed = torch.zeros((n_total, world, 10), **i64)
+    result = torch.zeros((n_total, 10), **i64)
+    nw = (S + 31) // 32
+    if bitmaps:
+        bm = torch.zeros((n_total, 2, nw), dtype=torch.int32, device="cuda")
+        bm_all = torch.zeros((n_total, world, 2, nw), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    e_main = [torch.cuda.Event() for _ in range(n_total)]
+    e_done = [torch.cuda.Event() for _ in range(n_total)]
+
+    def step(t, evs=None):
+        votes, out, rec = sets[t % a.sets]
+        base = 1 + t * window_slots
+        if t >= a.sets:  # the output buffer and records of window t - sets must be fixed up first
+            comp.wait_event(e_done[t - a.sets])
+        if evs is not None:
+            evs[0].record(comp)
+        ev.phase_step_shard_async(votes.data_ptr(), out.data_ptr(), S, stride, base + start, rec.data_ptr(), cap,
+                                  rows[t].data_ptr(), stream=comp.cuda_stream)
+        if evs is not None:
+            evs[1].record(comp)
+        e_main[t].record(comp)
+        with torch.cuda.stream(fix):
+            fix.wait_event(e_main[t])
+            gather(g_rows[t], rows[t])
+            ev.shard_fixup_async(out.data_ptr(), S, stride, base + start, rec.data_ptr(), cap, g_rows[t].data_ptr(),
+                                 rank, world, fixed[t].data_ptr(), stream=fix.cuda_stream)
+            gather(g_fixed[t], fixed[t])
+            ev.shard_commit_async(g_fixed[t].data_ptr(), world, base, window_slots, result[t].data_ptr(),
+                                  stream=fix.cuda_stream)
+            if bitmaps:
+                ev.decision_bitmap_async(out.data_ptr(), S, stride, bm[t, 0].data_ptr(), bm[t, 1].data_ptr(),
+                                         fix.cuda_stream)
+                gather(bm_all[t], bm[t])
+            e_done[t].record(fix)
+
+    for t in range(a.warmup):
+        step(t)
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    t_begin, t_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t_begin.record(comp)
+    for k in range(a.steps):
+        step(a.warmup + k, evs[k])
+    comp.wait_event(e_done[n_total - 1])
+    t_end.record(comp)
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    total_ms = t_begin.elapsed_time(t_end)
+    kern_ms = float(np.mean([b.elapsed_time(e) for b, e in evs]))
+    res = result.cpu().numpy().view(np.uint64)
+    if int(res[:, 9].max()) != 0 or int(fixed.cpu().numpy().view(np.uint64)[:, 9].max()) != 0:
+        raise RuntimeError("device-side fault flagged in a step result (look-back timeout or record overflow)")
+    timed = res[a.warmup:]
+    assert (timed[:, 0] == window_slots).all(), "a timed window did not complete"
+    decided = int(timed[:, 1].sum())  # global (every shard), identical on every rank
+    if bitmaps:  # the gathered committed bitmaps carry exactly the folded decided count
+        b_all = bm_all[a.warmup:].cpu().numpy().view(np.uint32)
+        pop = int(np.unpackbits(b_all[:, :, 0].view(np.uint8)).sum())
+        assert pop == decided, (pop, decided)
+    tm = torch.tensor([total_ms, kern_ms], dtype=torch.float64, device="cuda" if a.backend == "nccl" else "cpu")
+    dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+    return {"total_ms": float(tm[0]), "kern_ms": float(tm[1]), "decided": decided, "sweep_us": None, "ev": ev,
+            "stream": comp}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.backend == "gloo":  # rehearsal: ranks may share the box's one GPU
+        local %= torch.cuda.device_count()
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
+    if a.config == "c5":
+        n, window_slots = 9, a.c5_windows * WINDOW
+        assert window_slots % (world * 32 * (a.tile_words or 4)) == 0, "C5 needs equal tile-aligned shards"
+        S = window_slots // world
+    else:
+        n, S = a.replicas, a.windows * WINDOW
+        window_slots = S * world
+    if world == 1:
+        r = run_single(a, n, S, a.config)
+    else:
+        r = run_sharded(a, n, S, window_slots, world, rank, dist, bitmaps=a.config == "c5")
     if rank == 0:
-        value = decided_all / (total_ms / 1000.0)
+        value = r["decided"] / (r["total_ms"] / 1000.0)
         alg_bytes = S * bytes_per_slot_ref(n)
-        achieved = alg_bytes / (kavg_ms / 1000.0) / 1e9
-        cpu = None if a.no_cpu_baseline else cpu_baseline(n, a.cpu_sample_windows)
+        achieved = alg_bytes / (r["kern_ms"] / 1000.0) / 1e9
+        cpu = None if (a.no_cpu_baseline or world > 1 or a.config != "c2") else cpu_baseline(a, n, r["ev"],
+                                                                                              r["stream"])
+        par = f"slot-shard x{world}" + (", one engine: sharded draws + fix-up" if world > 1 else "")
+        if a.config == "c5":
+            metric = "consensus slots decided/sec (9 replicas, 2^26 slots per step, bitmap all-gather)"
+            workload = (f"C5: {n} replicas x {window_slots} slots per step (one engine), REF sweep split over "
+                        f"{world} GPU(s)" + (", committed + V1 bitmaps and shard rows all-gathered every step"
+                                             if world > 1 else ""))
+            scaling = "strong"
+        else:
+            metric = "consensus slots decided/sec (5 replicas, 1M slots) + HBM GB/s as % of peak"
+            workload = (f"C2: {n} replicas x 2^20-slot windows, agree90 trace, REF single phase sweep; "
+                        f"{a.windows} windows per step per GPU, one engine over all GPUs' windows")
+            scaling = "weak"
         line = {
-            "metric": "consensus slots decided/sec (5 replicas, 1M slots) + HBM GB/s as % of peak",
+            "metric": metric,
             "value": value,
             "unit": "slots decided/s",
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": total_ms / a.steps,
+            "ms_per_step": r["total_ms"] / a.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "u32 bit-sliced 2-bit vote codes (integer only)",
             "data": "synthetic (seeded agree90 vote trace generated on device)",
-            "config": {"workload": f"C2: {n} replicas x 2^20-slot windows, agree90 trace, REF single phase "
-                                   f"sweep; {G} windows per step per GPU",
-                       "replicas": n, "slots_per_window": WINDOW, "windows_per_step": G,
-                       "slots_per_step_per_gpu": S, "mode": "ref", "layout": f"slot-tiled {T}" if T else "planar",
-                       "parallelism": f"slot-shard x{world}"},
+            "config": {"workload": workload, "replicas": n, "slots_per_window": WINDOW,
+                       "slots_per_step_per_gpu": S, "slots_per_step": window_slots, "mode": "ref",
+                       "layout": f"slot-tiled {a.tile_words}" if a.tile_words else "planar", "parallelism": par},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": load_pmc(a.pmc_file, n, S),
-                         "alg_bytes_per_launch": alg_bytes, "kernel_avg_us": kavg_ms * 1000.0},
+                         "traffic": load_pmc(a.pmc_file, n, S) if world == 1 else None,
+                         "alg_bytes_per_launch": alg_bytes, "kernel_avg_us": r["kern_ms"] * 1000.0},
             "cpu_baseline": cpu,
-            "sweep_1m_us": sweep_us,
+            "sweep_1m_us": r["sweep_us"],
         }
         print(json.dumps(line), flush=True)
-    ev.close()
+    r["ev"].close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -88,6 +88,16 @@ int or_ref_structured(int n, int q, int self_lane, uint64_t seed, uint64_t rng_b
                       uint64_t slot_base, const uint8_t* r1, const uint8_t* r2,
                       uint64_t S, uint8_t* o_dec, or_result* res);
 
+/* --- fast CPU path (bench all-core baseline; rabia_cpu_soa.c) --------------- */
+/* or_ref_step on the device's planar plane layout (votes: (4n+1) planes of
+ * `stride` u32 words, stride even), 64 slots per u64 op, OpenMP over chunks
+ * (n_threads <= 0: OpenMP default). out: 8 planes x stride (may be NULL). */
+int or_ref_step_soa(int n, int q, int self_lane, uint64_t seed, uint64_t rng_base, uint64_t slot_base,
+                    uint64_t max_phase, uint64_t last_committed_in, uint64_t watermark_in,
+                    const uint32_t* votes, uint64_t stride, uint64_t S, uint32_t* out, or_result* res,
+                    int n_threads);
+int or_omp_max_threads(void);
+
 /* --- synthetic traces (restatement of the device generator) ----------------- */
 void or_trace(int kind, int n, uint64_t seed, uint64_t slot_base, uint64_t S,
               uint8_t* r1, uint8_t* r2, uint8_t* state);

@@ -32,7 +32,7 @@ _lib = None
 
 
 def build():
-    src = [os.path.join(ORACLE_DIR, f) for f in ("rabia_oracle.c", "rabia_oracle.h")]
+    src = [os.path.join(ORACLE_DIR, f) for f in ("rabia_oracle.c", "rabia_cpu_soa.c", "rabia_oracle.h", "Makefile")]
     if not os.path.exists(ORACLE_SO) or any(os.path.getmtime(s) > os.path.getmtime(ORACLE_SO) for s in src):
         subprocess.run(["make", "-C", ORACLE_DIR, "build/librabia_oracle.so"], check=True,
                        capture_output=True)
@@ -63,6 +63,9 @@ def load():
     lib.or_trace.argtypes = [i, i, u64, u64, u64, u8p, u8p, u8p]
     lib.or_digest_trace.argtypes = [i, u64, u64, u64, u64p]
     lib.or_pack_planes.argtypes = [u8p, i, u64, u64, u32p]
+    lib.or_ref_step_soa.argtypes = [i, i, i, u64, u64, u64, u64, u64, u64, u32p, u64, u64, u32p,
+                                    ctypes.POINTER(OrResult), i]
+    lib.or_omp_max_threads.restype = i
     lib.or_unpack_planes.argtypes = [u32p, i, u64, u64, u8p]
     _lib = lib
     return lib
@@ -117,6 +120,20 @@ def ref_structured(n, q, self_lane, seed, rng_base, slot_base, r1, r2):
                                S, _p(dec, u8p), ctypes.byref(res))
     assert rc == 0
     return dec, res.as_dict()
+
+
+def ref_step_soa(n, q, self_lane, seed, rng_base, slot_base, planes, stride, S, max_phase=0, lc_in=0, wm_in=1,
+                 threads=0, want_out=True):
+    """The fast all-core CPU path on planar planes [(4n+1) x stride] (rabia_cpu_soa.c)."""
+    lib = load()
+    planes = np.ascontiguousarray(planes, np.uint32)
+    out = np.zeros((8, stride), np.uint32) if want_out else None
+    res = OrResult()
+    rc = lib.or_ref_step_soa(n, q, self_lane, seed, rng_base, slot_base, max_phase, lc_in, wm_in,
+                             _p(planes, u32p), stride, S, _p(out, u32p) if want_out else None,
+                             ctypes.byref(res), threads)
+    assert rc == 0
+    return out, res.as_dict()
 
 
 def digest_majority(digests, q):

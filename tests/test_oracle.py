@@ -181,3 +181,26 @@ def test_cluster_safety_and_validity():
         for v in (0, 1):
             outs = R.wmvc_cluster(n, q, fp1, 1, 0, 5, 64, 1, [[v] * n] * 50)
             assert all(o[0] == v and o[1] == 1 for o in outs)
+
+
+@pytest.mark.parametrize("n", [1, 3, 5, 9, 16])
+@pytest.mark.parametrize("S", [1, 63, 64, 65, 100_003, 300_001])
+def test_soa_cpu_path_equals_oracle(oracle, n, S):
+    """The all-core CPU baseline (rabia_cpu_soa.c) computes exactly or_ref_step:
+    outputs, counts, StdRng position, watermarks — with the VQ prefix split over
+    OpenMP chunks and a max_phase cut."""
+    from rabia_amd.engine import decode_outputs, plane_stride
+    for kind in (0, 1, 2):
+        r1, r2, _ = oracle.trace(kind, n, 31 + S, 9, S)
+        q, lane = n // 2 + 1, n // 2
+        exp, eres = oracle.ref_step(n, q, lane, 42, 55, 9, r1, r2, max_phase=9 + S // 2, lc_in=4, wm_in=9)
+        stride = plane_stride(S)
+        planes = np.zeros((4 * n + 1, stride), np.uint32)
+        planes[: 2 * n] = oracle.pack_planes(r1, stride)
+        planes[2 * n: 4 * n] = oracle.pack_planes(r2, stride)
+        out, res = oracle.ref_step_soa(n, q, lane, 42, 55, 9, planes, stride, S, max_phase=9 + S // 2, lc_in=4,
+                                       wm_in=9, threads=4)
+        got = decode_outputs(out, S)
+        for k in exp:
+            np.testing.assert_array_equal(got[k], exp[k], err_msg=k)
+        assert res == eres
