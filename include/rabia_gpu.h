@@ -180,6 +180,23 @@ int rg_shard_commit_async(rg_ctx* ctx, const rg_step_result* rows_dev, uint32_t 
                           uint64_t window_base, uint64_t window_slots, rg_step_result* result_dev,
                           void* stream);
 
+/* Follower side of a decided window (RabiaEngine::handle_decision,
+ * engine.rs:708-746): the window's decisions, as an output buffer in the context's
+ * layout (plane 6 committed, plane 7 V1), applied in ascending PhaseId order. A V1
+ * batch is applied iff its PhaseId > last_committed (engine.rs:723-728); within one
+ * window that gate is last_committed at the window's start (the context's state at
+ * call time), since every batch applied in the window is below the later slots.
+ * last_committed then advances as commit_phase does (max, refused above max_phase;
+ * state.rs:65-103), the contiguous watermark as in a phase step.
+ *  applied_dev (optional): one plane of ceil(n_slots/32) words, the applied bits;
+ *  gate_dev (optional): receives last_committed before the window — the gate
+ *    rg_kv_mark_applied_async (rabia_kv.h) takes;
+ *  result_dev (optional): n_decided = committed slots, n_v1 = batches applied. */
+int rg_follower_commit_async(rg_ctx* ctx, const uint32_t* out_dev, uint64_t n_slots,
+                             uint64_t stride_words, uint64_t slot_base, uint64_t max_phase,
+                             uint32_t* applied_dev, uint64_t* gate_dev,
+                             rg_step_result* result_dev, void* stream);
+
 /* Exchange stage: state bit = 1 iff some proposal digest is held by >= quorum
  * replicas (weak_mvc.ivy:109-128). digests_dev = [n][digest_stride] u64 (0 = no
  * proposal received), state_dev = one plane of stride_words. */
@@ -233,7 +250,8 @@ int rg_digest_trace_async(rg_ctx* ctx, uint64_t seed, uint64_t slot_base, uint64
  * a hash keyed by delivery_seed, slot, phase, round, receiver) with the common
  * coin, until all replicas decided or max_phases (<= 255).
  * states_dev: n planar planes (replica r's initial state bit), stride_words apart.
- * info_dev[s] = decision (0 V0, 1 V1, 3 not all decided) | phases << 8 |
+ * info_dev[s] = decision (0 V0, 1 V1, 3 not all decided, 2 replicas disagree — an
+ *               agreement violation that must never occur) | phases << 8 |
  *               first decision phase << 16 | coin phases << 24.
  * stats_dev (8 x u64, may be NULL): slots all decided, decided V1, sum of phases,
  * max phases, sum of coin phases, sum of first-decision phases, slots, 0. */

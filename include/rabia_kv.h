@@ -77,14 +77,20 @@ int rg_kv_destroy(rg_kv* kv);
 const char* rg_kv_last_error(const rg_kv* kv);
 
 /* Which commands to apply: apply_mask[c] = 1 iff command c belongs to a slot whose
- * decision is V1 (output plane 7 of an rg_phase_step over the same window).
+ * decision is V1 (output plane 7 of an rg_phase_step over the same window) and,
+ * when gate_dev is given, whose PhaseId slot_base + s is above *gate_dev.
+ *  gate_dev = NULL: the proposer (make_decision applies every V1 decision,
+ *                   engine.rs:641-650);
+ *  gate_dev = the follower's last_committed before the window (handle_decision
+ *             applies only if phase_id > last_committed, engine.rs:723-728; e.g. the
+ *             gate written by rg_follower_commit_async, rabia_gpu.h).
  * slot_cmd_off[n_slots + 1] = CSR offsets of each slot's batch in the command list.
  * out_dev / stride_words / tile_words = the step's output buffer and its layout
  * (rabia_gpu.h "Layout"). */
 int rg_kv_mark_applied_async(rg_kv* kv, const uint32_t* out_dev, uint64_t stride_words,
-                             uint32_t tile_words, uint64_t n_slots,
-                             const uint64_t* slot_cmd_off_dev, uint8_t* apply_mask_dev,
-                             void* stream);
+                             uint32_t tile_words, uint64_t n_slots, uint64_t slot_base,
+                             const uint64_t* gate_dev, const uint64_t* slot_cmd_off_dev,
+                             uint8_t* apply_mask_dev, void* stream);
 
 /* Apply n_cmds commands in total order. Command c's bytes are
  * data_dev[cmd_off_dev[c] .. cmd_off_dev[c+1]). apply_mask_dev may be NULL (apply

@@ -571,7 +571,9 @@ int or_wmvc_cluster(int n, int q, int fp1, uint64_t coin_seed, uint64_t epoch,
       st = nst;
       if (decided == all) o.phases = (uint8_t)p;
     }
-    if (decided == all) o.dec = (uint8_t)(decv & 1u);  /* agreement: every decider decided decv bit 0's value */
+    /* agreement (weak_mvc.ivy invariants): every replica decided the same value;
+     * a disagreement would be reported as OR_VQ (a safety violation, never seen) */
+    if (decided == all) o.dec = (uint8_t)((decv == 0 || decv == all) ? (decv & 1u) : OR_VQ);
     out[s] = o;
   }
   return 0;

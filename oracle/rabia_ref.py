@@ -151,6 +151,25 @@ def round1_votes(seed, rng_base, props, proposed, slot_base, track=True):
     return votes, k - rng_base
 
 
+def handle_decisions(values, committed, slot_base, last_committed, max_phase=0, order=None):
+    """Follower (RabiaEngine::handle_decision, engine.rs:708-746), one Decision
+    message at a time, in `order` (default ascending PhaseId): set_decision; if the
+    decision is V1 and phase_id > last_committed (engine.rs:723-728): apply_batch,
+    then commit_phase, which raises last_committed to phase_id (monotonic max) or
+    refuses it when phase_id > current_phase (state.rs:65-75) AFTER the batch was
+    applied (engine.rs:728-735). Returns (applied flags, last_committed)."""
+    S = len(values)
+    applied = [0] * S
+    lc = last_committed
+    for s in (order if order is not None else range(S)):
+        pid = slot_base + s
+        if committed[s] and values[s] and pid > lc:
+            applied[s] = 1
+            if max_phase == 0 or pid <= max_phase:
+                lc = max(lc, pid)
+    return applied, lc
+
+
 def coin(coin_key, epoch, slot, phase):
     """Common coin (build-defined)."""
     b = chacha_block(coin_key, ((phase - 1) << 40) | (slot >> 9), epoch | (1 << 63), 12)

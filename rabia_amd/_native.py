@@ -107,7 +107,8 @@ _SIGS = {
     "rg_kv_create": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.POINTER(RgKvConfig)]),
     "rg_kv_destroy": (ctypes.c_int, [vp]),
     "rg_kv_last_error": (ctypes.c_char_p, [vp]),
-    "rg_kv_mark_applied_async": (ctypes.c_int, [vp, vp, u64, u32, u64, vp, vp, vp]),
+    "rg_kv_mark_applied_async": (ctypes.c_int, [vp, vp, u64, u32, u64, u64, vp, vp, vp, vp]),
+    "rg_follower_commit_async": (ctypes.c_int, [vp, vp, u64, u64, u64, u64, vp, vp, vp, vp]),
     "rg_kv_apply_async": (ctypes.c_int, [vp, vp, vp, u64, vp, vp, vp]),
     "rg_kv_get_stats": (ctypes.c_int, [vp, ctypes.POINTER(RgKvStats)]),
     "rg_kv_dump": (ctypes.c_int, [vp, vp, vp, vp, u64]),

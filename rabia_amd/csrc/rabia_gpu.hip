@@ -491,6 +491,40 @@ int rg_shard_fixup_async(rg_ctx* ctx, uint32_t* out_dev, uint64_t n_slots, uint6
   return RG_OK;
 }
 
+int rg_follower_commit_async(rg_ctx* ctx, const uint32_t* out_dev, uint64_t n_slots, uint64_t stride_words,
+                             uint64_t slot_base, uint64_t max_phase, uint32_t* applied_dev, uint64_t* gate_dev,
+                             rg_step_result* result_dev, void* stream) {
+  if (!ctx) return fail(nullptr, RG_EINVAL, "rg_follower_commit: null context");
+  if (!out_dev || n_slots == 0) return fail(ctx, RG_EINVAL, "rg_follower_commit: bad argument");
+  if (n_slots >= (1ull << 32)) return fail(ctx, RG_EINVAL, "rg_follower_commit: n_slots must be < 2^32 per call");
+  RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
+  const uint64_t n_words = (n_slots + 31) / 32;
+  Layout lout;
+  uint64_t need;
+  if (int rc = make_layout(ctx, kOutPlanes, n_words, stride_words, &lout, &need, "rg_follower_commit")) return rc;
+  if (!ctx->fix_acc) RG_HIP(ctx, hipMalloc(&ctx->fix_acc, 4 * sizeof(unsigned long long)));
+  hipStream_t s = pick_stream(ctx, stream);
+  RG_HIP(ctx, hipMemsetAsync(ctx->fix_acc, 0, 3 * sizeof(unsigned long long), s));
+  RG_HIP(ctx, hipMemsetAsync(ctx->fix_acc + 3, 0xFF, sizeof(unsigned long long), s));
+  FollowParams f;
+  f.out = out_dev;
+  f.lout = lout;
+  f.n_slots = n_slots;
+  f.n_words = n_words;
+  f.slot_base = slot_base;
+  f.max_phase = max_phase;
+  f.state = ctx->state;
+  f.applied = applied_dev;
+  f.acc = ctx->fix_acc;
+  const uint64_t g = (n_words + 255) / 256;
+  hipLaunchKernelGGL(follower_kernel, dim3((uint32_t)(g < 2048 ? g : 2048)), dim3(256), 0, s, f);
+  hipLaunchKernelGGL(follower_finish_kernel, dim3(1), dim3(64), 0, s, f,
+                     reinterpret_cast<unsigned long long*>(gate_dev), ctx->result,
+                     reinterpret_cast<DevResult*>(result_dev));
+  RG_HIP(ctx, hipGetLastError());
+  return RG_OK;
+}
+
 int rg_shard_commit_async(rg_ctx* ctx, const rg_step_result* rows_dev, uint32_t n_shards, uint64_t window_base,
                           uint64_t window_slots, rg_step_result* result_dev, void* stream) {
   if (!ctx) return fail(nullptr, RG_EINVAL, "rg_shard_commit: null context");

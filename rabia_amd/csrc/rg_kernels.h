@@ -939,6 +939,98 @@ static __global__ void shard_commit_kernel(const DevResult* rows, uint32_t n_sha
 }
 
 // ============================================================================
+// Follower side of a decided window (handle_decision, engine.rs:708-746): the
+// window's decisions arrive as an output buffer (plane 6 committed, plane 7 V1);
+// in ascending PhaseId order the one gate is "PhaseId > last_committed at the
+// window's start" (a batch decided inside the window only raises last_committed
+// to its own id, below every later slot), so applied = V1 & (id > L_in), and
+// last_committed = max(L_in, applied ids <= max_phase) (commit_phase, state.rs:65-103).
+// ============================================================================
+struct FollowParams {
+  const uint32_t* out;
+  Layout lout;
+  uint64_t n_slots, n_words, slot_base, max_phase;
+  DevState* state;
+  uint32_t* applied;          // optional: one plane of n_words words
+  unsigned long long* acc;    // [4] applied, committed, max applied id + 1 (<= max_phase), min uncommitted id
+};
+
+static __global__ __launch_bounds__(256) void follower_kernel(FollowParams f) {
+  const unsigned long long lc = f.state->last_committed;
+  unsigned long long app = 0, com = 0, mx = 0, mn = ~0ull;
+  for (uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x; w < f.n_words; w += (uint64_t)gridDim.x * 256) {
+    const uint64_t b = f.lout.base(w);
+    const uint32_t vm = valid_mask(w, f.n_words, f.n_slots);
+    const uint32_t committed = f.out[b + 6 * f.lout.pstride] & vm, v1 = f.out[b + 7 * f.lout.pstride] & vm;
+    const uint64_t first = f.slot_base + 32 * w;  // PhaseId of bit 0
+    uint32_t gate = ~0u;                          // bits with PhaseId > lc
+    if (first <= lc) gate = lc - first >= 31 ? 0u : ~((2u << (lc - first)) - 1u);
+    const uint32_t ap = v1 & gate;
+    if (f.applied) f.applied[w] = ap;
+    app += __builtin_popcount(ap);
+    com += __builtin_popcount(committed);
+    const uint32_t apl = ap & phase_limit_mask(f.slot_base, w, f.max_phase);
+    if (apl) {
+      const unsigned long long id1 = first + (31u - __builtin_clz(apl)) + 1u;
+      mx = id1 > mx ? id1 : mx;
+    }
+    const uint32_t und = ~committed & vm;
+    if (und) {
+      const unsigned long long id = first + __builtin_ctz(und);
+      mn = id < mn ? id : mn;
+    }
+  }
+  __shared__ unsigned long long red[4][4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  app = wave_sum64(app);
+  com = wave_sum64(com);
+  mx = wave_max64(mx);
+  mn = wave_min64(mn);
+  if (lane == 0) { red[wave][0] = app; red[wave][1] = com; red[wave][2] = mx; red[wave][3] = mn; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; w++) {
+      app += red[w][0]; com += red[w][1];
+      mx = red[w][2] > mx ? red[w][2] : mx;
+      mn = red[w][3] < mn ? red[w][3] : mn;
+    }
+    if (app) atomicAdd(f.acc + 0, app);
+    if (com) atomicAdd(f.acc + 1, com);
+    if (mx) atomicMax(f.acc + 2, mx);
+    if (mn != ~0ull) atomicMin(f.acc + 3, mn);
+  }
+}
+
+static __global__ void follower_finish_kernel(FollowParams f, unsigned long long* gate_out, DevResult* res_ctx,
+                                              DevResult* res_user) {
+  if (threadIdx.x != 0) return;
+  DevState s = *f.state;
+  DevResult r;
+  r.n_slots = f.n_slots;
+  r.n_v1 = f.acc[0];
+  r.n_decided = f.acc[1];
+  r.n_pending_r1 = 0;
+  r.n_draws = 0;
+  if (gate_out) *gate_out = s.last_committed;
+  unsigned long long lc = s.last_committed;
+  if (f.acc[2] && f.acc[2] - 1 > lc) lc = f.acc[2] - 1;
+  const unsigned long long end = f.slot_base + f.n_slots;
+  const unsigned long long fu = f.acc[3] < end ? f.acc[3] : end;
+  unsigned long long wm = s.commit_watermark;
+  if (f.slot_base <= wm && wm < fu) wm = fu;
+  r.last_committed_max = lc;
+  r.first_undecided = fu;
+  r.rng_next = s.rng_next;
+  r.commit_watermark = wm;
+  r.flags = 0;
+  s.last_committed = lc;
+  s.commit_watermark = wm;
+  *f.state = s;
+  *res_ctx = r;
+  if (res_user) *res_user = r;
+}
+
+// ============================================================================
 // WMVC phase step, one replica's view (weak_mvc.ivy:129-191).
 // ============================================================================
 __device__ __forceinline__ uint32_t coin_word(const Key& key, uint64_t stream, uint64_t phase,
@@ -1524,7 +1616,9 @@ __global__ __launch_bounds__(256) void wmvc_cluster_kernel(const uint32_t* state
       st = nst;
       if (decided == kAll) phases = p;
     }
-    const uint32_t dec = decided == kAll ? (decv & 1u) : kCodeNone;
+    // all replicas decided: their common value (kCodeVQ = they disagree, an agreement
+    // violation of weak_mvc.ivy the property tests assert never occurs)
+    const uint32_t dec = decided == kAll ? ((decv == 0 || decv == kAll) ? (decv & 1u) : kCodeVQ) : kCodeNone;
     info[s] = dec | (phases << 8) | (first << 16) | (coins << 24);
     acc[0] += decided == kAll;
     acc[1] += dec == kCodeV1;
@@ -1673,7 +1767,7 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
     const bool all = decided == kAll;
     if (all || p >= max_phases) {
       const uint32_t phases = all ? p : 0u;
-      const uint32_t dec = all ? (decv & 1u) : kCodeNone;
+      const uint32_t dec = all ? ((decv == 0 || decv == kAll) ? (decv & 1u) : kCodeVQ) : kCodeNone;
       info[s] = dec | (phases << 8) | (first << 16) | (coins << 24);
       acc[0] += all;
       acc[1] += dec == kCodeV1;

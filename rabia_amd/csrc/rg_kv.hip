@@ -515,10 +515,15 @@ __global__ void kv_finish_kernel(KvCounters* k, const unsigned long long* part, 
 }
 
 // ---- mark applied commands from the phase step's decision plane -----------------
+// gate (follower, handle_decision engine.rs:723-728): a V1 slot's batch is applied
+// only if its PhaseId is above last_committed (*gate); NULL = the proposer's
+// make_decision, which applies every V1 decision (engine.rs:641-650).
 __global__ void kv_mark_kernel(const uint32_t* out, uint64_t stride, uint32_t tile_words, uint64_t n_slots,
-                               const uint64_t* slot_off, uint8_t* mask) {
+                               uint64_t slot_base, const unsigned long long* gate, const uint64_t* slot_off,
+                               uint8_t* mask) {
   const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n_slots) return;
+  const unsigned long long lc = gate ? *gate : 0ull;
   const uint64_t w = s >> 5;
   uint64_t idx;
   if (tile_words) {
@@ -527,7 +532,7 @@ __global__ void kv_mark_kernel(const uint32_t* out, uint64_t stride, uint32_t ti
   } else {
     idx = 7 * stride + w;
   }
-  const uint8_t v = (uint8_t)((out[idx] >> (s & 31)) & 1u);
+  const uint8_t v = (uint8_t)(((out[idx] >> (s & 31)) & 1u) && (!gate || slot_base + s > lc));
   for (uint64_t c = slot_off[s]; c < slot_off[s + 1]; c++) mask[c] = v;
 }
 
@@ -715,8 +720,8 @@ int rg_kv_destroy(rg_kv* kv) {
 const char* rg_kv_last_error(const rg_kv* kv) { return kv ? kv->err.c_str() : g_kv_err.c_str(); }
 
 int rg_kv_mark_applied_async(rg_kv* kv, const uint32_t* out_dev, uint64_t stride_words, uint32_t tile_words,
-                             uint64_t n_slots, const uint64_t* slot_cmd_off_dev, uint8_t* apply_mask_dev,
-                             void* stream) {
+                             uint64_t n_slots, uint64_t slot_base, const uint64_t* gate_dev,
+                             const uint64_t* slot_cmd_off_dev, uint8_t* apply_mask_dev, void* stream) {
   if (!kv) return kfail(nullptr, -1, "rg_kv_mark_applied_async: null store");
   if (!n_slots) return 0;
   if (!out_dev || !slot_cmd_off_dev || !apply_mask_dev) return kfail(kv, -1, "rg_kv_mark_applied_async: null buffer");
@@ -724,7 +729,8 @@ int rg_kv_mark_applied_async(rg_kv* kv, const uint32_t* out_dev, uint64_t stride
   if (!tile_words && stride_words < (n_slots + 31) / 32) return kfail(kv, -1, "rg_kv_mark_applied_async: stride_words too small");
   hipStream_t s = stream ? (hipStream_t)stream : kv->stream;
   hipLaunchKernelGGL(kv_mark_kernel, dim3((uint32_t)((n_slots + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
-                     out_dev, stride_words, tile_words, n_slots, slot_cmd_off_dev, apply_mask_dev);
+                     out_dev, stride_words, tile_words, n_slots, slot_base,
+                     reinterpret_cast<const unsigned long long*>(gate_dev), slot_cmd_off_dev, apply_mask_dev);
   KV_HIP(kv, hipGetLastError());
   return 0;
 }

@@ -273,6 +273,14 @@ class PhaseEvaluator:
         N.check(self.lib.rg_shard_commit_async(self.ctx, rows_ptr, n_shards, window_base, window_slots,
                                                result_ptr or None, stream or None), self.ctx)
 
+    def follower_commit_async(self, out_ptr, n_slots, stride, slot_base, applied_ptr=0, gate_ptr=0, result_ptr=0,
+                              max_phase=0, stream=0):
+        """handle_decision over a decided window (engine.rs:708-746): applied = V1 slots
+        above last_committed; last_committed / watermark advance."""
+        N.check(self.lib.rg_follower_commit_async(self.ctx, out_ptr, n_slots, stride, slot_base, max_phase,
+                                                  applied_ptr or None, gate_ptr or None, result_ptr or None,
+                                                  stream or None), self.ctx)
+
     def digest_majority_async(self, digests_ptr, digest_stride, state_ptr, n_slots, stream=0):
         N.check(self.lib.rg_digest_majority_async(self.ctx, digests_ptr, digest_stride, state_ptr,
                                                   n_slots, stream or None), self.ctx)

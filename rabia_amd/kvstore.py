@@ -126,9 +126,12 @@ class DeviceKVStore:
                                               results_ptr, stream or None), self.kv)
 
     def mark_applied_async(self, out_ptr, stride_words, tile_words, n_slots, slot_cmd_off_ptr, mask_ptr,
-                           stream=0):
+                           stream=0, slot_base=1, gate_ptr=0):
+        """gate_ptr = 0: proposer (every V1 slot); else a device u64 last_committed:
+        follower (V1 slots with PhaseId above it, engine.rs:723-728)."""
         N.check_kv(self.lib.rg_kv_mark_applied_async(self.kv, out_ptr, stride_words, tile_words, n_slots,
-                                                     slot_cmd_off_ptr, mask_ptr, stream or None), self.kv)
+                                                     slot_base, gate_ptr or None, slot_cmd_off_ptr, mask_ptr,
+                                                     stream or None), self.kv)
 
     def trace_async(self, seed, n_cmds, key_space, data_ptr, data_cap, off_ptr, stream=0):
         N.check_kv(self.lib.rg_kv_trace_async(self.kv, seed, n_cmds, key_space, data_ptr, data_cap, off_ptr,

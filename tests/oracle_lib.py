@@ -32,7 +32,7 @@ _lib = None
 
 
 def build():
-    src = [os.path.join(ORACLE_DIR, f) for f in ("rabia_oracle.c", "rabia_cpu_soa.c", "rabia_oracle.h", "Makefile")]
+    src = [os.path.join(ORACLE_DIR, f) for f in ("rabia_oracle.c", "rabia_cpu_soa.c", "kvstore_ref.c", "rabia_oracle.h", "Makefile")]
     if not os.path.exists(ORACLE_SO) or any(os.path.getmtime(s) > os.path.getmtime(ORACLE_SO) for s in src):
         subprocess.run(["make", "-C", ORACLE_DIR, "build/librabia_oracle.so"], check=True,
                        capture_output=True)
@@ -66,6 +66,12 @@ def load():
     lib.or_ref_step_soa.argtypes = [i, i, i, u64, u64, u64, u64, u64, u64, u32p, u64, u64, u32p,
                                     ctypes.POINTER(OrResult), i]
     lib.or_omp_max_threads.restype = i
+    lib.or_kv_create.restype = ctypes.c_void_p
+    lib.or_kv_create.argtypes = [u64, u64, i]
+    lib.or_kv_destroy.argtypes = [ctypes.c_void_p]
+    lib.or_kv_apply.argtypes = [ctypes.c_void_p, u8p, u64p, u64, u8p, u8p]
+    lib.or_kv_stats.argtypes = [ctypes.c_void_p, u64p]
+    lib.or_kv_dump.argtypes = [ctypes.c_void_p, u64p, u8p, u64p, u8p, u32p]
     lib.or_unpack_planes.argtypes = [u32p, i, u64, u64, u8p]
     _lib = lib
     return lib
@@ -224,3 +230,54 @@ def cluster_trace(n, seed, slot_base, S):
     st = np.zeros((S, n), np.uint8)
     lib.or_cluster_trace(n, seed, slot_base, S, _p(st, u8p))
     return st
+
+
+class KVStoreC:
+    """oracle/kvstore_ref.c: the sequential C restatement of the kvstore apply
+    (same semantics as oracle/kvstore_ref.py, pinned by the reference's kvstore
+    test outcomes). Used as the full-size checker and the C4 CPU baseline."""
+
+    def __init__(self, max_keys=0, max_value_size=0, enable_notifications=True):
+        self.lib = load()
+        self.h = self.lib.or_kv_create(max_keys, max_value_size, 1 if enable_notifications else 0)
+        assert self.h
+
+    def close(self):
+        if self.h:
+            self.lib.or_kv_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def apply(self, data, offs, mask=None):
+        """data: uint8 bytes of all commands, offs: uint64[n+1]; -> uint8 results[n]."""
+        data = np.ascontiguousarray(data, np.uint8)
+        offs = np.ascontiguousarray(offs, np.uint64)
+        n = offs.size - 1
+        res = np.zeros(max(n, 1), np.uint8)
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+        rc = self.lib.or_kv_apply(self.h, _p(data if data.size else np.zeros(1, np.uint8), u8p), _p(offs, u64p), n,
+                                  _p(m, u8p) if m is not None else None, _p(res, u8p))
+        assert rc == 0
+        return res[:n]
+
+    def stats(self):
+        out = np.zeros(5, np.uint64)
+        self.lib.or_kv_stats(self.h, _p(out, u64p))
+        return {"live_keys": int(out[0]), "version": int(out[1]), "total_operations": int(out[2]),
+                "key_bytes": int(out[3]), "value_bytes": int(out[4])}
+
+    def state(self):
+        """{"data": {key: (value, entry version)}, "version"} like kvstore_ref.KVStoreRef.state()."""
+        st = self.stats()
+        n = st["live_keys"]
+        ko = np.zeros(n + 1, np.uint64)
+        vo = np.zeros(n + 1, np.uint64)
+        kb = np.zeros(max(st["key_bytes"], 1), np.uint8)
+        vb = np.zeros(max(st["value_bytes"], 1), np.uint8)
+        ver = np.zeros(max(n, 1), np.uint32)
+        self.lib.or_kv_dump(self.h, _p(ko, u64p), _p(kb, u8p), _p(vo, u64p), _p(vb, u8p), _p(ver, u32p))
+        kbytes, vbytes = kb.tobytes(), vb.tobytes()
+        data = {kbytes[ko[i]:ko[i + 1]]: (vbytes[vo[i]:vo[i + 1]], int(ver[i])) for i in range(n)}
+        return {"data": data, "version": st["version"]}

@@ -1,0 +1,164 @@
+"""The BASELINE.json configs at their full sizes on the GPU (C2's 2^20 window is in
+test_gpu_parity.py, C5 over 8 shards in test_shard_ref.py):
+
+  C3  5 replicas x 2^24 slots, adversarial split, Weak-MVC to termination (cluster view)
+  C4  7 replicas x 2^22 slots: digest exchange -> REF sweep -> kvstore apply of the V1 batches
+  C5  9 replicas x 2^26 slots, one REF sweep (the bench's slot-tiled layout)
+
+Checked through size-independent properties (counts = plane popcounts, agreement,
+termination bounds, stats = info sums), the oracle on slices (every slot of C3 is
+independent; REF slices take the prefix-derived draw offset), full-size oracle runs
+where the C oracle finishes in seconds (C4's 2^22 REF sweep and digests, and the
+C restatement of the kvstore apply), and window-split equivalence."""
+import numpy as np
+import pytest
+
+from rabia_amd import _native as N
+from rabia_amd.engine import PhaseEvaluator, decode_outputs, from_tiled, plane_stride
+
+pytestmark = pytest.mark.gpu
+
+
+def torch_cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def test_c3_full_size_cluster(oracle):
+    torch = torch_cuda()
+    n, S, q, fp1, maxp = 5, 1 << 24, 3, 3, 32
+    stride = plane_stride(S)
+    states = torch.zeros(n * stride, dtype=torch.int32, device="cuda")
+    info = torch.zeros(S, dtype=torch.int32, device="cuda")
+    stats = torch.zeros(8, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    with PhaseEvaluator(n, mode="wmvc", coin_seed=7, epoch=3) as ev:
+        ev.cluster_trace_async(42, 1, S, stride, states.data_ptr())
+        ev.wmvc_cluster_async(states.data_ptr(), stride, S, 1, 99, maxp, info.data_ptr(), stats.data_ptr())
+        ev.sync()
+    got = info.cpu().numpy().view(np.uint32)
+    dec, phases = got & 255, (got >> 8) & 255
+    first, coins = (got >> 16) & 255, got >> 24
+    assert not (dec == 2).any(), "agreement violated"
+    assert ((dec == 3) == (phases == 0)).all()
+    assert phases.max() <= maxp and (first <= phases).all() | (phases == 0).all()
+    assert ((first >= 1) | (dec == 3)).all()
+    assert (dec != 3).mean() > 0.999  # the coin terminates the adversarial split fast
+    sv = stats.cpu().numpy().view(np.uint64)
+    assert sv[0] == (dec != 3).sum() and sv[1] == (dec == 1).sum()
+    assert sv[2] == phases.sum() and sv[3] == phases.max() and sv[4] == coins.sum()
+    assert sv[5] == first.sum() and sv[6] == S
+    # the coin makes both values reachable; several phases are needed on average
+    assert 0.3 < (dec == 1).mean() < 0.7 and phases.mean() > 1.5
+    for lo in (0, S // 2 + 12345, S - 30000):
+        cnt = 30000
+        st = oracle.cluster_trace(n, 42, 1 + lo, cnt)
+        exp = oracle.wmvc_cluster(n, q, fp1, 7, 3, 99, maxp, 1 + lo, st)
+        np.testing.assert_array_equal(got[lo:lo + cnt], exp, err_msg=f"slice at {lo}")
+
+
+def test_c4_full_size_pipeline(oracle):
+    torch = torch_cuda()
+    from rabia_amd.kvstore import DeviceKVStore, KVStoreConfig
+    n, S, ks = 7, 1 << 22, 1 << 20
+    q = n // 2 + 1
+    stride = plane_stride(S)
+    votes = torch.zeros((4 * n + 1) * stride, dtype=torch.int32, device="cuda")
+    out = torch.zeros(8 * stride, dtype=torch.int32, device="cuda")
+    digests = torch.zeros(n * S, dtype=torch.int64, device="cuda")
+    slot_off = torch.arange(S + 1, dtype=torch.int64, device="cuda")  # one command per slot
+    cmd_data = torch.zeros(68 * S, dtype=torch.uint8, device="cuda")
+    cmd_off = torch.zeros(S + 1, dtype=torch.int64, device="cuda")
+    mask = torch.zeros(S, dtype=torch.uint8, device="cuda")
+    res = torch.zeros(S, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    with PhaseEvaluator(n, self_lane=n - 1, seed=42) as ev, DeviceKVStore(KVStoreConfig(max_keys=4 * ks)) as kv:
+        ev.trace_generate_async(N.RG_TRACE_AGREE90, 5, 1, S, stride, votes.data_ptr())
+        ev.digest_trace_async(5, 1, S, S, digests.data_ptr())
+        kv.trace_async(1, S, ks, cmd_data.data_ptr(), cmd_data.numel(), cmd_off.data_ptr())
+        ev.sync()
+        kv.sync()
+        ev.digest_majority_async(digests.data_ptr(), S, votes.data_ptr() + 4 * 4 * n * stride, S)
+        ev.phase_step_async(votes.data_ptr(), out.data_ptr(), S, stride, slot_base=1)
+        ev.sync()
+        kv.mark_applied_async(out.data_ptr(), stride, 0, S, slot_off.data_ptr(), mask.data_ptr())
+        kv.apply_async(cmd_data.data_ptr(), cmd_off.data_ptr(), S, mask.data_ptr(), res.data_ptr())
+        kv.sync()
+        stats = kv.stats()
+        # exchange stage vs the oracle over all 2^22 slots
+        dg = oracle.digest_trace(n, 5, 1, S)
+        np.testing.assert_array_equal(digests.view(n, S).cpu().numpy().view(np.uint64), dg)
+        st_bits = np.unpackbits(votes.view(4 * n + 1, stride)[4 * n].cpu().numpy().view(np.uint8),
+                                bitorder="little")[:S]
+        np.testing.assert_array_equal(st_bits, oracle.digest_majority(dg, q))
+        del dg
+        # REF sweep vs the oracle over all 2^22 slots
+        r1, r2, _ = oracle.trace(1, n, 5, 1, S)
+        exp, eres = oracle.ref_step(n, q, n - 1, 42, 0, 1, r1, r2)
+        del r1, r2
+        got = decode_outputs(out.view(8, stride).cpu().numpy().view(np.uint32), S)
+        for k in exp:
+            np.testing.assert_array_equal(got[k], exp[k], err_msg=k)
+        # the apply: every command's result and the final store vs the C restatement
+        m = mask.cpu().numpy()
+        np.testing.assert_array_equal(m, exp["value"])
+        data = cmd_data.cpu().numpy()
+        offs = cmd_off.cpu().numpy().view(np.uint64)
+        ref = oracle.KVStoreC(max_keys=4 * ks)
+        exp_res = ref.apply(data[: int(offs[-1])], offs, m)
+        np.testing.assert_array_equal(res.cpu().numpy(), exp_res)
+        rs = ref.stats()
+        assert stats["live_keys"] == rs["live_keys"] and stats["version"] == rs["version"]
+        assert stats["total_operations"] == rs["total_operations"] and stats["flags"] == 0
+        got_state, exp_state = kv.get_state(), ref.state()
+        assert got_state["version"] == exp_state["version"]
+        assert got_state["data"] == exp_state["data"]
+
+
+def test_c5_full_size_step(oracle):
+    torch = torch_cuda()
+    n, S, T = 9, 1 << 26, 1024
+    q = n // 2 + 1
+    nw = S // 32
+    P = 4 * n + 1
+    votes = torch.zeros((nw // T) * P * T, dtype=torch.int32, device="cuda")
+    out1 = torch.zeros((nw // T) * 8 * T, dtype=torch.int32, device="cuda")
+    out2 = torch.zeros_like(out1)
+    torch.cuda.synchronize()
+    with PhaseEvaluator(n, self_lane=n - 1, seed=42, tile_words=T) as ev:
+        ev.trace_generate_async(N.RG_TRACE_AGREE90, 11, 1, S, T, votes.data_ptr())
+        ev.phase_step_async(votes.data_ptr(), out1.data_ptr(), S, T, slot_base=1, max_phase=S - 1000)
+        res = ev.last_result()
+        st1 = ev.get_state()
+    planes = from_tiled(out1.cpu().numpy().view(np.uint32), 8, nw, T, nw)
+    dec = decode_outputs(planes, S)
+    del planes
+    assert res["n_decided"] == int(dec["committed"].sum()) and res["n_v1"] == int(dec["value"].sum())
+    assert res["n_draws"] == int((dec["r1"] == 2).sum()) == st1["rng_next"] > 0
+    assert res["n_pending_r1"] == int((dec["r1"] == 3).sum())
+    assert ((dec["dec"] <= 1) == (dec["committed"] == 1)).all()
+    assert ((dec["dec"] == 1) == (dec["value"] == 1)).all()
+    ids_v1 = np.nonzero(dec["value"][: S - 1000])[0]
+    assert res["last_committed_max"] == int(ids_v1[-1]) + 1   # commit_phase refuses ids above max_phase
+    und = np.nonzero(dec["committed"] == 0)[0]
+    assert res["first_undecided"] == int(und[0]) + 1 == res["commit_watermark"]
+    for lo in (0, S // 3, S - 8192):
+        k0 = int((dec["r1"][:lo] == 2).sum())
+        r1, r2, _ = oracle.trace(1, n, 11, 1 + lo, 8192)
+        exp, _ = oracle.ref_step(n, q, n - 1, 42, k0, 1 + lo, r1, r2)
+        for k in exp:
+            np.testing.assert_array_equal(dec[k][lo:lo + 8192], exp[k], err_msg=f"{k} at {lo}")
+    del dec
+    # the same 2^26 slots as 4 windows of 2^24 on a fresh context (tiled offsets)
+    with PhaseEvaluator(n, self_lane=n - 1, seed=42, tile_words=T) as ev:
+        qw = nw // 4
+        for i in range(4):
+            t0 = i * qw // T
+            ev.phase_step_async(votes.data_ptr() + 4 * t0 * P * T, out2.data_ptr() + 4 * t0 * 8 * T, S // 4, T,
+                                slot_base=1 + i * (S // 4), max_phase=S - 1000)
+        st2 = ev.get_state()
+    assert torch.equal(out1, out2)
+    assert st1["rng_next"] == st2["rng_next"] and st1["last_committed"] == st2["last_committed"]
+    assert st1["commit_watermark"] == st2["commit_watermark"]

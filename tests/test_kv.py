@@ -256,3 +256,113 @@ def test_gpu_c4_pipeline_phase_step_then_apply(oracle):
         exp = R.apply_decided(ref, blobs, slot_off, applied)
         assert res.cpu().numpy().tolist() == exp
         _check_state(dev, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lc_in_frac,max_frac", [(0.0, 0.0), (0.5, 0.0), (0.3, 0.7), (1.2, 0.0)])
+def test_gpu_follower_gate_then_apply(oracle, lc_in_frac, max_frac):
+    """a11: a follower applies a decided window's V1 batches only above its
+    last_committed (handle_decision, engine.rs:723-728) — including a window
+    evaluated after a later commit (last_committed inside or past the window) —
+    and advances last_committed like commit_phase; vs the message-at-a-time
+    restatement (oracle/rabia_ref.py:handle_decisions) and kvstore_ref."""
+    import torch
+    import rabia_ref as P
+    from rabia_amd.engine import PhaseEvaluator, PhaseWindow, decode_outputs
+    n, S, base = 7, 20_011, 101
+    r1, r2, _ = oracle.trace(1, n, 5, base, S)
+    lc_in = int(base + lc_in_frac * S) if lc_in_frac else 0
+    mp = int(base + max_frac * S) if max_frac else 0
+    rng = random.Random(7)
+    counts = [rng.randrange(0, 3) for _ in range(S)]
+    slot_off = np.zeros(S + 1, np.uint64)
+    slot_off[1:] = np.cumsum(counts)
+    blobs = random_blobs(rng, int(slot_off[-1]), 500, edge=False)
+    with PhaseEvaluator(n, self_lane=6, seed=9) as prop:   # the proposer decided the window
+        out, _ = prop.phase_step_host(PhaseWindow.from_codes(r1, r2, slot_base=base))
+    dec = decode_outputs(out, S)
+    exp_app, exp_lc = P.handle_decisions(dec["value"].tolist(), dec["committed"].tolist(), base, lc_in, mp)
+    stride = out.shape[1]
+    out_d = torch.from_numpy(out.view(np.int32).copy()).cuda()
+    applied = torch.zeros(stride, dtype=torch.int32, device="cuda")
+    gate = torch.zeros(1, dtype=torch.int64, device="cuda")
+    res = torch.zeros(10, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    with PhaseEvaluator(n, self_lane=2, seed=9) as fol, _store() as dev:
+        fol.set_state(last_committed=lc_in, commit_watermark=base)
+        fol.follower_commit_async(out_d.data_ptr(), S, stride, base, applied.data_ptr(), gate.data_ptr(),
+                                  res.data_ptr(), max_phase=mp)
+        fol.sync()
+        st = fol.get_state()
+        bits = np.unpackbits(applied.cpu().numpy().view(np.uint8), bitorder="little")[:S]
+        np.testing.assert_array_equal(bits, np.array(exp_app, np.uint8))
+        assert st["last_committed"] == exp_lc and int(gate.cpu()[0]) == lc_in
+        r = res.cpu().numpy().view(np.uint64)
+        assert int(r[2]) == sum(exp_app) and int(r[1]) == int(dec["committed"].sum())
+        assert int(r[5]) == exp_lc
+        # the follower's kv apply: only the applied slots' batches
+        from rabia_amd.kvstore import pack_commands
+        data, offs = pack_commands(blobs)
+        d = torch.from_numpy(data.copy()).cuda()
+        o = torch.from_numpy(offs.view(np.int64)).cuda()
+        so = torch.from_numpy(slot_off.view(np.int64)).cuda()
+        mask = torch.empty(len(blobs), dtype=torch.uint8, device="cuda")
+        kres = torch.empty(len(blobs), dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        dev.mark_applied_async(out_d.data_ptr(), stride, 0, S, so.data_ptr(), mask.data_ptr(), 0, slot_base=base,
+                               gate_ptr=gate.data_ptr())
+        dev.apply_async(d.data_ptr(), o.data_ptr(), len(blobs), mask.data_ptr(), kres.data_ptr(), 0)
+        dev.sync()
+        ref = R.KVStoreRef()
+        exp = R.apply_decided(ref, blobs, slot_off, [s_ for s_ in range(S) if exp_app[s_]])
+        assert kres.cpu().numpy().tolist() == exp
+        _check_state(dev, ref)
+
+
+def test_follower_restatement_skips_late_lower_phases():
+    """The literal handler in arrival order skips a lower phase decided after a
+    higher one (engine.rs:727); in ascending order only phases <= the starting
+    last_committed are skipped — the closed form the device uses."""
+    import rabia_ref as P
+    vals, com = [1, 1, 1, 0, 1], [1, 1, 1, 1, 1]
+    app, lc = P.handle_decisions(vals, com, 10, 0, order=[2, 0, 1, 3, 4])
+    assert app == [0, 0, 1, 0, 1] and lc == 14
+    app, lc = P.handle_decisions(vals, com, 10, 11)
+    assert app == [0, 0, 1, 0, 1] and lc == 14
+    app, lc = P.handle_decisions(vals, com, 10, 0, max_phase=12)
+    assert app == [1, 1, 1, 0, 1] and lc == 12   # 14 applied, its commit_phase refused (state.rs:70-75)
+
+
+def _packed(blobs):
+    offs = np.zeros(len(blobs) + 1, np.uint64)
+    offs[1:] = np.cumsum([len(b) for b in blobs])
+    return np.frombuffer(b"".join(blobs), np.uint8), offs
+
+
+def test_c_restatement_equals_python_restatement(oracle):
+    """oracle/kvstore_ref.c (the full-size checker and C4 CPU baseline) == the
+    Python restatement pinned by the reference's own test outcomes: the golden
+    cases, random mixed batches with every edge case, StoreFull, masks."""
+    for case in golden_cases():
+        blobs = [blob(c) for c in case["commands"]]
+        data, offs = _packed(blobs)
+        c = oracle.KVStoreC(max_keys=case.get("max_keys", 0), max_value_size=case.get("max_value_size", 0))
+        got = c.apply(data, offs).tolist()
+        ref = R.KVStoreRef(max_keys=case.get("max_keys", R.DEFAULT_MAX_KEYS),
+                           max_value_size=case.get("max_value_size", R.DEFAULT_MAX_VALUE))
+        assert got == ref.apply_commands(blobs), case.get("name")
+        assert c.state() == ref.state()
+    rng = random.Random(5)
+    for trial in range(6):
+        blobs = random_blobs(rng, 5000, 50 + 400 * trial)
+        data, offs = _packed(blobs)
+        mask = np.array([rng.random() < 0.8 for _ in blobs], np.uint8) if trial % 2 else None
+        mk = 40 if trial == 3 else 0
+        c = oracle.KVStoreC(max_keys=mk, max_value_size=64)
+        ref = R.KVStoreRef(max_keys=mk or R.DEFAULT_MAX_KEYS, max_value_size=64)
+        got = c.apply(data, offs, mask).tolist()
+        exp = [ref.apply_data(b) if mask is None or mask[i] else R.NOT_APPLIED for i, b in enumerate(blobs)]
+        assert got == exp
+        assert c.state() == ref.state()
+        st = c.stats()
+        assert st["total_operations"] == ref.total_operations and st["live_keys"] == len(ref.data)
