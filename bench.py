@@ -65,7 +65,8 @@ def parse():
                     help="threads of the all-core CPU baseline (0: OMP_NUM_THREADS, else min(cpus, 16))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_c2.json"))
-    ap.add_argument("--config", choices=["c2", "c5"], default="c2",
+    ap.add_argument("--c3-slots", type=int, default=1 << 24, help="C3: slots per step, all ranks")
+    ap.add_argument("--config", choices=["c2", "c3", "c5"], default="c2",
                     help="c2: the headline (weak scaling); c5: 9 replicas x 2^26 slots per step split over the "
                          "ranks (strong scaling) with the decision bitmaps all-gathered every step")
     ap.add_argument("--c5-windows", type=int, default=64, help="C5: 2^20-slot windows per step, all ranks")
@@ -355,6 +356,80 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, bitmaps):
             "stream": comp}
 
 
+# ---------------------------------------------------------------------------
+# C3 (BASELINE.json configs[2]): 5 replicas x 2^24 slots, adversarial split,
+# Weak-MVC to termination with the common coin, sharded over the GPUs. The coin is
+# keyed by the GLOBAL slot id, so the shards need no data-path exchange; the
+# per-shard statistics and decided/V1 bitmaps are all-gathered every step.
+# ---------------------------------------------------------------------------
+def run_c3(a, world, rank, dist):
+    from rabia_amd import shard
+    n, total = 5, a.c3_slots
+    start, S = shard.shard_range(total, world, rank, align=128)
+    stride = ((S + 127) // 128) * 4
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    sp = stream.cuda_stream
+    ev = PhaseEvaluator(n, mode="wmvc", coin_seed=SEED, epoch=1)
+    states = torch.empty(n * stride, dtype=torch.int32, device="cuda")
+    info = torch.empty(max(S, 1), dtype=torch.int32, device="cuda")
+    nw = (S + 31) // 32
+    n_total = a.warmup + a.steps
+    stats = torch.zeros((n_total, 8), dtype=torch.int64, device="cuda")
+    bm = torch.zeros((n_total, 2, nw), dtype=torch.int32, device="cuda")
+    g_stats = torch.zeros((n_total, world, 8), dtype=torch.int64, device="cuda")
+    g_bm = torch.zeros((n_total, world, 2, nw), dtype=torch.int32, device="cuda")
+    ev.cluster_trace_async(SEED, 1 + start, S, stride, states.data_ptr(), sp)
+    torch.cuda.synchronize()
+    gather = make_gather(dist, a.backend) if world > 1 else None
+    kern = []
+
+    def step(t, evs=None):
+        if evs is not None:
+            evs[0].record(stream)
+        ev.wmvc_cluster_async(states.data_ptr(), stride, S, 1 + start, 99, 32, info.data_ptr(),
+                              stats[t].data_ptr(), sp)
+        if evs is not None:
+            evs[1].record(stream)
+        ev.cluster_bitmap_async(info.data_ptr(), S, bm[t, 0].data_ptr(), bm[t, 1].data_ptr(), sp)
+        if gather is not None:
+            gather(g_stats[t], stats[t])
+            gather(g_bm[t], bm[t])
+
+    for t in range(a.warmup):
+        step(t)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    t_begin, t_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t_begin.record(stream)
+    for k in range(a.steps):
+        step(a.warmup + k, evs[k])
+    t_end.record(stream)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    total_ms = t_begin.elapsed_time(t_end)
+    kern_ms = float(np.mean([b.elapsed_time(e) for b, e in evs]))
+    rows = (g_stats if world > 1 else stats[:, None, :]).cpu().numpy().view(np.uint64)
+    decided = 0
+    for t in range(a.warmup, n_total):
+        g = shard.combine_cluster(rows[t].tolist())
+        assert g["slots"] == total
+        decided += g["all_decided"]
+        if world > 1:  # the gathered decided bitmaps carry the folded count
+            pop = int(np.unpackbits(g_bm[t, :, 0].cpu().numpy().view(np.uint8)).sum())
+            assert pop == g["all_decided"], (pop, g["all_decided"])
+    if dist is not None:
+        tm = torch.tensor([total_ms, kern_ms], dtype=torch.float64, device="cuda" if a.backend == "nccl" else "cpu")
+        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+        total_ms, kern_ms = float(tm[0]), float(tm[1])
+    last = shard.combine_cluster(rows[n_total - 1].tolist())
+    return {"total_ms": total_ms, "kern_ms": kern_ms, "decided": decided, "ev": ev, "S": S, "total": total,
+            "mean_phases": last["sum_phases"] / max(last["all_decided"], 1), "max_phases": last["max_phases"]}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -370,6 +445,39 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group("gloo")
+    if a.config == "c3":
+        r = run_c3(a, world, rank, dist)
+        if rank == 0:
+            # bytes the cluster kernels move per slot: 5 initial-state bits read, the u32 info word
+            # written, the u32 read + 2 bitmap bits written by the bitmap kernel, the coin table
+            # (16 phases x 1 bit written, ~mean phases bits read); the kernel is VALU-bound
+            # (per phase: 2n keyed scheduler hashes per slot), so this is not a roofline claim
+            bytes_slot = 5 / 8 + 4 + 4 + 2 / 8 + 16 / 8 + r["mean_phases"] / 8
+            line = {
+                "metric": "consensus slots decided/sec (5 replicas, 2^24 slots, adversarial split, "
+                          "Weak-MVC to termination)",
+                "value": r["decided"] / (r["total_ms"] / 1000.0), "unit": "slots decided/s", "n_gpus": world,
+                "steps": a.steps, "warmup": a.warmup, "ms_per_step": r["total_ms"] / a.steps,
+                "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+                "dtype": "u32 replica bit masks (integer only)",
+                "data": "synthetic (adversarial split initial states generated on device)",
+                "config": {"workload": f"C3: 5 replicas x {r['total']} slots, every replica of every slot runs "
+                                       f"Weak-MVC phases (f+1 decide, common coin) until all decided (<= 32)",
+                           "replicas": 5, "slots_per_step": r["total"], "slots_per_gpu": r["S"],
+                           "mean_phases": r["mean_phases"], "max_phases": r["max_phases"],
+                           "parallelism": f"slot-shard x{world}, stats + decided bitmaps all-gathered"},
+                "roofline": {"bound": "valu", "achieved": r["S"] * bytes_slot / (r["kern_ms"] / 1000.0) / 1e9,
+                             "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": r["S"] * bytes_slot / (r["kern_ms"] / 1000.0) / 1e9 / HBM_PEAK_GBS,
+                             "traffic": None, "kernel_avg_us": r["kern_ms"] * 1000.0,
+                             "note": "VALU-bound (scheduler hashes + coin), HBM fraction shown for reference"},
+                "cpu_baseline": None, "sweep_1m_us": None,
+            }
+            print(json.dumps(line), flush=True)
+        r["ev"].close()
+        if dist is not None:
+            dist.destroy_process_group()
+        return
     if a.config == "c5":
         n, window_slots = 9, a.c5_windows * WINDOW
         assert window_slots % (world * 32 * (a.tile_words or 4)) == 0, "C5 needs equal tile-aligned shards"

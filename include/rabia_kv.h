@@ -20,6 +20,12 @@
  *   0 Success   1 NotFound   2 Error(InvalidKey "Key cannot be empty")
  *   3 Error(InvalidKey "Key too long")   4 Error(ValueTooLarge)   5 Error(StoreFull)
  *   6 Command.data is not a bincode KVOperation   7 not applied (slot not decided V1)
+ *   8 refused: the store's capacity (table slots / heap bytes) cannot hold the batch;
+ *     the whole batch was refused before any write (rg_kv_stats.flags says which)
+ *
+ * Value bytes are allocated in size classes (powers of two >= 16): a SET whose value
+ * fits its key's current allocation overwrites it in place, so updates of existing
+ * keys never grow the heap; only new keys and outgrown values take heap bytes.
  */
 #ifndef RABIA_KV_H
 #define RABIA_KV_H
@@ -41,6 +47,7 @@ enum {
   RG_KV_E_FULL = 5,
   RG_KV_E_DECODE = 6,
   RG_KV_NOT_APPLIED = 7,
+  RG_KV_E_CAPACITY = 8,
 };
 
 /* KVStoreConfig (store.rs:17-42) fields the apply reads, plus device capacities. */
@@ -53,7 +60,8 @@ typedef struct rg_kv_config {
   uint64_t heap_bytes;           /* key + value byte heap; 0 => 64 * table_slots          */
   uint32_t hash_bits;            /* test hook: keep only the low hash_bits bits of the key
                                     hash (0 = all 64) to force hash-collision runs        */
-  uint32_t reserved;
+  uint32_t bucket_bits;          /* test hook: sort bucket width (0 = 31 bits); a narrow
+                                    bucket puts keys with distinct full hashes in one run */
 } rg_kv_config;
 
 /* Store counters (host copy). */
@@ -66,10 +74,10 @@ typedef struct rg_kv_stats {
   uint64_t batches;          /* rg_kv_apply calls                                      */
   uint64_t ordered_batches;  /* batches applied on the exact in-order path (StoreFull
                                 reachable or a hash collision group too large)          */
-  uint64_t flags;            /* nonzero: capacity fault (table or heap full); the batch
-                                that raised it was not applied                          */
+  uint64_t flags;            /* nonzero: a capacity fault (1 table slots, 2 heap bytes)
+                                refused a batch; that batch changed nothing              */
   uint64_t last_path;        /* the last batch: 0 keyed replay, 1 ordered replay,
-                                2 refused (capacity fault)                              */
+                                2 refused (capacity fault, results RG_KV_E_CAPACITY)     */
 } rg_kv_stats;
 
 int rg_kv_create(rg_kv** out, const rg_kv_config* cfg);

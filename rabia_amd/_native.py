@@ -59,7 +59,7 @@ INGEST_STATS = ["r1", "r2", "superseded", "other", "outside", "invalid", "sender
 class RgKvConfig(ctypes.Structure):
     _fields_ = [("max_keys", u64), ("max_value_size", u64), ("enable_notifications", u32),
                 ("device", i32), ("table_slots", u64), ("heap_bytes", u64), ("hash_bits", u32),
-                ("reserved", u32)]
+                ("bucket_bits", u32)]
 
 
 KV_STATS_FIELDS = ["live_keys", "version", "total_operations", "occupied_slots", "heap_used",
@@ -98,6 +98,7 @@ _SIGS = {
     "rg_digest_trace_async": (ctypes.c_int, [vp, u64, u64, u64, u64, vp, vp]),
     "rg_wmvc_cluster_async": (ctypes.c_int, [vp, vp, u64, u64, u64, u64, u32, vp, vp, vp]),
     "rg_cluster_trace_async": (ctypes.c_int, [vp, u64, u64, u64, u64, vp, vp]),
+    "rg_cluster_bitmap_async": (ctypes.c_int, [vp, vp, u64, vp, vp, vp]),
     "rg_stream_sync": (ctypes.c_int, [vp, vp]),
     "rg_pack_codes": (ctypes.c_int, [vp, u32, u64, u64, vp]),
     "rg_unpack_planes": (ctypes.c_int, [vp, u32, u64, u64, vp]),

@@ -36,16 +36,21 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in DEPS)
 
 
-def build(force: bool = False, resource_usage: bool = False, verbose: bool = False) -> str:
-    """Compile each translation unit to an object in parallel (hipcc -c), then link."""
-    if not force and not needs_build() and not resource_usage:
+def build(force: bool = False, resource_usage: bool = False, verbose: bool = False, out: str = None,
+          defines=()) -> str:
+    """Compile each translation unit to an object in parallel (hipcc -c), then link.
+    out/defines: an experiment build (-D flags) written elsewhere (A/B runs load it
+    through RABIA_GPU_LIB)."""
+    if out is None and not force and not needs_build() and not resource_usage:
         return LIB
-    obj_dir = os.path.join(LIB_DIR, "obj")
+    lib = out or LIB
+    obj_dir = os.path.join(LIB_DIR, "obj" if out is None else "obj_" + os.path.basename(out))
     os.makedirs(obj_dir, exist_ok=True)
     base = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result",
             "-I", os.path.join(ROOT, "include")]
     if resource_usage:
         base.insert(1, "-Rpass-analysis=kernel-resource-usage")
+    base += [f"-D{d}" for d in defines]
     objs, procs = [], []
     for src in SOURCES:
         obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
@@ -59,17 +64,17 @@ def build(force: bool = False, resource_usage: bool = False, verbose: bool = Fal
         if proc.returncode != 0:
             sys.stderr.write(out + err)
             raise RuntimeError(f"hipcc failed ({proc.returncode}): {' '.join(cmd)}")
-    link = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB + ".tmp", *objs]
+    link = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib + ".tmp", *objs]
     proc = subprocess.run(link, capture_output=True, text=True)
     if proc.returncode != 0:
         sys.stderr.write(proc.stdout + proc.stderr)
         raise RuntimeError(f"hipcc link failed ({proc.returncode}): {' '.join(link)}")
-    os.replace(LIB + ".tmp", LIB)
+    os.replace(lib + ".tmp", lib)
     if verbose and err_text:
         sys.stderr.write(err_text)
     if resource_usage:
         print_resource_usage(err_text)
-    return LIB
+    return lib
 
 
 def print_resource_usage(text: str) -> None:
@@ -96,5 +101,13 @@ def print_resource_usage(text: str) -> None:
 
 
 if __name__ == "__main__":
-    build(force=True, resource_usage="--resource-usage" in sys.argv, verbose="-v" in sys.argv)
-    print(LIB)
+    args = sys.argv[1:]
+    out = None
+    defs = []
+    for a in args:
+        if a.startswith("--out="):
+            out = a.split("=", 1)[1]
+        elif a.startswith("-D"):
+            defs.append(a[2:])
+    print(build(force=True, resource_usage="--resource-usage" in args, verbose="-v" in args, out=out,
+                defines=defs))

@@ -768,6 +768,17 @@ int rg_wmvc_cluster_async(rg_ctx* ctx, const uint32_t* states_dev, uint64_t stri
   return RG_OK;
 }
 
+int rg_cluster_bitmap_async(rg_ctx* ctx, const uint32_t* info_dev, uint64_t n_slots, uint32_t* decided_dev,
+                            uint32_t* v1_dev, void* stream) {
+  if (!ctx || !info_dev || !decided_dev || !v1_dev || n_slots == 0)
+    return fail(ctx, RG_EINVAL, "rg_cluster_bitmap: bad argument");
+  RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
+  hipLaunchKernelGGL(cluster_bitmap_kernel, dim3((uint32_t)((n_slots + 255) / 256)), dim3(256), 0,
+                     pick_stream(ctx, stream), info_dev, n_slots, decided_dev, v1_dev);
+  RG_HIP(ctx, hipGetLastError());
+  return RG_OK;
+}
+
 int rg_cluster_trace_async(rg_ctx* ctx, uint64_t seed, uint64_t slot_base, uint64_t n_slots, uint64_t stride_words,
                            uint32_t* states_dev, void* stream) {
   if (!ctx || !states_dev || n_slots == 0 || stride_words < (n_slots + 31) / 32)

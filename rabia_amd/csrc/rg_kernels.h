@@ -59,7 +59,12 @@ struct StepParams {
 constexpr int kFinRef = 0, kFinWmvc = 1, kFinShard = 2;
 
 __device__ __forceinline__ void stamp(const StepParams& p, uint32_t tile, int k, int tid) {
-  if ((p.diag & 4u) && tid == 0) p.dbg[(uint64_t)tile * 8 + k] = __builtin_amdgcn_s_memrealtime();
+  if ((p.diag & 4u) && tid == 0) {
+    p.dbg[(uint64_t)tile * 8 + k] = __builtin_amdgcn_s_memrealtime();
+    // placement of the tile: XCC id (hwreg 20, gfx950) and HW_ID (hwreg 4: CU, SH, SE)
+    if (k == 0) p.dbg[(uint64_t)tile * 8 + 6] = __builtin_amdgcn_s_getreg((15 << 11) | 20);
+    if (k == 0) p.dbg[(uint64_t)tile * 8 + 7] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+  }
 }
 
 constexpr int ctr_bits(int n) { return n < 2 ? 1 : n < 4 ? 2 : n < 8 ? 3 : n < 16 ? 4 : 5; }
@@ -264,7 +269,11 @@ __device__ __forceinline__ uint32_t lookback_exclusive(unsigned long long* statu
         }
         break;
       }
+#ifdef RG_LB_SLEEP  // build-time experiment: longer back-off between polls
+      for (int z = 0; z < RG_LB_SLEEP; z++) __builtin_amdgcn_s_sleep(1);
+#else
       __builtin_amdgcn_s_sleep(1);
+#endif
       continue;
     }
     const uint32_t v = (lane <= first) ? (uint32_t)g : 0u;
@@ -274,6 +283,72 @@ __device__ __forceinline__ uint32_t lookback_exclusive(unsigned long long* statu
   }
   if (lane == 0)
     atomic_store_agent(status + tile, ((unsigned long long)tag_inc << 32) | (agg + excl));
+  return excl;
+}
+
+// Look-back polling K x 64 predecessor granules per round trip (lane l loads the
+// granules at distance 64k + l + 1, k < K, all in flight at once). kfirst = K of
+// the first poll, knext = K of the later ones; sleep = s_sleep between spins.
+// (Diagnostic variants of lookback_exclusive, selected by StepParams.diag bits 12-14.)
+template <int KMAX>
+__device__ __forceinline__ uint32_t lookback_exclusive_wide(unsigned long long* status, uint32_t tile, uint32_t seq,
+                                                            uint32_t agg, int lane, unsigned long long* err,
+                                                            int kfirst, int knext, int sleep) {
+  const uint32_t tag_agg = seq << 1, tag_inc = (seq << 1) | 1u;
+  if (tile == 0) {
+    if (lane == 0) atomic_store_agent(status, ((unsigned long long)tag_inc << 32) | agg);
+    return 0;
+  }
+  if (lane == 0) atomic_store_agent(status + tile, ((unsigned long long)tag_agg << 32) | agg);
+  uint32_t excl = 0;
+  int64_t pos = (int64_t)tile - 1;  // distance 0 = tile - 1
+  uint32_t spins = 0;
+  int K = kfirst;
+  for (;;) {
+    unsigned long long g[KMAX];
+#pragma unroll
+    for (int k = 0; k < KMAX; k++) {
+      const int64_t pidx = pos - lane - 64 * k;
+      g[k] = (k < K && pidx >= 0) ? atomic_load_agent(status + pidx) : ((unsigned long long)tag_inc << 32);
+    }
+    // newest inclusive granule (smallest distance) and readiness of everything before it
+    int first = 64 * KMAX;  // distance of the newest inclusive
+    bool blocked = false;
+#pragma unroll
+    for (int k = 0; k < KMAX; k++) {
+      if (k >= K) break;
+      const uint32_t tag = (uint32_t)(g[k] >> 32);
+      const bool ready = (tag >> 1) == seq;
+      const unsigned long long im = __ballot(ready && (tag & 1u));
+      const unsigned long long nr = __ballot(!ready);
+      if (first == 64 * KMAX) {
+        const int f = im ? __builtin_ctzll(im) : 64;
+        const unsigned long long need = f >= 63 ? ~0ull : ((2ull << f) - 1ull);
+        if (nr & need) { blocked = true; break; }
+        if (f < 64) first = 64 * k + f;
+      }
+    }
+    if (blocked) {
+      if (++spins > (1u << 22)) {
+        if (lane == 0) {
+          atomicOr(err, 1ull);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        break;
+      }
+      for (int z = 0; z < sleep; z++) __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    uint32_t v = 0;
+#pragma unroll
+    for (int k = 0; k < KMAX; k++)
+      if (k < K && 64 * k + lane <= first) v += (uint32_t)g[k];
+    excl += (uint32_t)wave_sum64(v);
+    if (first < 64 * KMAX) break;
+    pos -= 64 * K;
+    K = knext;
+  }
+  if (lane == 0) atomic_store_agent(status + tile, ((unsigned long long)tag_inc << 32) | (agg + excl));
   return excl;
 }
 
@@ -534,6 +609,25 @@ __device__ __forceinline__ TileStats thread_stats(const uint32_t (&committed)[W]
 // Occupancy: 4 waves per SIMD (<= 128 VGPRs) so that at least two 512-thread or
 // four 256-thread tiles are resident per CU and one tile's look-back / stores
 // overlap another's loads.
+template <int N, int W>
+__device__ __forceinline__ void load_planes(const StepParams& p, uint64_t w0, bool active, int first_plane,
+                                            uint32_t (&lo)[N][W], uint32_t (&hi)[N][W]) {
+  if (active) {
+    const uint32_t* base = p.votes + p.lin.base(w0);
+    const uint64_t ps = p.lin.pstride;
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      load_words<W>(base + (first_plane + 2 * j) * ps, lo[j]);
+      load_words<W>(base + (first_plane + 2 * j + 1) * ps, hi[j]);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < N; j++)
+#pragma unroll
+      for (int i = 0; i < W; i++) lo[j][i] = hi[j][i] = ~0u;
+  }
+}
+
 // Decision code masks (lo, hi) of count_votes over the round-2 lanes of word i
 // (messages.rs:185-211; 3 = None): V0 0/0, V1 1/0, VQ 0/1, None 1/1.
 template <int N, int W>
@@ -567,6 +661,7 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
   constexpr int WAVES = BLOCK / 64;
   __shared__ uint32_t s_wave[WAVES];
   __shared__ uint32_t s_excl;
+  __shared__ uint32_t s_cls[2 * W][BLOCK];  // (c1 > c0), (c1 < c0) of the VQ slots, parked in LDS
   Record* rec = p.rec + (p.seq & 1u);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t tile = blockIdx.x;
@@ -578,35 +673,19 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
 
   // Issue every plane load up front (R2 stays in flight across the look-back).
   uint32_t r1lo[N][W], r1hi[N][W], r2lo[N][W], r2hi[N][W];
-  if (active) {
-    const uint32_t* base = p.votes + p.lin.base(w0);
-    const uint64_t ps = p.lin.pstride;
-#pragma unroll
-    for (int j = 0; j < N; j++) {
-      load_words<W>(base + (2 * j) * ps, r1lo[j]);
-      load_words<W>(base + (2 * j + 1) * ps, r1hi[j]);
-    }
-#pragma unroll
-    for (int j = 0; j < N; j++) {
-      load_words<W>(base + (2 * N + 2 * j) * ps, r2lo[j]);
-      load_words<W>(base + (2 * N + 2 * j + 1) * ps, r2hi[j]);
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < N; j++)
-#pragma unroll
-      for (int i = 0; i < W; i++) r1lo[j][i] = r1hi[j][i] = r2lo[j][i] = r2hi[j][i] = ~0u;
-  }
-  uint32_t vm[W];
-#pragma unroll
-  for (int i = 0; i < W; i++) vm[i] = valid_mask(w0 + i, p.n_words, p.n_slots);
+  load_planes<N, W>(p, w0, active, 0, r1lo, r1hi);
+#ifdef RG_R1_BARRIER  // build-time experiment: every wave's R1 loads queue ahead of any R2 load
+  __builtin_amdgcn_s_barrier();
+#endif
+  load_planes<N, W>(p, w0, active, 2 * N, r2lo, r2hi);
 
   // ---- round 1: count_votes + |votes| >= quorum fallback (engine.rs:495-505).
   // Only what the draws need survives the tally: per-slot (c1 > c0), (c1 < c0).
-  uint32_t r1v1[W], r1vq[W], pend[W], c1gt[W], c1lt[W];
+  uint32_t r1v1[W], r1vq[W], pend[W];
   uint32_t vq_count = 0;
 #pragma unroll
   for (int i = 0; i < W; i++) {
+    const uint32_t vm = valid_mask(w0 + i, p.n_words, p.n_slots);
     Ctr<B> c0, c1, cp;
     ctr_zero(c0); ctr_zero(c1); ctr_zero(cp);
 #pragma unroll
@@ -617,11 +696,14 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
       ctr_add(cp, ~(lo & hi));
     }
     const uint32_t g0 = ctr_ge(c0, p.q), g1 = ctr_ge(c1, p.q), gp = ctr_ge(cp, p.q);
-    const uint32_t v0 = g0 & vm[i];
-    r1v1[i] = ~g0 & g1 & vm[i];
-    r1vq[i] = ~g0 & ~g1 & gp & vm[i];  // cq >= q implies present >= q
-    pend[i] = ~(v0 | r1v1[i] | r1vq[i]) & vm[i];
-    ctr_cmp(c1, c0, c1gt[i], c1lt[i]);
+    const uint32_t v0 = g0 & vm;
+    r1v1[i] = ~g0 & g1 & vm;
+    r1vq[i] = ~g0 & ~g1 & gp & vm;  // cq >= q implies present >= q
+    pend[i] = ~(v0 | r1v1[i] | r1vq[i]) & vm;
+    uint32_t gt, lt;
+    ctr_cmp(c1, c0, gt, lt);
+    s_cls[2 * i][tid] = gt & r1vq[i];
+    s_cls[2 * i + 1][tid] = lt & r1vq[i];
     vq_count += __builtin_popcount(r1vq[i]);
   }
 
@@ -637,8 +719,14 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
   }
   stamp(p, tile, 1, tid);
   if (wave == 0) {
+#ifdef RG_LB_WIDE  // build-time experiment: K-wide polls (tools/ab_variants.sh)
+    const uint32_t e = (p.diag & 1u) ? 0u
+                                     : lookback_exclusive_wide<4>(p.lookback, tile, p.seq, tile_total, lane,
+                                                                  &rec->error.v, RG_LB_WIDE);
+#else
     const uint32_t e = (p.diag & 1u) ? 0u
                                      : lookback_exclusive(p.lookback, tile, p.seq, tile_total, lane, &rec->error.v);
+#endif
     if (lane == 0) s_excl = e;
   }
   lds_barrier();
@@ -671,13 +759,15 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
       const unsigned long long k_lim = (cb + BLOCK) << 3;
 #pragma unroll
       for (int i = 0; i < W; i++) {
+        if (!mq[i] || k >= k_lim) continue;
+        const uint32_t gtm = s_cls[2 * i][tid], ltm = s_cls[2 * i + 1][tid];
         while (mq[i] && k < k_lim) {
           const int b = __builtin_ctz(mq[i]);
           mq[i] &= mq[i] - 1;
           const uint32_t row = (uint32_t)((k >> 3) - cb), ws = (uint32_t)(k & 7u) * 2u;
           const unsigned long long u =
               (unsigned long long)s_blk[row][ws] | ((unsigned long long)s_blk[row][ws + 1] << 32);
-          const bool gt = (c1gt[i] >> b) & 1u, lt = (c1lt[i] >> b) & 1u;
+          const bool gt = (gtm >> b) & 1u, lt = (ltm >> b) & 1u;
           const bool v1 = gt ? (u < kP90) : (lt ? (u >= kP90) : (u < kP80));
           own_lo[i] |= (uint32_t)v1 << b;
           k++;
@@ -687,89 +777,439 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
     }
   }
 
-  // ---- own vote joins round2_votes (engine.rs:540-542); decision (613-628)
-  uint32_t dlo[W], dhi[W], alo[W], ahi[W];
-  if constexpr (SHARD) {
-    // the decision under the other own vote, for the VQ slots' draw records
-#pragma unroll
-    for (int j = 0; j < N; j++) {
-      if (j == p.self_lane) {
-#pragma unroll
-        for (int i = 0; i < W; i++) {
-          const uint32_t l = r2lo[j][i], h = r2hi[j][i];
-          r2lo[j][i] = (l & pend[i]) | ((own_lo[i] ^ r1vq[i]) & ~pend[i]);
-          r2hi[j][i] = h & pend[i];
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < W; i++) r2_decision<N, W>(r2lo, r2hi, i, p.q, alo[i], ahi[i]);
-  }
-#pragma unroll
-  for (int j = 0; j < N; j++) {
-    if (j == p.self_lane) {
-#pragma unroll
-      for (int i = 0; i < W; i++) {
-        r2lo[j][i] = (r2lo[j][i] & pend[i]) | (own_lo[i] & ~pend[i]);
-        r2hi[j][i] &= pend[i];
-      }
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < W; i++) r2_decision<N, W>(r2lo, r2hi, i, p.q, dlo[i], dhi[i]);
-  uint32_t o[kOutPlanes][W];
+  // ---- own vote joins round2_votes (engine.rs:540-542); decision (613-628),
+  // one word at a time; only the decision masks stay live for the stores
+  uint32_t dlo[W], dhi[W];
+  unsigned long long kr = k_first - k_base;  // SHARD: local draw number of this thread's first VQ slot
 #pragma unroll
   for (int i = 0; i < W; i++) {
-    const uint32_t d1 = dlo[i] & ~dhi[i];
-    const uint32_t dc = ~dhi[i];  // V0 or V1
-    o[0][i] = (r1v1[i] | pend[i]) & vm[i];
-    o[1][i] = (r1vq[i] | pend[i]) & vm[i];
-    o[2][i] = (own_lo[i] | pend[i]) & vm[i];
-    o[3][i] = pend[i];
-    o[4][i] = dlo[i] & vm[i];
-    o[5][i] = dhi[i] & vm[i];
-    o[6][i] = dc & vm[i];   // set_decision: committed iff not VQuestion
-    o[7][i] = d1 & vm[i];   // V1: apply_batch + commit_phase
-  }
-  if (active) {
-    uint32_t* ob = p.out + p.lout.base(w0);
+    if constexpr (SHARD) {
+      uint32_t alo = 0, ahi = 0;
+      if (r1vq[i]) {  // the decision under the other own vote, for the draw records
 #pragma unroll
-    for (int pl = 0; pl < kOutPlanes; pl++) store_words_nt<W>(ob + pl * p.lout.pstride, o[pl]);
-  }
-  if constexpr (SHARD) {
-    // draw records, indexed by local draw number (ascending slot order)
-    unsigned long long kr = k_first - k_base;
+        for (int j = 0; j < N; j++)
+          if (j == p.self_lane) {
+            const uint32_t l = r2lo[j][i], h = r2hi[j][i];
+            r2lo[j][i] = (l & pend[i]) | ((own_lo[i] ^ r1vq[i]) & ~pend[i]);
+            r2hi[j][i] = h & pend[i];
+            r2_decision<N, W>(r2lo, r2hi, i, p.q, alo, ahi);
+            r2lo[j][i] = l;
+            r2hi[j][i] = h;
+          }
+      }
 #pragma unroll
-    for (int i = 0; i < W; i++) {
+      for (int j = 0; j < N; j++)
+        if (j == p.self_lane) {
+          r2lo[j][i] = (r2lo[j][i] & pend[i]) | (own_lo[i] & ~pend[i]);
+          r2hi[j][i] &= pend[i];
+        }
+      r2_decision<N, W>(r2lo, r2hi, i, p.q, dlo[i], dhi[i]);
       uint32_t m = r1vq[i];
-      while (m) {
+      const uint32_t gtm = m ? s_cls[2 * i][tid] : 0u, ltm = m ? s_cls[2 * i + 1][tid] : 0u;
+      while (m) {  // draw records, indexed by local draw number (ascending slot order)
         const int b = __builtin_ctz(m);
         m &= m - 1;
         const uint32_t own = (own_lo[i] >> b) & 1u;
         const uint32_t dp = ((dlo[i] >> b) & 1u) | (((dhi[i] >> b) & 1u) << 1);
-        const uint32_t da = ((alo[i] >> b) & 1u) | (((ahi[i] >> b) & 1u) << 1);
+        const uint32_t da = ((alo >> b) & 1u) | (((ahi >> b) & 1u) << 1);
         const uint32_t d_v0 = own ? da : dp, d_v1 = own ? dp : da;
-        const uint32_t cls = ((c1gt[i] >> b) & 1u) ? kRecGt : (((c1lt[i] >> b) & 1u) ? kRecLt : 0u);
+        const uint32_t cls = ((gtm >> b) & 1u) ? kRecGt : (((ltm >> b) & 1u) ? kRecLt : 0u);
         const uint32_t info = cls | (d_v0 << 2) | (d_v1 << 4) | (own << 6);
         const uint32_t off = (uint32_t)(32u * (w0 + i) + b);
         if (kr < p.vq_cap) p.vq_rec[kr] = ((unsigned long long)info << 32) | off;
         kr++;
       }
+    } else {
+#pragma unroll
+      for (int j = 0; j < N; j++)
+        if (j == p.self_lane) {
+          r2lo[j][i] = (r2lo[j][i] & pend[i]) | (own_lo[i] & ~pend[i]);
+          r2hi[j][i] &= pend[i];
+        }
+      r2_decision<N, W>(r2lo, r2hi, i, p.q, dlo[i], dhi[i]);
     }
+    const uint32_t vm = valid_mask(w0 + i, p.n_words, p.n_slots);
+    dlo[i] &= vm;
+    dhi[i] &= vm;
+  }
+  uint32_t st_dec[W], st_v1[W];
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    st_dec[i] = ~dhi[i] & valid_mask(w0 + i, p.n_words, p.n_slots);  // committed iff not VQuestion
+    st_v1[i] = dlo[i] & ~dhi[i];  // V1: apply_batch + commit_phase
+  }
+  if (active) {  // plane by plane from the masks (include/rabia_gpu.h output planes)
+    uint32_t* ob = p.out + p.lout.base(w0);
+    const uint64_t ps = p.lout.pstride;
+    uint32_t v[W];
+#pragma unroll
+    for (int i = 0; i < W; i++) v[i] = r1v1[i] | pend[i];
+    store_words_nt<W>(ob, v);
+#pragma unroll
+    for (int i = 0; i < W; i++) v[i] = r1vq[i] | pend[i];
+    store_words_nt<W>(ob + ps, v);
+#pragma unroll
+    for (int i = 0; i < W; i++) v[i] = own_lo[i] | pend[i];
+    store_words_nt<W>(ob + 2 * ps, v);
+    store_words_nt<W>(ob + 3 * ps, pend);
+    store_words_nt<W>(ob + 4 * ps, dlo);
+    store_words_nt<W>(ob + 5 * ps, dhi);
+    store_words_nt<W>(ob + 6 * ps, st_dec);
+    store_words_nt<W>(ob + 7 * ps, st_v1);
   }
   stamp(p, tile, 3, tid);
   if (p.diag & 2u) return;
-  uint32_t st_dec[W], st_v1[W], st_vm[W];
+  uint32_t st_vm[W];
 #pragma unroll
   for (int i = 0; i < W; i++) {  // SHARD: VQ slots are counted by the fix-up
     const uint32_t keep = SHARD ? ~r1vq[i] : ~0u;
-    st_dec[i] = o[6][i] & keep;
-    st_v1[i] = o[7][i] & keep;
-    st_vm[i] = vm[i] & keep;
+    st_dec[i] &= keep;
+    st_v1[i] &= keep;
+    st_vm[i] = valid_mask(w0 + i, p.n_words, p.n_slots) & keep;
   }
   const TileStats ts = thread_stats<W>(st_dec, st_v1, pend, st_vm, vq_count, w0, tw0, p);
   finish_tile<SHARD ? kFinShard : kFinRef, BLOCK, W>(p, rec, ts, tile, tid, lane, wave);
   stamp(p, tile, 4, tid);
+}
+
+// ============================================================================
+// Persistent REF step (large launches). G workgroups, all resident at once
+// (G = resident blocks per CU x CUs); WG g handles tiles g, g+G, g+2G, ... in
+// order. Software pipeline per WG: the next tile's R1 planes are loaded into the
+// registers of the current tile's R1 (dead after the tally) while this tile waits
+// for its look-back, and the next tile's R2 planes right after this tile's stores
+// — so a WG always has its next tile's bytes in flight and the look-back wait
+// overlaps HBM traffic instead of idling the CU. Statistics accumulate per WG in
+// registers; WG 0 folds the G per-WG records at the end. Forward progress: the
+// lowest unfinished tile's predecessors are all done and every WG is resident.
+// ============================================================================
+// per-WG statistics record: 4 tagged granules (tag 12 bits at [52, 64))
+//   g0 = dec:26 | v1:26 << 26      g1 = pend:26 | draws:26 << 26
+//   g2 = (largest accepted V1 offset + 1, 0 = none):33   g3 = smallest undecided offset (2^33-1 = none):33
+constexpr int kPersistStatGranules = 4;
+constexpr unsigned long long kOff33 = (1ull << 33) - 1;
+__device__ __forceinline__ unsigned long long pstat_tag(uint32_t seq) {
+  return (unsigned long long)(0x800u | (seq & 0x7FFu)) << 52;
+}
+
+// PREF = 1: the next tile's R1 loads are issued by waves 1.. during wave 0's
+// look-back; PREF = 0: by every wave right after the draws (fewer live registers
+// across the draws' ChaCha blocks).
+template <int N, int W, int BLOCK, bool SHARD, int PREF>
+__global__ __launch_bounds__(BLOCK, 4) void ref_persist_kernel(StepParams p) {
+  constexpr int B = ctr_bits(N);
+  constexpr int WAVES = BLOCK / 64;
+  constexpr uint64_t kTileWords = (uint64_t)BLOCK * W;
+  __shared__ uint32_t s_wave[WAVES];
+  __shared__ uint32_t s_excl;
+  __shared__ uint32_t s_cls[2 * W][BLOCK];  // c1 > c0 / c1 < c0 masks, parked across the look-back
+  __shared__ uint32_t s_blk[BLOCK][17];
+  Record* rec = p.rec + (p.seq & 1u);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t G = gridDim.x;
+  uint32_t tile = blockIdx.x;
+  if (tile == 0 && tid == 0) atomic_store_agent(&p.rec[(p.seq + 1) & 1u].error.v, 0ull);
+  const uint32_t tw0 = (uint32_t)tid * W;
+  const unsigned long long k_base = SHARD ? p.state->shard_draws : p.state->rng_next;
+  uint32_t a_dec = 0, a_v1 = 0, a_pend = 0, a_draws = 0;
+  unsigned long long a_max1 = 0, a_min = kOff33;
+
+  uint32_t r1lo[N][W], r1hi[N][W], r2lo[N][W], r2hi[N][W];
+  {
+    const uint64_t w0 = (uint64_t)tile * kTileWords + tw0;
+    load_planes<N, W>(p, w0, w0 < p.n_words, 0, r1lo, r1hi);
+    load_planes<N, W>(p, w0, w0 < p.n_words, 2 * N, r2lo, r2hi);
+  }
+  for (;;) {
+    const uint64_t w0 = (uint64_t)tile * kTileWords + tw0;
+    const bool active = w0 < p.n_words;
+    const uint32_t next = tile + G;
+    const bool has_next = next < p.n_tiles;
+    const uint64_t nw0 = (uint64_t)next * kTileWords + tw0;
+
+    // ---- round 1 (engine.rs:495-505)
+    uint32_t r1v1[W], r1vq[W], pend[W];
+    uint32_t vq_count = 0;
+#pragma unroll
+    for (int i = 0; i < W; i++) {
+      const uint32_t vm = valid_mask(w0 + i, p.n_words, p.n_slots);
+      Ctr<B> c0, c1, cp;
+      ctr_zero(c0); ctr_zero(c1); ctr_zero(cp);
+#pragma unroll
+      for (int j = 0; j < N; j++) {
+        const uint32_t lo = r1lo[j][i], hi = r1hi[j][i];
+        ctr_add(c0, ~lo & ~hi);
+        ctr_add(c1, lo & ~hi);
+        ctr_add(cp, ~(lo & hi));
+      }
+      const uint32_t g0 = ctr_ge(c0, p.q), g1 = ctr_ge(c1, p.q), gp = ctr_ge(cp, p.q);
+      r1v1[i] = ~g0 & g1 & vm;
+      r1vq[i] = ~g0 & ~g1 & gp & vm;
+      pend[i] = ~((g0 & vm) | r1v1[i] | r1vq[i]) & vm;
+      uint32_t gt, lt;
+      ctr_cmp(c1, c0, gt, lt);
+      s_cls[2 * i][tid] = gt & r1vq[i];
+      s_cls[2 * i + 1][tid] = lt & r1vq[i];
+      vq_count += __builtin_popcount(r1vq[i]);
+    }
+    const uint32_t incl = wave_incl_scan32(vq_count, lane);
+    if (lane == 63) s_wave[wave] = incl;
+    lds_barrier();
+    uint32_t wave_off = 0, tile_total = 0;
+#pragma unroll
+    for (int w = 0; w < WAVES; w++) {
+      wave_off += (w < wave) ? s_wave[w] : 0u;
+      tile_total += s_wave[w];
+    }
+    // ---- look-back (wave 0) while waves 1.. prefetch the next tile's R1 planes
+    if (wave == 0) {
+      const uint32_t e = (p.diag & 1u) ? 0u
+                                       : lookback_exclusive(p.lookback, tile, p.seq, tile_total, lane, &rec->error.v);
+      if (lane == 0) s_excl = e;
+    } else if (PREF && has_next) {
+      load_planes<N, W>(p, nw0, nw0 < p.n_words, 0, r1lo, r1hi);
+    }
+    lds_barrier();
+    if (PREF && wave == 0 && has_next) load_planes<N, W>(p, nw0, nw0 < p.n_words, 0, r1lo, r1hi);
+
+    // ---- own round-2 vote: one StdRng draw per VQ slot (engine.rs:523-537, 567-611)
+    const unsigned long long k_tile = k_base + s_excl;
+    const unsigned long long k_first = k_tile + wave_off + incl - vq_count;
+    unsigned long long k = k_first;
+    uint32_t own_lo[W], mq[W];
+#pragma unroll
+    for (int i = 0; i < W; i++) {
+      own_lo[i] = r1v1[i];
+      mq[i] = r1vq[i];
+    }
+    if (tile_total) {
+      const unsigned long long b_first = k_tile >> 3, b_last = (k_tile + tile_total - 1) >> 3;
+      for (unsigned long long cb = b_first; cb <= b_last; cb += BLOCK) {
+        if (cb + tid <= b_last) {
+          uint32_t x[16];
+          chacha_block<12>(p.key, cb + tid, 0, x);
+#pragma unroll
+          for (int j = 0; j < 16; j++) s_blk[tid][j] = x[j];
+        }
+        lds_barrier();
+        const unsigned long long k_lim = (cb + BLOCK) << 3;
+#pragma unroll
+        for (int i = 0; i < W; i++) {
+          if (!mq[i] || k >= k_lim) continue;
+          const uint32_t gtm = s_cls[2 * i][tid], ltm = s_cls[2 * i + 1][tid];
+          while (mq[i] && k < k_lim) {
+            const int b = __builtin_ctz(mq[i]);
+            mq[i] &= mq[i] - 1;
+            const uint32_t row = (uint32_t)((k >> 3) - cb), ws = (uint32_t)(k & 7u) * 2u;
+            const unsigned long long u =
+                (unsigned long long)s_blk[row][ws] | ((unsigned long long)s_blk[row][ws + 1] << 32);
+            const bool gt = (gtm >> b) & 1u, lt = (ltm >> b) & 1u;
+            const bool v1 = gt ? (u < kP90) : (lt ? (u >= kP90) : (u < kP80));
+            own_lo[i] |= (uint32_t)v1 << b;
+            k++;
+          }
+        }
+        lds_barrier();
+      }
+    }
+
+    if (!PREF && has_next) load_planes<N, W>(p, nw0, nw0 < p.n_words, 0, r1lo, r1hi);
+
+    // ---- round 2, one word at a time (engine.rs:540-542, 613-628): only the
+    // decision masks stay live, so the R2 registers free up before the stores
+    unsigned long long kr = k_first - k_base;  // SHARD: local draw number of this thread's first VQ slot
+    uint32_t dlo[W], dhi[W];
+#pragma unroll
+    for (int i = 0; i < W; i++) {
+      const uint32_t vm = valid_mask(w0 + i, p.n_words, p.n_slots);
+      if constexpr (SHARD) {
+        uint32_t alo = 0, ahi = 0;
+        if (r1vq[i]) {  // the decision under the other own vote, for the draw records
+#pragma unroll
+          for (int j = 0; j < N; j++)
+            if (j == p.self_lane) {
+              const uint32_t l = r2lo[j][i], h = r2hi[j][i];
+              r2lo[j][i] = (l & pend[i]) | ((own_lo[i] ^ r1vq[i]) & ~pend[i]);
+              r2hi[j][i] = h & pend[i];
+              r2_decision<N, W>(r2lo, r2hi, i, p.q, alo, ahi);
+              r2lo[j][i] = l;
+              r2hi[j][i] = h;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < N; j++)
+          if (j == p.self_lane) {
+            r2lo[j][i] = (r2lo[j][i] & pend[i]) | (own_lo[i] & ~pend[i]);
+            r2hi[j][i] &= pend[i];
+          }
+        r2_decision<N, W>(r2lo, r2hi, i, p.q, dlo[i], dhi[i]);
+        uint32_t m = r1vq[i];
+        if (m) {
+          const uint32_t gtm = s_cls[2 * i][tid], ltm = s_cls[2 * i + 1][tid];
+          while (m) {
+            const int b = __builtin_ctz(m);
+            m &= m - 1;
+            const uint32_t own = (own_lo[i] >> b) & 1u;
+            const uint32_t dp = ((dlo[i] >> b) & 1u) | (((dhi[i] >> b) & 1u) << 1);
+            const uint32_t da = ((alo >> b) & 1u) | (((ahi >> b) & 1u) << 1);
+            const uint32_t d_v0 = own ? da : dp, d_v1 = own ? dp : da;
+            const uint32_t cls = ((gtm >> b) & 1u) ? kRecGt : (((ltm >> b) & 1u) ? kRecLt : 0u);
+            const uint32_t info = cls | (d_v0 << 2) | (d_v1 << 4) | (own << 6);
+            const uint32_t off = (uint32_t)(32u * (w0 + i) + b);
+            if (kr < p.vq_cap) p.vq_rec[kr] = ((unsigned long long)info << 32) | off;
+            kr++;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < N; j++)
+          if (j == p.self_lane) {
+            r2lo[j][i] = (r2lo[j][i] & pend[i]) | (own_lo[i] & ~pend[i]);
+            r2hi[j][i] &= pend[i];
+          }
+        r2_decision<N, W>(r2lo, r2hi, i, p.q, dlo[i], dhi[i]);
+      }
+      dlo[i] &= vm;
+      dhi[i] &= vm;
+      const uint32_t d1 = dlo[i] & ~dhi[i], dc = ~dhi[i] & vm;
+      // statistics (SHARD: the fix-up counts the VQ slots)
+      const uint32_t keep = SHARD ? ~r1vq[i] : ~0u;
+      a_dec += __builtin_popcount(dc & keep);
+      const uint32_t v1k = d1 & keep;
+      a_v1 += __builtin_popcount(v1k);
+      a_pend += __builtin_popcount(pend[i]);
+      const uint32_t v1l = v1k & phase_limit_mask(p.slot_base, w0 + i, p.max_phase);
+      if (v1l) {
+        const unsigned long long m1 = 32ull * (w0 + i) + (31u - __builtin_clz(v1l)) + 1u;
+        a_max1 = m1 > a_max1 ? m1 : a_max1;
+      }
+      const uint32_t und = ~dc & vm & keep;
+      if (und) {
+        const unsigned long long mn = 32ull * (w0 + i) + __builtin_ctz(und);
+        a_min = mn < a_min ? mn : a_min;
+      }
+    }
+    a_draws += vq_count;
+    if (active) {  // plane by plane from the masks (include/rabia_gpu.h output planes)
+      uint32_t* ob = p.out + p.lout.base(w0);
+      const uint64_t ps = p.lout.pstride;
+      uint32_t v[W];
+#pragma unroll
+      for (int i = 0; i < W; i++) v[i] = r1v1[i] | pend[i];
+      store_words_nt<W>(ob, v);
+#pragma unroll
+      for (int i = 0; i < W; i++) v[i] = r1vq[i] | pend[i];
+      store_words_nt<W>(ob + ps, v);
+#pragma unroll
+      for (int i = 0; i < W; i++) v[i] = own_lo[i] | pend[i];
+      store_words_nt<W>(ob + 2 * ps, v);
+      store_words_nt<W>(ob + 3 * ps, pend);
+      store_words_nt<W>(ob + 4 * ps, dlo);
+      store_words_nt<W>(ob + 5 * ps, dhi);
+#pragma unroll
+      for (int i = 0; i < W; i++) v[i] = ~dhi[i] & valid_mask(w0 + i, p.n_words, p.n_slots);
+      store_words_nt<W>(ob + 6 * ps, v);  // set_decision: committed iff not VQuestion
+#pragma unroll
+      for (int i = 0; i < W; i++) v[i] = dlo[i] & ~dhi[i];
+      store_words_nt<W>(ob + 7 * ps, v);  // V1: apply_batch + commit_phase
+    }
+    if (!has_next) break;
+    load_planes<N, W>(p, nw0, nw0 < p.n_words, 2 * N, r2lo, r2hi);
+    tile = next;
+  }
+
+  // ---- per-WG record, folded by WG 0
+  if (p.diag & 2u) return;
+  {
+    __shared__ unsigned long long red[WAVES][4];
+    const unsigned long long packed = (unsigned long long)a_dec | ((unsigned long long)a_v1 << 26);
+    const unsigned long long packed2 = (unsigned long long)a_pend | ((unsigned long long)a_draws << 26);
+    const unsigned long long s0 = wave_sum64(packed), s1 = wave_sum64(packed2);
+    const unsigned long long mx = wave_max64(a_max1), mn = wave_min64(a_min);
+    if (lane == 0) { red[wave][0] = s0; red[wave][1] = s1; red[wave][2] = mx; red[wave][3] = mn; }
+    lds_barrier();
+    if (tid == 0) {
+      unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = kOff33;
+#pragma unroll
+      for (int w = 0; w < WAVES; w++) {
+        t0 += red[w][0]; t1 += red[w][1];
+        t2 = red[w][2] > t2 ? red[w][2] : t2;
+        t3 = red[w][3] < t3 ? red[w][3] : t3;
+      }
+      const unsigned long long tag = pstat_tag(p.seq);
+      unsigned long long* g = p.stats + (uint64_t)blockIdx.x * kPersistStatGranules;
+      atomic_store_agent(g + 0, tag | t0);
+      atomic_store_agent(g + 1, tag | t1);
+      atomic_store_agent(g + 2, tag | t2);
+      atomic_store_agent(g + 3, tag | t3);
+    }
+  }
+  if (blockIdx.x != 0) return;
+  unsigned long long v[7] = {0, 0, 0, 0, 0, ~0ull, 0};  // dec v1 pend draws max(id+1) min(id) fault
+  const unsigned long long tag = pstat_tag(p.seq);
+  constexpr unsigned long long kTagMask = ~0ull << 52, kMask26 = (1ull << 26) - 1;
+  for (uint32_t wg = tid; wg < G; wg += BLOCK) {
+    unsigned long long* gp = p.stats + (uint64_t)wg * kPersistStatGranules;
+    unsigned long long g[4];
+#pragma unroll
+    for (int k2 = 0; k2 < 4; k2++) g[k2] = atomic_load_agent(gp + k2);
+    uint32_t spins = 0;
+    for (;;) {
+      bool ready = true;
+#pragma unroll
+      for (int k2 = 0; k2 < 4; k2++) ready &= (g[k2] & kTagMask) == tag;
+      if (ready) break;
+      if (++spins > kSpinLimit) { v[6] = 2; break; }
+      __builtin_amdgcn_s_sleep(2);
+#pragma unroll
+      for (int k2 = 0; k2 < 4; k2++)
+        if ((g[k2] & kTagMask) != tag) g[k2] = atomic_load_agent(gp + k2);
+    }
+    v[0] += g[0] & kMask26;
+    v[1] += (g[0] >> 26) & kMask26;
+    v[2] += g[1] & kMask26;
+    v[3] += (g[1] >> 26) & kMask26;
+    const unsigned long long mx = g[2] & kOff33, mn = g[3] & kOff33;
+    if (mx && p.slot_base + mx > v[4]) v[4] = p.slot_base + mx;
+    if (mn != kOff33 && p.slot_base + mn < v[5]) v[5] = p.slot_base + mn;
+  }
+  block_reduce_totals<BLOCK>(v, lane, wave);
+  if (tid != 0) return;
+  const unsigned long long err = atomicAdd(&rec->error.v, 0ull) | v[6];
+  DevState st = *p.state;
+  DevResult r;
+  r.n_slots = p.n_slots;
+  r.n_decided = v[0];
+  r.n_v1 = v[1];
+  r.n_pending_r1 = v[2];
+  r.n_draws = v[3];
+  const unsigned long long end = p.slot_base + p.n_slots;
+  const unsigned long long fu = v[5] < end ? v[5] : end;
+  if constexpr (SHARD) {
+    r.last_committed_max = v[4] ? v[4] - 1 : 0;
+    r.first_undecided = fu;
+    r.rng_next = st.shard_draws + r.n_draws;
+    r.commit_watermark = 0;
+    r.flags = err;
+    st.shard_draws = r.rng_next;
+  } else {
+    unsigned long long lc = st.last_committed;  // commit_phase: monotonic max, state.rs:77-99
+    if (v[4] && v[4] - 1 > lc) lc = v[4] - 1;
+    unsigned long long wm = st.commit_watermark;
+    if (p.slot_base <= wm && wm < fu) wm = fu;
+    r.last_committed_max = lc;
+    r.first_undecided = fu;
+    r.rng_next = st.rng_next + r.n_draws;
+    r.commit_watermark = wm;
+    r.flags = err;
+    st.rng_next = r.rng_next;
+    st.last_committed = lc;
+    st.commit_watermark = wm;
+    st.steps += 1;
+  }
+  *p.state = st;
+  *p.result = r;
+  if (p.result_user) *p.result_user = r;
 }
 
 // ============================================================================
@@ -1795,6 +2235,20 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
     for (int w = 0; w < 4; w++) v = k == 3 ? (red[w][k] > v ? red[w][k] : v) : v + red[w][k];
     partials[(uint64_t)blockIdx.x * kClusterStats + k] = v;
   }
+}
+
+// Decided / V1 bitmaps of a cluster run's info words (one wave ballot per 64 slots):
+// the per-shard payload the C3 multi-GPU exchange all-gathers.
+static __global__ __launch_bounds__(256) void cluster_bitmap_kernel(const uint32_t* info, uint64_t n_slots,
+                                                                    uint32_t* decided, uint32_t* v1) {
+  const uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint32_t d = s < n_slots ? (info[s] & 255u) : kCodeNone;
+  const unsigned long long bd = __ballot(d <= kCodeV1), b1 = __ballot(d == kCodeV1);
+  const int lane = threadIdx.x & 63;
+  const uint64_t w = (s - lane) / 32;  // this wave's first word
+  const uint64_t n_words = (n_slots + 31) / 32;
+  if (lane == 0 && w < n_words) { decided[w] = (uint32_t)bd; v1[w] = (uint32_t)b1; }
+  if (lane == 32 && w + 1 < n_words) { decided[w + 1] = (uint32_t)(bd >> 32); v1[w + 1] = (uint32_t)(b1 >> 32); }
 }
 
 static __global__ void cluster_stats_kernel(const unsigned long long* partials, uint32_t nblocks, unsigned long long* out) {

@@ -34,25 +34,36 @@ namespace {
 
 constexpr uint64_t kEmpty = 0;
 constexpr uint64_t kInvalidKey = ~0ull;    // full hash of commands that are not applied
-// Sort key: a 31-bit bucket of the full hash (equal hashes -> equal buckets), so the
-// radix sort runs 4 digit passes instead of 8; commands that are not applied get
-// kInvalidBucket and sort last. A bucket run may hold several hashes: the walkers
+// Sort key: a bucket of the full hash (equal hashes -> equal buckets) narrow enough
+// for 3-4 radix digit passes instead of 8; commands that are not applied get the
+// invalid bucket and sort last. A bucket run may hold several hashes: the walkers
 // already split runs into keys by comparing key bytes, and look each key up with
 // its own full hash.
-constexpr uint64_t kInvalidBucket = 0xFFFFFFFFull;
+// (The bucket width is chosen per batch: valid buckets take sbits - 1 bits and the
+// invalid bucket is 1 << (sbits - 1), so a radix sort over sbits bits orders them.)
 // Command bytes sit at arbitrary byte offsets: multi-byte fields, key compares and
 // copies go through 1-byte-aligned types (gfx950 global memory takes unaligned
 // dword accesses; little-endian like bincode's fixint encoding).
 typedef uint64_t u64_unaligned __attribute__((aligned(1)));
 typedef uint32_t u32_unaligned __attribute__((aligned(1)));
-constexpr int kSortBits = 32;
-__device__ __forceinline__ uint64_t hash_bucket(uint64_t h) { return (h ^ (h >> 32)) & 0x7FFFFFFFull; }
+__device__ __forceinline__ uint64_t hash_bucket(uint64_t h, uint64_t bmask) { return (h ^ (h >> 32)) & bmask; }
 constexpr uint32_t kMaxKeyLen = 256;       // store.rs:467
 constexpr int kBlock = 256;
 constexpr int kMaxRunKeys = 8;             // distinct keys per hash run on the keyed path
 constexpr uint8_t kPending = 0xFF;
 
 enum : uint64_t { kFaultTable = 1, kFaultHeap = 2 };
+
+// Value allocations come in size classes (0, then powers of two >= 16): a SET whose
+// value's class is not above the class of the slot's current value length
+// overwrites the bytes in place, so updating a key never grows the heap; only new
+// keys and values outgrowing their allocation take heap bytes.
+__device__ __forceinline__ uint64_t val_class(uint64_t len) {
+  if (len == 0) return 0;
+  uint64_t c = 16;
+  while (c < len) c <<= 1;
+  return c;
+}
 
 struct KvEntry {        // one table slot (the hash lives in its own array for probing)
   uint64_t key_off;     // heap offset of the key bytes
@@ -80,7 +91,10 @@ struct KvCounters {
 };
 
 // Per-block partials of the plan / commit walks.
-enum { kPCreated = 0, kPNewSlots, kPOverflow, kPLiveDelta, kPVersion, kPOps, kPCount };
+enum { kPCreated = 0, kPNewSlots, kPOverflow, kPLiveDelta, kPVersion, kPOps, kPNeed, kPCount };
+constexpr int kWalkPerLane = 4;                              // sorted positions per walker lane
+constexpr int kWalkSpan = 64 * kWalkPerLane;                 // positions per wave
+constexpr int kWalkBlockSpan = kBlock * kWalkPerLane;        // positions per block
 
 __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
   k ^= k >> 33; k *= 0xff51afd7ed558ccdull;
@@ -157,12 +171,15 @@ __device__ __forceinline__ void bytes_copy(uint8_t* dst, const uint8_t* src, uin
 }
 
 // ---- 1 decode ----------------------------------------------------------------
-__global__ void kv_decode_kernel(const uint8_t* __restrict__ data, const uint64_t* __restrict__ off,
-                                 uint64_t n, const uint8_t* __restrict__ mask, uint64_t max_value, uint64_t hmask,
-                                 KvOp* __restrict__ ops, uint64_t* __restrict__ sort_key, uint64_t* __restrict__ full_hash,
-                                 uint32_t* __restrict__ sort_idx, uint8_t* __restrict__ results) {
+__global__ __launch_bounds__(kBlock) void kv_decode_kernel(
+    const uint8_t* __restrict__ data, const uint64_t* __restrict__ off, uint64_t n, const uint8_t* __restrict__ mask,
+    uint64_t max_value, uint64_t hmask, uint64_t bmask, uint64_t invalid_bucket, KvOp* __restrict__ ops,
+    uint64_t* __restrict__ sort_key,
+    uint64_t* __restrict__ full_hash, uint32_t* __restrict__ sort_idx, uint8_t* __restrict__ results,
+    unsigned long long* __restrict__ set_part) {
   const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= n) return;
+  unsigned long long sets = 0, set_bytes = 0;  // worst-case growth of the batch (the refusal check)
+  if (c < n) {
   KvOp op{0, 0, 0, 0, 0, kPending};
   uint64_t key = kInvalidKey;
   if (mask && !mask[c]) {
@@ -204,10 +221,28 @@ __global__ void kv_decode_kernel(const uint8_t* __restrict__ data, const uint64_
     }
   }
   ops[c] = op;
-  sort_key[c] = key == kInvalidKey ? kInvalidBucket : hash_bucket(key);
+  sort_key[c] = key == kInvalidKey ? invalid_bucket : hash_bucket(key, bmask);
   full_hash[c] = key;
   sort_idx[c] = (uint32_t)c;
   if (op.status != kPending) results[c] = (uint8_t)op.status;
+  if (op.status == kPending && op.kind == 0) {
+    sets = 1;
+    set_bytes = op.key_len + val_class(op.val_len);
+  }
+  }
+  __shared__ unsigned long long red[kBlock / 64][2];
+  for (int o = 32; o > 0; o >>= 1) {
+    sets += __shfl_xor(sets, o, 64);
+    set_bytes += __shfl_xor(set_bytes, o, 64);
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) { red[wave][0] = sets; red[wave][1] = set_bytes; }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    unsigned long long t = 0;
+    for (int w = 0; w < kBlock / 64; w++) t += red[w][threadIdx.x];
+    set_part[(uint64_t)blockIdx.x * 2 + threadIdx.x] = t;
+  }
 }
 
 // ---- table lookup ------------------------------------------------------------
@@ -262,7 +297,8 @@ struct BatchView {
   uint8_t* results;
   uint8_t* done;          // per sorted position: handled by an earlier key of its run
   uint64_t* need;         // per sorted position: plan bytes (run heads only)
-  uint64_t* heap_off;     // exclusive scan of need
+  uint64_t* block_base;   // per walk block: heap offset of its first byte (decide's scan)
+  uint64_t invalid_bucket;  // sort key of the commands that are not applied (sorted last)
   unsigned long long* part;  // [blocks][kPCount]
 };
 
@@ -337,104 +373,208 @@ __device__ __forceinline__ void block_add_partials(unsigned long long (&v)[kPCou
 }
 
 // ---- 3 plan / 5 commit -------------------------------------------------------
+// Each wave owns kWalkSpan consecutive sorted positions; its lanes find the run
+// heads among them (ballots), compact them into LDS and each lane walks one head
+// at a time, so every lane has a run (a run starts at a head and may extend past
+// the wave's span). Plan sizes the heap bytes each run writes; the block totals go
+// to the partials and decide scans them into per-block bases; commit re-derives
+// the same lanes' offsets by a block scan of their plan sizes.
 template <bool COMMIT>
 __global__ __launch_bounds__(kBlock) void kv_walk_kernel(BatchView b, StoreView st) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  unsigned long long acc[kPCount] = {0, 0, 0, 0, 0, 0};
+  __shared__ uint16_t s_heads[kBlock / 64][kWalkSpan];
+  __shared__ unsigned long long s_wsum[kBlock / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  unsigned long long acc[kPCount] = {0, 0, 0, 0, 0, 0, 0};
   const bool go = !COMMIT || st.ctr->mode == 0;
-  if (go && i < b.n) {
-    const uint64_t h = b.skey[i];
-    if (h != kInvalidBucket && (i == 0 || b.skey[i - 1] != h)) {
-      uint64_t end = i + 1;
-      while (end < b.n && b.skey[end] == h) end++;
-      uint64_t need = 0, heap_pos = COMMIT ? st.ctr->batch_base + b.heap_off[i] : 0;
-      int keys = 0;
-      for (uint64_t first = i; first < end; first++) {
-        if (b.done[first]) continue;
-        if (++keys > kMaxRunKeys) { acc[kPOverflow] = 1; break; }
-        const KvOp lead = b.ops[b.sidx[first]];
-        const uint64_t hl = b.hfull[b.sidx[first]];
-        const uint8_t* kp = b.data + lead.key_off;
-        const int64_t slot = table_find(st.hashes, st.ent, st.heap, st.mask, hl, kp, lead.key_len);
-        const KeyOutcome o = replay_key<COMMIT>(b, st, first, end, lead, slot, true);
-        acc[kPOps] += o.n_ops;
-        acc[kPVersion] += o.n_version;
-        acc[kPLiveDelta] += (unsigned long long)((int64_t)o.live1 - (int64_t)o.live0);
-        // keys that become live at some point of the batch (bound on data.len())
-        acc[kPCreated] += !o.live0 && o.any_set;
-        const bool new_slot = slot < 0 && o.live1;
-        acc[kPNewSlots] += new_slot;
-        const uint64_t kbytes = new_slot ? lead.key_len : 0;
-        const uint64_t vbytes = (o.live1 && o.wrote_value) ? b.ops[o.last_set].val_len : 0;
-        need += kbytes + vbytes;
-        if (COMMIT) {
-          int64_t s = slot;
-          if (new_slot) {
-            s = table_claim(st.hashes, st.mask, hl);
-            if (s < 0) { atomicOr(&st.ctr->flags, kFaultTable); continue; }
-            uint8_t* dst = st.heap + heap_pos;
-            bytes_copy(dst, kp, lead.key_len);
-            st.ent[s].key_off = heap_pos;
-            st.ent[s].key_len = lead.key_len;
-            heap_pos += kbytes;
-          }
-          if (s >= 0 && (o.live0 || o.live1)) {
-            if (o.live1 && o.wrote_value) {
-              const KvOp& sop = b.ops[o.last_set];
-              const uint8_t* src = b.data + sop.val_off;
-              uint8_t* dst = st.heap + heap_pos;
-              bytes_copy(dst, src, sop.val_len);
+  const uint64_t wbase = ((uint64_t)blockIdx.x * (kBlock / 64) + wave) * kWalkSpan;
+  uint32_t nh = 0;
+#pragma unroll
+  for (int k = 0; k < kWalkPerLane; k++) {
+    const uint64_t i = wbase + 64 * k + lane;
+    bool head = false;
+    if (go && i < b.n) {
+      const uint64_t h = b.skey[i];
+      head = h != b.invalid_bucket && (i == 0 || b.skey[i - 1] != h);
+    }
+    const unsigned long long m = __ballot(head);
+    if (head) s_heads[wave][nh + __builtin_popcountll(m & ((1ull << lane) - 1ull))] = (uint16_t)(64 * k + lane);
+    nh += (uint32_t)__builtin_popcountll(m);
+  }
+  __builtin_amdgcn_wave_barrier();
+  uint64_t heap_pos = 0;
+  if (COMMIT) {  // this lane's heap offset: block base + exclusive prefix of plan sizes over (wave, lane)
+    unsigned long long mine = 0;
+    for (uint32_t h = lane; h < nh; h += 64) mine += b.need[wbase + s_heads[wave][h]];
+    unsigned long long incl = mine;
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned long long t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
+    }
+    if (lane == 63) s_wsum[wave] = incl;
+    __syncthreads();
+    unsigned long long before = 0;
+    for (int w = 0; w < wave; w++) before += s_wsum[w];
+    if (go) heap_pos = st.ctr->batch_base + b.block_base[blockIdx.x] + before + incl - mine;
+  }
+  for (uint32_t h = lane; h < nh; h += 64) {
+    const uint64_t i = wbase + s_heads[wave][h];
+    const uint64_t hb = b.skey[i];
+    uint64_t end = i + 1;
+    while (end < b.n && b.skey[end] == hb) end++;
+    uint64_t need = 0;
+    int keys = 0;
+    for (uint64_t first = i; first < end; first++) {
+      if (b.done[first]) continue;
+      if (++keys > kMaxRunKeys) { acc[kPOverflow] = 1; break; }
+      const KvOp lead = b.ops[b.sidx[first]];
+      const uint64_t hl = b.hfull[b.sidx[first]];
+      const uint8_t* kp = b.data + lead.key_off;
+      const int64_t slot = table_find(st.hashes, st.ent, st.heap, st.mask, hl, kp, lead.key_len);
+      const KeyOutcome o = replay_key<COMMIT>(b, st, first, end, lead, slot, true);
+      acc[kPOps] += o.n_ops;
+      acc[kPVersion] += o.n_version;
+      acc[kPLiveDelta] += (unsigned long long)((int64_t)o.live1 - (int64_t)o.live0);
+      // keys that become live at some point of the batch (bound on data.len())
+      acc[kPCreated] += !o.live0 && o.any_set;
+      const bool new_slot = slot < 0 && o.live1;
+      acc[kPNewSlots] += new_slot;
+      const uint64_t kbytes = new_slot ? lead.key_len : 0;
+      const uint64_t vlen = (o.live1 && o.wrote_value) ? b.ops[o.last_set].val_len : 0;
+      // in place when the final value's class fits the slot's current allocation
+      const bool in_place = slot >= 0 && o.live1 && o.wrote_value && val_class(vlen) <= val_class(st.ent[slot].val_len);
+      const uint64_t vbytes = (o.live1 && o.wrote_value && !in_place) ? val_class(vlen) : 0;
+      need += kbytes + vbytes;
+      if (COMMIT) {
+        int64_t s = slot;
+        if (new_slot) {
+          s = table_claim(st.hashes, st.mask, hl);
+          if (s < 0) { atomicOr(&st.ctr->flags, kFaultTable); continue; }
+          bytes_copy(st.heap + heap_pos, kp, lead.key_len);
+          st.ent[s].key_off = heap_pos;
+          st.ent[s].key_len = lead.key_len;
+          st.ent[s].val_len = 0;
+          heap_pos += kbytes;
+        }
+        if (s >= 0 && (o.live0 || o.live1)) {
+          if (o.live1 && o.wrote_value) {
+            const KvOp& sop = b.ops[o.last_set];
+            if (!in_place) {
               st.ent[s].val_off = heap_pos;
-              st.ent[s].val_len = sop.val_len;
               heap_pos += vbytes;
             }
-            st.ent[s].version = o.live1 ? o.ver1 : 0;
+            bytes_copy(st.heap + st.ent[s].val_off, b.data + sop.val_off, sop.val_len);
+            st.ent[s].val_len = sop.val_len;
           }
+          st.ent[s].version = o.live1 ? o.ver1 : 0;
         }
       }
-      if (!COMMIT) b.need[i] = need;
-    } else if (!COMMIT) {
-      b.need[i] = 0;
     }
-  } else if (!COMMIT && i < b.n) {
-    b.need[i] = 0;
+    if (!COMMIT) b.need[i] = need;
+    acc[kPNeed] += need;
   }
   block_add_partials(acc, b.part);
 }
 
 // ---- 4 decide ----------------------------------------------------------------
-__global__ void kv_decide_kernel(StoreView st, const unsigned long long* part, uint32_t blocks,
-                                 const uint64_t* need, const uint64_t* heap_off, uint64_t n) {
-  __shared__ unsigned long long red[kBlock][3];
-  unsigned long long c = 0, ns = 0, ov = 0;
-  for (uint32_t k = threadIdx.x; k < blocks; k += blockDim.x) {
-    c += part[(uint64_t)k * kPCount + kPCreated];
-    ns += part[(uint64_t)k * kPCount + kPNewSlots];
-    ov |= part[(uint64_t)k * kPCount + kPOverflow];
+// One 1024-thread block folds the per-block partials (16 loads per thread in
+// flight, wave shuffles, one LDS step) and picks the batch's path:
+//   0 keyed commit: StoreFull unreachable (live + keys created <= max_keys);
+//   1 ordered replay: exact in-order path;
+//   2 refused: a capacity (table slots or heap bytes) cannot hold the batch's
+//     worst case — nothing is written, every pending command gets RG_KV_E_CAPACITY.
+constexpr int kFoldBlock = 1024;
+template <int K>
+__device__ __forceinline__ void fold_block(unsigned long long (&v)[K], const unsigned long long* src, uint32_t rows,
+                                           uint32_t stride, const int (&field)[K]) {
+  for (uint32_t r0 = threadIdx.x; r0 < rows; r0 += kFoldBlock * 16) {
+    unsigned long long x[16][K];
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      const uint32_t r = r0 + (uint32_t)u * kFoldBlock;
+#pragma unroll
+      for (int k = 0; k < K; k++) x[u][k] = r < rows ? src[(uint64_t)r * stride + field[k]] : 0ull;
+    }
+#pragma unroll
+    for (int u = 0; u < 16; u++)
+#pragma unroll
+      for (int k = 0; k < K; k++) v[k] = field[k] == kPOverflow ? (v[k] | x[u][k]) : v[k] + x[u][k];
   }
-  red[threadIdx.x][0] = c; red[threadIdx.x][1] = ns; red[threadIdx.x][2] = ov;
+  __shared__ unsigned long long red[kFoldBlock / 64][K];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    unsigned long long t = v[k];
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);  // overflow flags: any nonzero sum
+    if (lane == 0) red[wave][k] = t;
+  }
   __syncthreads();
-  if (threadIdx.x != 0) return;
-  for (int t = 1; t < (int)blockDim.x; t++) {
-    c += red[t][0]; ns += red[t][1]; ov |= red[t][2];
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    unsigned long long t = 0;
+    for (int w = 0; w < kFoldBlock / 64; w++) t += red[w][k];
+    v[k] = t;
   }
+}
+
+__global__ __launch_bounds__(kFoldBlock) void kv_decide_kernel(StoreView st, const unsigned long long* part,
+                                                               uint32_t walk_blocks,
+                                                               const unsigned long long* set_part, uint32_t blocks,
+                                                               uint64_t* block_base) {
+  unsigned long long v[3] = {0, 0, 0};
+  const int f3[3] = {kPCreated, kPNewSlots, kPOverflow};
+  fold_block<3>(v, part, walk_blocks, kPCount, f3);
+  unsigned long long w[2] = {0, 0};
+  const int f2[2] = {0, 1};
+  fold_block<2>(w, set_part, blocks, 2, f2);
+  // exclusive scan of the walk blocks' plan bytes -> block_base; total = the batch's bytes
+  __shared__ unsigned long long s_scan[kFoldBlock];
+  const uint32_t per = (walk_blocks + kFoldBlock - 1) / kFoldBlock;
+  const uint32_t lo = threadIdx.x * per, hi = lo + per < walk_blocks ? lo + per : walk_blocks;
+  unsigned long long run = 0;
+  for (uint32_t q = lo; q < hi; q++) run += part[(uint64_t)q * kPCount + kPNeed];
+  s_scan[threadIdx.x] = run;
+  __syncthreads();
+  for (int o = 1; o < kFoldBlock; o <<= 1) {  // inclusive Hillis-Steele over the thread sums
+    const unsigned long long t = threadIdx.x >= (uint32_t)o ? s_scan[threadIdx.x - o] : 0ull;
+    __syncthreads();
+    s_scan[threadIdx.x] += t;
+    __syncthreads();
+  }
+  unsigned long long off = s_scan[threadIdx.x] - run;
+  for (uint32_t q = lo; q < hi; q++) {
+    block_base[q] = off;
+    off += part[(uint64_t)q * kPCount + kPNeed];
+  }
+  const uint64_t bytes = s_scan[kFoldBlock - 1];
+  if (threadIdx.x != 0) return;
+  const unsigned long long c = v[0], ns = v[1], ov = v[2], sets = w[0], set_bytes = w[1];
   KvCounters* k = st.ctr;
-  const uint64_t bytes = n ? heap_off[n - 1] + need[n - 1] : 0;
   unsigned long long mode = 0;
   // StoreFull unreachable iff live + created <= max_keys (size never exceeds it).
   if (ov || k->live + c > st.max_keys) mode = 1;
-  // capacities: at most 7/8 of the table occupied; heap bytes available
-  const uint64_t cap = st.mask + 1;
-  if (mode == 0 && (k->occupied + ns > cap - cap / 8 || k->heap_top + bytes > st.heap_cap)) mode = 2;
+  // capacities: at most 7/8 of the table occupied; heap bytes available. The ordered
+  // replay is checked against its worst case (every pending SET a new key and a new
+  // value allocation), so a batch either fits whole or is refused before any write.
+  const uint64_t cap = st.mask + 1, slot_cap = cap - cap / 8;
+  if (mode == 0 && (k->occupied + ns > slot_cap || k->heap_top + bytes > st.heap_cap)) mode = 2;
+  if (mode == 1 && (k->occupied + sets > slot_cap || k->heap_top + set_bytes > st.heap_cap)) mode = 2;
   k->mode = mode;
   k->batches += 1;
   if (mode == 0) {
     k->occupied += ns;
-    k->batch_base = k->heap_top;  // commit writes [batch_base + heap_off[i], ...)
+    k->batch_base = k->heap_top;  // commit writes [batch_base + block_base[b] + ..., ...)
     k->heap_top += bytes;
   } else if (mode == 2) {
-    k->flags |= (k->occupied + ns > cap - cap / 8) ? kFaultTable : kFaultHeap;
+    const bool table = mode == 2 && (k->occupied + (ov || k->live + c > st.max_keys ? sets : ns) > slot_cap);
+    k->flags |= table ? kFaultTable : kFaultHeap;
   }
+}
+
+// Refused batch (mode 2): every command still pending gets RG_KV_E_CAPACITY.
+__global__ void kv_refuse_kernel(const KvOp* ops, uint64_t n, const KvCounters* k, uint8_t* results) {
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n || k->mode != 2) return;
+  if (ops[c].status == kPending) results[c] = RG_KV_E_CAPACITY;
 }
 
 // ---- 6 ordered replay (StoreFull reachable) -------------------------------------
@@ -443,7 +583,6 @@ __global__ void kv_ordered_kernel(const uint8_t* data, const KvOp* ops, const ui
   if (threadIdx.x != 0 || st.ctr->mode != 1) return;
   KvCounters* k = st.ctr;
   unsigned long long live = k->live, ver = k->version, tops = k->total_ops, occ = k->occupied, top = k->heap_top;
-  const uint64_t cap = st.mask + 1;
   for (uint64_t c = 0; c < n; c++) {
     const KvOp op = ops[c];
     if (op.status != kPending) continue;
@@ -457,22 +596,26 @@ __global__ void kv_ordered_kernel(const uint8_t* data, const KvOp* ops, const ui
         results[c] = RG_KV_E_FULL;
         continue;
       }
+      // capacity for the worst case was checked before the batch (kv_decide_kernel)
+      bool fits = false;
       if (s < 0) {
-        if (occ + 1 > cap - cap / 8 || top + op.key_len > st.heap_cap) { k->flags |= kFaultTable; break; }
         s = table_claim(st.hashes, st.mask, h);
-        if (s < 0) { k->flags |= kFaultTable; break; }
         occ++;
         bytes_copy(st.heap + top, kp, op.key_len);
         st.ent[s].key_off = top;
         st.ent[s].key_len = op.key_len;
+        st.ent[s].val_len = 0;
         st.ent[s].version = 0;
         top += op.key_len;
+      } else {
+        fits = val_class(op.val_len) <= val_class(st.ent[s].val_len);
       }
-      if (top + op.val_len > st.heap_cap) { k->flags |= kFaultHeap; break; }
-      bytes_copy(st.heap + top, data + op.val_off, op.val_len);
-      st.ent[s].val_off = top;
+      if (!fits) {
+        st.ent[s].val_off = top;
+        top += val_class(op.val_len);
+      }
+      bytes_copy(st.heap + st.ent[s].val_off, data + op.val_off, op.val_len);
       st.ent[s].val_len = op.val_len;
-      top += op.val_len;
       st.ent[s].version = is_live ? st.ent[s].version + 1 : 1;
       if (!is_live) live++;
       ver += st.notify;
@@ -495,23 +638,16 @@ __global__ void kv_ordered_kernel(const uint8_t* data, const KvOp* ops, const ui
 }
 
 // ---- 7 finish (keyed path counters) ----------------------------------------------
-__global__ void kv_finish_kernel(KvCounters* k, const unsigned long long* part, uint32_t blocks) {
-  __shared__ unsigned long long red[kBlock][3];
-  unsigned long long ld = 0, vv = 0, ops = 0;
-  for (uint32_t b = threadIdx.x; b < blocks; b += blockDim.x) {
-    ld += part[(uint64_t)b * kPCount + kPLiveDelta];
-    vv += part[(uint64_t)b * kPCount + kPVersion];
-    ops += part[(uint64_t)b * kPCount + kPOps];
-  }
-  red[threadIdx.x][0] = ld; red[threadIdx.x][1] = vv; red[threadIdx.x][2] = ops;
-  __syncthreads();
-  if (threadIdx.x != 0 || k->mode != 0) return;
-  for (int t = 1; t < (int)blockDim.x; t++) {
-    ld += red[t][0]; vv += red[t][1]; ops += red[t][2];
-  }
-  k->live += ld;  // two's-complement sum of +-1 deltas
-  k->version += vv;
-  k->total_ops += ops;
+__global__ __launch_bounds__(kFoldBlock) void kv_finish_kernel(KvCounters* k, const unsigned long long* part,
+                                                               uint32_t blocks) {
+  if (k->mode != 0) return;
+  unsigned long long v[3] = {0, 0, 0};
+  const int f3[3] = {kPLiveDelta, kPVersion, kPOps};
+  fold_block<3>(v, part, blocks, kPCount, f3);
+  if (threadIdx.x != 0) return;
+  k->live += v[0];  // two's-complement sum of +-1 deltas
+  k->version += v[1];
+  k->total_ops += v[2];
 }
 
 // ---- mark applied commands from the phase step's decision plane -----------------
@@ -585,10 +721,11 @@ struct rg_kv {
   // per-batch scratch
   uint64_t cap_cmds = 0;
   KvOp* ops = nullptr;
-  uint64_t *key_a = nullptr, *key_b = nullptr, *hfull = nullptr, *need = nullptr, *heap_off = nullptr;
+  uint64_t *key_a = nullptr, *key_b = nullptr, *hfull = nullptr, *need = nullptr, *block_base = nullptr;
   uint32_t *idx_a = nullptr, *idx_b = nullptr;
   uint8_t* done = nullptr;
   unsigned long long* part = nullptr;
+  unsigned long long* set_part = nullptr;  // [blocks][2] decode partials: pending SETs, worst-case bytes
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
   std::string err;
@@ -616,9 +753,11 @@ StoreView view(rg_kv* kv) {
 
 void free_scratch(rg_kv* kv) {
   (void)hipFree(kv->ops); (void)hipFree(kv->key_a); (void)hipFree(kv->key_b); (void)hipFree(kv->hfull);
-  (void)hipFree(kv->need); (void)hipFree(kv->heap_off); (void)hipFree(kv->idx_a);
+  (void)hipFree(kv->need); (void)hipFree(kv->block_base); (void)hipFree(kv->idx_a);
   (void)hipFree(kv->idx_b); (void)hipFree(kv->done); (void)hipFree(kv->part); (void)hipFree(kv->tmp);
-  kv->ops = nullptr; kv->key_a = kv->key_b = kv->hfull = kv->need = kv->heap_off = nullptr;
+  (void)hipFree(kv->set_part);
+  kv->set_part = nullptr;
+  kv->ops = nullptr; kv->key_a = kv->key_b = kv->hfull = kv->need = kv->block_base = nullptr;
   kv->idx_a = kv->idx_b = nullptr; kv->done = nullptr; kv->part = nullptr; kv->tmp = nullptr;
   kv->cap_cmds = 0; kv->tmp_bytes = 0;
 }
@@ -635,15 +774,16 @@ int ensure_scratch(rg_kv* kv, uint64_t n) {
   KV_HIP(kv, hipMalloc(&kv->key_b, cap * 8));
   KV_HIP(kv, hipMalloc(&kv->hfull, cap * 8));
   KV_HIP(kv, hipMalloc(&kv->need, cap * 8));
-  KV_HIP(kv, hipMalloc(&kv->heap_off, cap * 8));
+  KV_HIP(kv, hipMalloc(&kv->block_base, (cap / kWalkBlockSpan + 1) * 8));
   KV_HIP(kv, hipMalloc(&kv->idx_a, cap * 4));
   KV_HIP(kv, hipMalloc(&kv->idx_b, cap * 4));
   KV_HIP(kv, hipMalloc(&kv->done, cap));
   KV_HIP(kv, hipMalloc(&kv->part, blocks * kPCount * 8));
+  KV_HIP(kv, hipMalloc(&kv->set_part, blocks * 2 * 8));
   size_t t1 = 0, t2 = 0;
   KV_HIP(kv, hipcub::DeviceRadixSort::SortPairs(nullptr, t1, kv->key_a, kv->key_b, kv->idx_a, kv->idx_b,
-                                                  (int)cap, 0, kSortBits, kv->stream));
-  KV_HIP(kv, hipcub::DeviceScan::ExclusiveSum(nullptr, t2, kv->need, kv->heap_off, (int)cap, kv->stream));
+                                                  (int)cap, 0, 32, kv->stream));
+  KV_HIP(kv, hipcub::DeviceScan::ExclusiveSum(nullptr, t2, kv->need, kv->key_b, (int)cap, kv->stream));
   kv->tmp_bytes = t1 > t2 ? t1 : t2;
   KV_HIP(kv, hipMalloc(&kv->tmp, kv->tmp_bytes));
   kv->cap_cmds = cap;
@@ -744,29 +884,37 @@ int rg_kv_apply_async(rg_kv* kv, const uint8_t* data_dev, const uint64_t* cmd_of
   if (int rc = ensure_scratch(kv, n_cmds)) return rc;
   hipStream_t s = stream ? (hipStream_t)stream : kv->stream;
   const uint32_t blocks = (uint32_t)((n_cmds + kBlock - 1) / kBlock);
+  // sort width: bucket bits enough that distinct keys rarely share a bucket (load
+  // <= 1/4), at most 31 (+1 bit for the invalid bucket): 24 + 1 bits up to 2^22 commands
+  int vbits = 14;
+  while (vbits < 31 && (1ull << (vbits - 2)) < n_cmds) vbits++;
+  if (kv->cfg.bucket_bits && (int)kv->cfg.bucket_bits < vbits) vbits = (int)kv->cfg.bucket_bits;
+  const int sbits = vbits + 1;
+  const uint64_t invalid_bucket = 1ull << vbits;
   hipLaunchKernelGGL(kv_decode_kernel, dim3(blocks), dim3(kBlock), 0, s, data_dev, cmd_off_dev, n_cmds,
                      apply_mask_dev, kv->cfg.max_value_size,
                      kv->cfg.hash_bits && kv->cfg.hash_bits < 64 ? (1ull << kv->cfg.hash_bits) - 1 : ~0ull,
-                     kv->ops, kv->key_a, kv->hfull, kv->idx_a, results_dev);
+                     invalid_bucket - 1, invalid_bucket, kv->ops, kv->key_a, kv->hfull, kv->idx_a,
+                     results_dev, kv->set_part);
   KV_HIP(kv, hipGetLastError());
   size_t tb = kv->tmp_bytes;
   KV_HIP(kv, hipcub::DeviceRadixSort::SortPairs(kv->tmp, tb, kv->key_a, kv->key_b, kv->idx_a, kv->idx_b,
-                                                  (int)n_cmds, 0, kSortBits, s));
+                                                  (int)n_cmds, 0, sbits, s));
   KV_HIP(kv, hipMemsetAsync(kv->done, 0, n_cmds, s));
   BatchView b{data_dev, kv->ops, kv->key_b, kv->hfull, kv->idx_b, n_cmds, results_dev, kv->done, kv->need,
-              kv->heap_off, kv->part};
+              kv->block_base, invalid_bucket, kv->part};
   const StoreView st = view(kv);
-  hipLaunchKernelGGL(kv_walk_kernel<false>, dim3(blocks), dim3(kBlock), 0, s, b, st);
+  const uint32_t walk_blocks = (uint32_t)((n_cmds + kWalkBlockSpan - 1) / kWalkBlockSpan);
+  hipLaunchKernelGGL(kv_walk_kernel<false>, dim3(walk_blocks), dim3(kBlock), 0, s, b, st);
   KV_HIP(kv, hipGetLastError());
-  tb = kv->tmp_bytes;
-  KV_HIP(kv, hipcub::DeviceScan::ExclusiveSum(kv->tmp, tb, kv->need, kv->heap_off, (int)n_cmds, s));
-  hipLaunchKernelGGL(kv_decide_kernel, dim3(1), dim3(kBlock), 0, s, st, kv->part, blocks, kv->need,
-                     kv->heap_off, n_cmds);
+  hipLaunchKernelGGL(kv_decide_kernel, dim3(1), dim3(kFoldBlock), 0, s, st, kv->part, walk_blocks, kv->set_part,
+                     blocks, kv->block_base);
   KV_HIP(kv, hipMemsetAsync(kv->done, 0, n_cmds, s));
-  hipLaunchKernelGGL(kv_walk_kernel<true>, dim3(blocks), dim3(kBlock), 0, s, b, st);
+  hipLaunchKernelGGL(kv_walk_kernel<true>, dim3(walk_blocks), dim3(kBlock), 0, s, b, st);
   hipLaunchKernelGGL(kv_ordered_kernel, dim3(1), dim3(64), 0, s, data_dev, kv->ops, kv->hfull, n_cmds,
                      results_dev, st);
-  hipLaunchKernelGGL(kv_finish_kernel, dim3(1), dim3(kBlock), 0, s, kv->ctr, kv->part, blocks);
+  hipLaunchKernelGGL(kv_finish_kernel, dim3(1), dim3(kFoldBlock), 0, s, kv->ctr, kv->part, walk_blocks);
+  hipLaunchKernelGGL(kv_refuse_kernel, dim3(blocks), dim3(kBlock), 0, s, kv->ops, n_cmds, kv->ctr, results_dev);
   KV_HIP(kv, hipGetLastError());
   return 0;
 }

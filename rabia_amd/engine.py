@@ -316,6 +316,10 @@ class PhaseEvaluator:
         N.check(self.lib.rg_wmvc_cluster_async(self.ctx, states_ptr, stride, n_slots, slot_base, delivery_seed,
                                                max_phases, info_ptr, stats_ptr or None, stream or None), self.ctx)
 
+    def cluster_bitmap_async(self, info_ptr, n_slots, decided_ptr, v1_ptr, stream=0):
+        N.check(self.lib.rg_cluster_bitmap_async(self.ctx, info_ptr, n_slots, decided_ptr, v1_ptr, stream or None),
+                self.ctx)
+
     def cluster_trace_async(self, seed, slot_base, n_slots, stride, states_ptr, stream=0):
         N.check(self.lib.rg_cluster_trace_async(self.ctx, seed, slot_base, n_slots, stride, states_ptr,
                                                 stream or None), self.ctx)

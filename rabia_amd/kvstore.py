@@ -32,6 +32,7 @@ class KVResult(IntEnum):
     ERR_STORE_FULL = 5
     ERR_DECODE = 6         # Command.data is not a bincode KVOperation
     NOT_APPLIED = 7        # slot not decided V1
+    ERR_CAPACITY = 8       # the store's table / heap could not hold the batch: refused whole
 
     def is_success(self):
         return self == KVResult.SUCCESS
@@ -78,6 +79,7 @@ class KVStoreConfig:
     table_slots: int = 0               # 0 => next pow2 >= 2 * max_keys
     heap_bytes: int = 0                # 0 => 64 * table_slots
     hash_bits: int = 0                 # test hook: truncated key hashes force collision runs
+    bucket_bits: int = 0               # test hook: narrow sort buckets mix distinct hashes in a run
 
 
 def pack_commands(blobs):
@@ -97,7 +99,8 @@ class DeviceKVStore:
         self.config = config or KVStoreConfig()
         c = N.RgKvConfig(self.config.max_keys, self.config.max_value_size,
                          1 if self.config.enable_notifications else 0, device,
-                         self.config.table_slots, self.config.heap_bytes, self.config.hash_bits, 0)
+                         self.config.table_slots, self.config.heap_bytes, self.config.hash_bits,
+                         self.config.bucket_bits)
         h = ctypes.c_void_p()
         N.check_kv(self.lib.rg_kv_create(ctypes.byref(h), ctypes.byref(c)))
         self.kv = h
@@ -155,9 +158,14 @@ class DeviceKVStore:
         m = torch.from_numpy(np.asarray(mask, np.uint8)).to(dev) if mask is not None else None
         r = torch.empty(n, dtype=torch.uint8, device=dev)
         torch.cuda.synchronize(dev)  # the store's stream does not order after torch's
+        flags0 = self.stats()["flags"]
         self.apply_async(d.data_ptr(), o.data_ptr(), n, m.data_ptr() if m is not None else None,
                          r.data_ptr(), None)
         self.sync()
+        st = self.stats()
+        if st["last_path"] == 2 or st["flags"] != flags0:
+            raise N.RabiaGpuError(N.RG_ESTATE, f"kvstore capacity exceeded (flags {st['flags']}): the batch of "
+                                               f"{n} commands was refused and changed nothing")
         return [KVResult(int(x)) for x in r.cpu().numpy()]
 
     def apply_command(self, blob) -> KVResult:

@@ -83,6 +83,22 @@ def draw_bases(n_draws, rng_base: int):
     return out, acc
 
 
+CLUSTER_FIELDS = ["all_decided", "decided_v1", "sum_phases", "max_phases", "sum_coin_phases",
+                  "sum_first_decision_phase", "slots", "reserved"]
+
+
+def combine_cluster(rows):
+    """Fold per-shard Weak-MVC cluster statistics (rg_wmvc_cluster_async stats_dev,
+    shards in rank order): counts and sums add, the phase maximum is the max. The
+    coin is keyed by the GLOBAL slot id, so the fold equals one run over the window."""
+    out = [0] * 8
+    for r in rows:
+        r = [int(x) for x in r]
+        for k in range(8):
+            out[k] = max(out[k], r[k]) if k == 3 else out[k] + r[k]
+    return dict(zip(CLUSTER_FIELDS, out))
+
+
 def result_row(d: dict):
     return [int(d.get(k, 0)) for k in RESULT_FIELDS]
 

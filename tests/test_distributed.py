@@ -169,3 +169,65 @@ def test_ref_shards_one_stream_gloo(oracle, world):
         assert g.commit_watermark == eres["commit_watermark"]
         for k in exp:
             np.testing.assert_array_equal(np.array(full[k], np.uint8), exp[k], err_msg=k)
+
+
+def _cluster_stats(info):
+    info = np.asarray(info, np.uint32)
+    dec, ph = info & 255, (info >> 8) & 255
+    first, coins = (info >> 16) & 255, info >> 24
+    return [int((dec != 3).sum()), int((dec == 1).sum()), int(ph.sum()), int(ph.max(initial=0)),
+            int(coins.sum()), int(first.sum()), int(info.size), 0]
+
+
+def _cluster_worker(rank, world, port, q):
+    """C3 across ranks: each rank runs Weak-MVC to termination on its contiguous
+    slot shard (the coin is keyed by the global slot id), then the per-shard
+    statistics and decided bitmaps are all-gathered and folded."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "tests"), root]
+    import oracle_lib as O
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n, S = 5, 30_000
+        start, count = shard.shard_range(S, world, rank)
+        st = O.cluster_trace(n, 42, 1 + start, count)
+        info = O.wmvc_cluster(n, 3, 3, 7, 3, 99, 32, 1 + start, st)
+        rows = shard.exchange_results(torch.tensor(_cluster_stats(info), dtype=torch.int64))
+        g = shard.combine_cluster(rows.tolist())
+        width = max(shard.shard_range(S, world, r)[1] for r in range(world))
+        bits = np.zeros(width, np.uint8)
+        bits[:count] = (info & 255) <= 1
+        allb = shard.exchange_bitmap(torch.from_numpy(bits)).numpy()
+        full = np.concatenate([allb[r][:shard.shard_range(S, world, r)[1]] for r in range(world)])
+        q.put((rank, g, full.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_cluster_shards_gloo(oracle):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cluster_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    import queue
+    got = []
+    while len(got) < world:
+        try:
+            got.append(q.get(timeout=1))
+        except queue.Empty:
+            assert all(p.is_alive() or p.exitcode == 0 for p in procs), "a rank died"
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    n, S = 5, 30_000
+    info = oracle.wmvc_cluster(n, 3, 3, 7, 3, 99, 32, 1, oracle.cluster_trace(n, 42, 1, S))
+    exp = shard.combine_cluster([_cluster_stats(info)])
+    for rank, g, bits in got:
+        assert g == exp
+        np.testing.assert_array_equal(np.array(bits, np.uint8), ((info & 255) <= 1).astype(np.uint8))

@@ -366,3 +366,93 @@ def test_c_restatement_equals_python_restatement(oracle):
         assert c.state() == ref.state()
         st = c.stats()
         assert st["total_operations"] == ref.total_operations and st["live_keys"] == len(ref.data)
+
+
+@pytest.mark.gpu
+def test_gpu_sustained_batches_heap_stays_bounded(oracle):
+    """30 device-generated C4 batches on ONE store whose heap holds only a few
+    batches' worth of bytes: value updates overwrite in place (size classes), so
+    the heap stops growing once every key exists; no batch is refused, and every
+    result and the final store equal the sequential C restatement."""
+    import torch
+    n, ks, batches = 1 << 16, 1 << 12, 30
+    heap = 3 * ks * (16 + 32) + (1 << 16)   # keys + one value class each, plus slack
+    with _store(max_keys=1 << 16, heap_bytes=heap) as dev:
+        ref = oracle.KVStoreC(max_keys=1 << 16)
+        data = torch.empty(68 * n, dtype=torch.uint8, device="cuda")
+        off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+        res = torch.empty(n, dtype=torch.uint8, device="cuda")
+        used = []
+        for b in range(batches):
+            torch.cuda.synchronize()
+            dev.trace_async(100 + b, n, ks, data.data_ptr(), data.numel(), off.data_ptr())
+            dev.apply_async(data.data_ptr(), off.data_ptr(), n, None, res.data_ptr())
+            dev.sync()
+            st = dev.stats()
+            assert st["flags"] == 0 and st["last_path"] == 0, (b, st)
+            offs = off.cpu().numpy().view(np.uint64)
+            exp = ref.apply(data.cpu().numpy()[: int(offs[-1])], offs)
+            np.testing.assert_array_equal(res.cpu().numpy(), exp, err_msg=f"batch {b}")
+            used.append(st["heap_used"])
+        assert used[-1] == used[5], used   # no growth once the key space is populated
+        got, exp = dev.get_state(), ref.state()
+        assert got["data"] == exp["data"] and got["version"] == exp["version"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("max_keys", [0, 30])  # 0: keyed path; 30: StoreFull reachable -> ordered path
+def test_gpu_refused_batch_changes_nothing(max_keys):
+    """A batch the heap cannot hold is refused whole: every pending command reports
+    RG_KV_E_CAPACITY, the store (entries, counters, heap) is exactly as before, the
+    flags say why, and the host apply raises. A later batch that fits applies."""
+    from rabia_amd import _native as N
+    rng = random.Random(9)
+    mk = max_keys or R.DEFAULT_MAX_KEYS
+    with _store(max_keys=max_keys, max_value_size=64, heap_bytes=2048, table_slots=1 << 10) as dev:
+        ref = R.KVStoreRef(max_keys=mk, max_value_size=64)
+        small = [R.encode_op(R.SET, f"k{i}".encode(), b"v" * 8) for i in range(8)]
+        assert [int(x) for x in dev.apply_commands(small)] == ref.apply_commands(small)
+        before, st0 = dev.get_state(), dev.stats()
+        big = random_blobs(rng, 400, 300, edge=False)
+        with pytest.raises(N.RabiaGpuError):
+            dev.apply_commands(big)
+        st1 = dev.stats()
+        assert st1["last_path"] == 2 and st1["flags"] != 0
+        for k in ("live_keys", "version", "total_operations", "occupied_slots", "heap_used"):
+            assert st1[k] == st0[k], k
+        assert dev.get_state() == before
+        # results of the refused batch: every pending command says "refused"
+        import torch
+        from rabia_amd.kvstore import pack_commands
+        data, offs = pack_commands(big)
+        d = torch.from_numpy(data.copy()).cuda()
+        o = torch.from_numpy(offs.view(np.int64)).cuda()
+        r = torch.zeros(len(big), dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        dev.apply_async(d.data_ptr(), o.data_ptr(), len(big), None, r.data_ptr())
+        dev.sync()
+        assert set(r.cpu().numpy().tolist()) <= {8, R.E_KEY_EMPTY, R.E_KEY_LONG, R.E_VALUE_LARGE, R.E_DECODE}
+        assert 8 in r.cpu().numpy().tolist()
+        more = [R.encode_op(R.SET, b"k1", b"w" * 8), R.encode_op(R.GET, b"k3")]
+        assert [int(x) for x in dev.apply_commands(more)] == ref.apply_commands(more)
+        got = dev.get_state()
+        assert got["data"] == ref.state()["data"] and got["version"] == ref.state()["version"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bucket_bits", [3, 6, 10])
+def test_gpu_narrow_buckets_mix_hashes(bucket_bits):
+    """Sort buckets narrower than the hash (ADVICE: the 31-bit bucket path): one
+    walker run holds keys with distinct full hashes, each looked up with its own
+    hash; inserts, deletes and the more-than-8-keys ordered fallback vs the
+    restatement."""
+    rng = random.Random(bucket_bits)
+    with _store(max_value_size=64, bucket_bits=bucket_bits, table_slots=1 << 14) as dev:
+        ref = R.KVStoreRef(max_value_size=64)
+        for _ in range(3):
+            blobs = random_blobs(rng, 3000, 500)
+            got = [int(x) for x in dev.apply_commands(blobs)]
+            assert got == ref.apply_commands(blobs)
+        _check_state(dev, ref)
+        # 3 / 6 bits: ~60 / ~8 keys per run -> ordered replay; 10 bits: ~1 key per run
+        assert (dev.stats()["ordered_batches"] > 0) == (bucket_bits <= 6)
