@@ -12,7 +12,10 @@ extern "C" {
 /* diag bits: 1 skip the look-back wait (wrong draws), 2 skip per-tile statistics
  * and the step result, 4 record per-tile s_memrealtime stamps (100 MHz);
  * bits 8-10: 0 = automatic tile shape, 1 big (512 x W), 2 mid (256 x W), 3 small (128 x 1),
- *            4 big (512 x 2), 5 mid (256 x 2) (REF, n = 5 only). */
+ *            4 big (512 x 2), 5 mid (256 x 2) (REF, n = 5 only),
+ *            6 the pipelined ring kernel at any size (REF rg_phase_step_async);
+ * bits 12-13: ring workgroups per CU (0 = up to 2); bit 15: large REF launches use
+ * the tiled kernel instead of the ring. */
 int rg_debug_set(rg_ctx* ctx, uint32_t diag);
 int rg_debug_stamps(rg_ctx* ctx, uint64_t* host_out, uint64_t n_words);
 /* REF kernel memory pattern (20 in-planes, 8 out-planes, 16 B/lane) without protocol.

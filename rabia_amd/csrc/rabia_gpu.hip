@@ -52,6 +52,8 @@ struct rg_ctx {
   unsigned long long* cluster_part = nullptr;  // [blocks][kClusterStats]
   unsigned long long* cluster_stats = nullptr;  // [kClusterStats]
   unsigned long long* fix_acc = nullptr;        // sharded REF fix-up accumulator [4]
+  uint32_t cus = 0;                             // compute units (ring-kernel grid)
+  uint32_t* sink = nullptr;                     // 4 KiB for the ring kernel's placeholder stores
   std::string err;
 };
 
@@ -81,8 +83,16 @@ constexpr int wmax_for(int n) { return n <= 5 ? 4 : (n <= 10 ? 2 : 1); }
 // Tile shapes: {threads, words per thread}. Big tiles keep the per-launch count
 // of tiles and look-back hand-offs low on large windows; small tiles fill
 // the 256 CUs on single 2^20-slot windows.
-enum TileCfg { kCfgBig = 0, kCfgMid = 1, kCfgSmall = 2, kCfgBigW2 = 3, kCfgMidW2 = 4 };
-constexpr int cfg_block(int c) { return (c == kCfgBig || c == kCfgBigW2) ? 512 : (c == kCfgSmall ? 128 : 256); }
+// kCfgRing: the pipelined persistent kernel (ref_ring_kernel, 256 compute threads x W
+// words per tile + one control wave), REF rg_phase_step_async only.
+enum TileCfg { kCfgBig = 0, kCfgMid = 1, kCfgSmall = 2, kCfgBigW2 = 3, kCfgMidW2 = 4, kCfgRing = 5 };
+constexpr int kRingBlock = 256;
+#ifndef RG_RING_DEFAULT
+#define RG_RING_DEFAULT 0
+#endif
+constexpr int cfg_block(int c) {
+  return (c == kCfgBig || c == kCfgBigW2) ? 512 : (c == kCfgSmall ? 128 : 256);
+}
 inline int cfg_words(int c, int n) { return c == kCfgSmall ? 1 : (c >= kCfgBigW2 ? 2 : wmax_for(n)); }
 
 int pick_cfg(int n, uint64_t n_words) {
@@ -111,6 +121,19 @@ struct Disp {
     if (c == kCfgBig) hipLaunchKernelGGL((ref_step_kernel<N, WM, 512, false>), dim3(grid), dim3(512), 0, s, p);
     else if (c == kCfgMid) hipLaunchKernelGGL((ref_step_kernel<N, WM, 256, false>), dim3(grid), dim3(256), 0, s, p);
     else hipLaunchKernelGGL((ref_step_kernel<N, 1, 128, false>), dim3(grid), dim3(128), 0, s, p);
+  }
+  // ring grid: every WG resident (forward progress of the look-back), at most
+  // `per_cu` per CU, never more WGs than tiles
+  static uint32_t ring_grid(uint32_t cus, uint32_t per_cu, uint32_t n_tiles) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ref_ring_kernel<N, WM, kRingBlock>, kRingBlock + 64, 0) !=
+            hipSuccess || nb < 1)
+      nb = 1;
+    const uint32_t g = cus * ((uint32_t)nb < per_cu ? (uint32_t)nb : per_cu);
+    return g < n_tiles ? g : n_tiles;
+  }
+  static void ring(uint32_t grid, hipStream_t s, const StepParams& p) {
+    hipLaunchKernelGGL((ref_ring_kernel<N, WM, kRingBlock>), dim3(grid), dim3(kRingBlock + 64), 0, s, p);
   }
   static void wmvc(int c, uint32_t grid, hipStream_t s, const StepParams& p) {
     if (c == kCfgBig) hipLaunchKernelGGL((wmvc_step_kernel<N, WM, 512>), dim3(grid), dim3(512), 0, s, p);
@@ -151,6 +174,10 @@ using DigestLaunch = void (*)(uint32_t, hipStream_t, const uint64_t*, uint64_t, 
    &Disp<12>::fn, &Disp<13>::fn, &Disp<14>::fn, &Disp<15>::fn, &Disp<16>::fn}
 
 const StepLaunch kRefLaunch[17] = RG_TABLE(ref);
+using RingLaunch = void (*)(uint32_t, hipStream_t, const StepParams&);
+using RingGrid = uint32_t (*)(uint32_t, uint32_t, uint32_t);
+const RingLaunch kRingLaunch[17] = RG_TABLE(ring);
+const RingGrid kRingGrid[17] = RG_TABLE(ring_grid);
 const StepLaunch kWmvcLaunch[17] = RG_TABLE(wmvc);
 const DigestLaunch kDigestLaunch[17] = RG_TABLE(digest);
 const ClusterLaunch kClusterLaunch[17] = RG_TABLE(cluster);
@@ -318,6 +345,7 @@ int rg_destroy(rg_ctx* ctx) {
   (void)hipFree(ctx->cluster_part);
   (void)hipFree(ctx->cluster_stats);
   (void)hipFree(ctx->fix_acc);
+  (void)hipFree(ctx->sink);
   (void)hipFree(ctx->d_votes);
   (void)hipFree(ctx->d_out);
   (void)hipFree(ctx->d_user_result);
@@ -354,6 +382,9 @@ int rg_get_state(rg_ctx* ctx, rg_engine_state* st) {
   return RG_OK;
 }
 
+// Large REF launches take the ring kernel unless diag bit 15 asks for the tiled one.
+static bool ring_default(const rg_ctx* ctx) { return RG_RING_DEFAULT && !(ctx->diag & 0x8000u); }
+
 static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, uint64_t n_slots, uint64_t stride_words,
               uint64_t slot_base, uint64_t phase, uint64_t max_phase, rg_step_result* result_dev, void* stream,
               bool shard, uint64_t* records_dev, uint64_t records_cap) {
@@ -379,15 +410,37 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
   if (int rc = make_layout(ctx, 4 * n + 1, n_words, stride_words, &lin, &need_in, "rg_phase_step")) return rc;
   if (int rc = make_layout(ctx, kOutPlanes, n_words, stride_words, &lout, &need_out, "rg_phase_step")) return rc;
   uint32_t force = (ctx->diag >> 8) & 7u;  // diagnostics: force a tile shape
-  if (force > 3 && (n != 5 || wmvc || shard)) force = 0;
-  const int cfg = force ? (int)force - 1 : pick_cfg(n, n_words);
-  const uint64_t tile_words = (uint64_t)cfg_block(cfg) * cfg_words(cfg, n);
-  const uint64_t n_tiles = (n_words + tile_words - 1) / tile_words;
-  if (int rc = ensure_tiles(ctx, n_tiles, false)) return rc;
+  if ((force == 4 || force == 5) && (n != 5 || wmvc || shard)) force = 0;
+  if (force == 6 && (wmvc || shard)) force = 0;
+  int cfg = force ? (int)force - 1 : pick_cfg(n, n_words);
+  uint64_t tile_words = (uint64_t)cfg_block(cfg) * cfg_words(cfg, n);
+  uint64_t n_tiles = (n_words + tile_words - 1) / tile_words;
+  uint32_t ring_grid = 0;
+  if (!wmvc && !shard && (cfg == kCfgRing || (!force && ring_default(ctx)))) {
+    if (!ctx->sink) RG_HIP(ctx, hipMalloc(&ctx->sink, 4096));
+    if (!ctx->cus) {
+      int cus = 0;
+      RG_HIP(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->cfg.device));
+      ctx->cus = cus > 0 ? (uint32_t)cus : 1u;
+    }
+    const uint64_t rt = (n_words + (uint64_t)kRingBlock * wmax_for(n) - 1) / ((uint64_t)kRingBlock * wmax_for(n));
+    const uint32_t per_cu = (ctx->diag >> 12) & 3u ? (ctx->diag >> 12) & 3u : 2u;
+    const uint32_t gr = kRingGrid[n](ctx->cus, per_cu, (uint32_t)(rt < 0xFFFFFFFFull ? rt : 0xFFFFFFFFull));
+    // the pipeline pays off once every WG has a few tiles (forced: any size)
+    if (cfg == kCfgRing || rt >= 4ull * gr) {
+      cfg = kCfgRing;
+      tile_words = (uint64_t)kRingBlock * wmax_for(n);
+      n_tiles = rt;
+      ring_grid = gr;
+    }
+  }
+  // (the ring's per-WG records take 4 granules per WG of the 2 per tile allocated)
+  const uint64_t gran_tiles = n_tiles > 2ull * ring_grid ? n_tiles : 2ull * ring_grid;
+  if (int rc = ensure_tiles(ctx, gran_tiles, false)) return rc;
   // Statistics granules carry 12 bits of seq and look-back granules 31: start a
   // fresh epoch on zeroed granules whenever either wraps.
   if (++ctx->seq >= (1u << 31) || (ctx->seq & 0xFFFu) == 0) {
-    if (int rc = ensure_tiles(ctx, n_tiles, true)) return rc;
+    if (int rc = ensure_tiles(ctx, gran_tiles, true)) return rc;
     ctx->seq = 2 - (ctx->seq & 1u);  // keep the record-ring parity
   }
   StepParams p;
@@ -417,6 +470,7 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
   p.dbg = nullptr;
   p.vq_rec = reinterpret_cast<unsigned long long*>(records_dev);
   p.vq_cap = records_cap;
+  p.sink = ctx->sink;
   if (ctx->diag & 4u) {
     if (ctx->dbg_cap < n_tiles * 8) {
       RG_HIP(ctx, hipDeviceSynchronize());
@@ -430,6 +484,7 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
   }
   hipStream_t s = pick_stream(ctx, stream);
   if (shard) launch_ref_shard(n, cfg_block(cfg), cfg_words(cfg, n), (uint32_t)n_tiles, s, p);
+  else if (cfg == kCfgRing) kRingLaunch[n](ring_grid, s, p);
   else (wmvc ? kWmvcLaunch : kRefLaunch)[n](cfg, (uint32_t)n_tiles, s, p);
   RG_HIP(ctx, hipGetLastError());
   return RG_OK;

@@ -53,6 +53,7 @@ struct StepParams {
   unsigned long long* dbg;        // [n_tiles][8] s_memrealtime stamps when diag & 4
   unsigned long long* vq_rec;     // sharded REF: draw records [vq_cap] (rg_common.h)
   uint64_t vq_cap;
+  uint32_t* sink;                 // ring kernel: 4 KiB the prologue's placeholder stores go to
 };
 
 // finish_tile flavours
@@ -651,6 +652,34 @@ __device__ __forceinline__ void r2_decision(const uint32_t (&lo)[N][W], const ui
   dhi = dq | dn;
 }
 
+// The same with the own round-2 vote at lane `self` (engine.rs:540-542) selected
+// per lane instead of written into the plane registers: no runtime-indexed array
+// write (the ring kernel's register budget has no room for the scratch copy the
+// compiler otherwise keeps of the self lane's planes).
+template <int N, int W>
+__device__ __forceinline__ void r2_decision_own(const uint32_t (&lo)[N][W], const uint32_t (&hi)[N][W], int i,
+                                                uint32_t q, int self, uint32_t own, uint32_t pend, uint32_t& dlo,
+                                                uint32_t& dhi) {
+  constexpr int B = ctr_bits(N);
+  Ctr<B> c0, c1, cq;
+  ctr_zero(c0); ctr_zero(c1); ctr_zero(cq);
+#pragma unroll
+  for (int j = 0; j < N; j++) {
+    const bool me = j == self;
+    const uint32_t l = me ? ((lo[j][i] & pend) | (own & ~pend)) : lo[j][i];
+    const uint32_t h = me ? (hi[j][i] & pend) : hi[j][i];
+    ctr_add(c0, ~l & ~h);
+    ctr_add(c1, l & ~h);
+    ctr_add(cq, ~l & h);
+  }
+  const uint32_t d0 = ctr_ge(c0, q);
+  const uint32_t d1 = ~d0 & ctr_ge(c1, q);
+  const uint32_t dq = ~d0 & ~d1 & ctr_ge(cq, q);
+  const uint32_t dn = ~(d0 | d1 | dq);
+  dlo = d1 | dn;
+  dhi = dq | dn;
+}
+
 // SHARD = the sharded-REF flavour (rg_phase_step_shard_async): the draws come from
 // the shard's provisional stream position, every VQ slot also leaves a draw
 // record (its decision under both own votes) for rg_shard_fixup_async, and the
@@ -873,307 +902,323 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
 }
 
 // ============================================================================
-// Persistent REF step (large launches). G workgroups, all resident at once
-// (G = resident blocks per CU x CUs); WG g handles tiles g, g+G, g+2G, ... in
-// order. Software pipeline per WG: the next tile's R1 planes are loaded into the
-// registers of the current tile's R1 (dead after the tally) while this tile waits
-// for its look-back, and the next tile's R2 planes right after this tile's stores
-// — so a WG always has its next tile's bytes in flight and the look-back wait
-// overlaps HBM traffic instead of idling the CU. Statistics accumulate per WG in
-// registers; WG 0 folds the G per-WG records at the end. Forward progress: the
-// lowest unfinished tile's predecessors are all done and every WG is resident.
+// Pipelined persistent REF step (large launches of rg_phase_step_async). G
+// workgroups, all resident (G <= CUs x resident WGs per CU); WG g owns the tiles
+// g, g + G, g + 2G, ... in order. Each WG has BLOCK compute threads plus ONE
+// control wave and runs every tile in two halves one iteration apart:
+//   iteration j, compute waves: round 1 of tile j+1 (its R1 planes were loaded
+//     during iteration j-1), issue the R1 loads of tile j+2; barrier A(j); then
+//     draws + round 2 + stores of tile j (its R2 planes were loaded during
+//     iteration j-1) and issue the R2 loads of tile j+1.
+//   control wave, between A(j-1) and A(j): publish tile j's VQ count, look back
+//     for its exclusive prefix (one poll of up to 512 predecessor granules: the
+//     same-iteration predecessors publish theirs at about the same time and the
+//     previous iteration's last tile already holds an inclusive value), publish
+//     the inclusive value and compute tile j's first ChaCha12 blocks into LDS.
+// The look-back so has a whole tile period of slack and runs on a wave that holds
+// no plane loads (its polls never drain them), and the compute waves always have
+// the next tile's R1 or R2 planes in flight. Forward progress: a tile's look-back
+// needs only tiles published in the same or an earlier iteration, every WG is
+// resident (the host sizes G from the occupancy), and the spin is bounded
+// (Record.error -> RG_ESTATE). Statistics accumulate per WG in registers; WG 0
+// folds the G per-WG records.
 // ============================================================================
 // per-WG statistics record: 4 tagged granules (tag 12 bits at [52, 64))
 //   g0 = dec:26 | v1:26 << 26      g1 = pend:26 | draws:26 << 26
 //   g2 = (largest accepted V1 offset + 1, 0 = none):33   g3 = smallest undecided offset (2^33-1 = none):33
 constexpr int kPersistStatGranules = 4;
 constexpr unsigned long long kOff33 = (1ull << 33) - 1;
+constexpr int kRingBlk = 64;  // ChaCha12 blocks (512 draws) per tile prepared by the control wave
 __device__ __forceinline__ unsigned long long pstat_tag(uint32_t seq) {
   return (unsigned long long)(0x800u | (seq & 0x7FFu)) << 52;
 }
 
-// PREF = 1: the next tile's R1 loads are issued by waves 1.. during wave 0's
-// look-back; PREF = 0: by every wave right after the draws (fewer live registers
-// across the draws' ChaCha blocks).
-template <int N, int W, int BLOCK, bool SHARD, int PREF>
-__global__ __launch_bounds__(BLOCK, 4) void ref_persist_kernel(StepParams p) {
+// Plane loads without a branch: a thread past the window loads word 0 instead
+// (its valid masks are 0, so the values are never used). A conditional load makes
+// hipcc wait for it right away, which would drain the ring's prefetch.
+template <int N, int W>
+__device__ __forceinline__ void load_planes_any(const StepParams& p, uint64_t w0, int first_plane,
+                                                uint32_t (&lo)[N][W], uint32_t (&hi)[N][W]) {
+  const uint32_t* base = p.votes + p.lin.base(w0 < p.n_words ? w0 : 0);
+  const uint64_t ps = p.lin.pstride;
+#pragma unroll
+  for (int j = 0; j < N; j++) {
+    load_words<W>(base + (first_plane + 2 * j) * ps, lo[j]);
+    load_words<W>(base + (first_plane + 2 * j + 1) * ps, hi[j]);
+  }
+}
+
+// Round 1 of one tile (engine.rs:495-505) from the R1 registers: V1 / VQ /
+// pending masks, the VQ slots' (c1 > c0), (c1 < c0) masks into LDS, VQ count.
+template <int N, int W, int BLOCK>
+__device__ __forceinline__ uint32_t ring_tally(const StepParams& p, uint64_t w0, const uint32_t (&lo)[N][W],
+                                               const uint32_t (&hi)[N][W], uint32_t (*cls)[BLOCK], int tid,
+                                               uint32_t (&v1)[W], uint32_t (&vq)[W], uint32_t (&pd)[W]) {
   constexpr int B = ctr_bits(N);
-  constexpr int WAVES = BLOCK / 64;
-  constexpr uint64_t kTileWords = (uint64_t)BLOCK * W;
-  __shared__ uint32_t s_wave[WAVES];
-  __shared__ uint32_t s_excl;
-  __shared__ uint32_t s_cls[2 * W][BLOCK];  // c1 > c0 / c1 < c0 masks, parked across the look-back
-  __shared__ uint32_t s_blk[BLOCK][17];
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    const uint32_t vm = valid_mask(w0 + i, p.n_words, p.n_slots);
+    Ctr<B> c0, c1, cp;
+    ctr_zero(c0); ctr_zero(c1); ctr_zero(cp);
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      const uint32_t l = lo[j][i], h = hi[j][i];
+      ctr_add(c0, ~l & ~h);
+      ctr_add(c1, l & ~h);
+      ctr_add(cp, ~(l & h));
+    }
+    const uint32_t g0 = ctr_ge(c0, p.q), g1 = ctr_ge(c1, p.q), gp = ctr_ge(cp, p.q);
+    v1[i] = ~g0 & g1 & vm;
+    vq[i] = ~g0 & ~g1 & gp & vm;  // cq >= q implies present >= q
+    pd[i] = ~((g0 & vm) | v1[i] | vq[i]) & vm;
+    uint32_t gt, lt;
+    ctr_cmp(c1, c0, gt, lt);
+    cls[2 * i][tid] = gt & vq[i];
+    cls[2 * i + 1][tid] = lt & vq[i];
+    cnt += __builtin_popcount(vq[i]);
+  }
+  return cnt;
+}
+
+template <int N, int W, int BLOCK>
+__global__ __launch_bounds__(BLOCK + 64) void ref_ring_kernel(StepParams p) {
+  constexpr int WAVES = BLOCK / 64;  // compute waves; wave WAVES is the control wave
+  constexpr uint64_t kTW = (uint64_t)BLOCK * W;
+  __shared__ uint32_t s_wave[3][WAVES];        // per-wave inclusive VQ counts, by tile j % 3
+  __shared__ uint32_t s_excl[2];               // the tile's exclusive VQ prefix, by j % 2
+  __shared__ uint32_t s_cls[2][2 * W][BLOCK];  // (c1 > c0), (c1 < c0) of the VQ slots, by j % 2
+  __shared__ uint32_t s_blk[2][kRingBlk][17];  // the tile's first ChaCha12 blocks, by j % 2
   Record* rec = p.rec + (p.seq & 1u);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t G = gridDim.x;
-  uint32_t tile = blockIdx.x;
-  if (tile == 0 && tid == 0) atomic_store_agent(&p.rec[(p.seq + 1) & 1u].error.v, 0ull);
-  const uint32_t tw0 = (uint32_t)tid * W;
-  const unsigned long long k_base = SHARD ? p.state->shard_draws : p.state->rng_next;
+  const uint32_t G = gridDim.x, g = blockIdx.x;
+  const uint32_t nt = (p.n_tiles - g + G - 1) / G;  // this WG's tiles (>= 1: the host keeps G <= n_tiles)
+  if (g == 0 && tid == 0) atomic_store_agent(&p.rec[(p.seq + 1) & 1u].error.v, 0ull);
+  const unsigned long long k_base = p.state->rng_next;
   uint32_t a_dec = 0, a_v1 = 0, a_pend = 0, a_draws = 0;
   unsigned long long a_max1 = 0, a_min = kOff33;
 
-  uint32_t r1lo[N][W], r1hi[N][W], r2lo[N][W], r2hi[N][W];
-  {
-    const uint64_t w0 = (uint64_t)tile * kTileWords + tw0;
-    load_planes<N, W>(p, w0, w0 < p.n_words, 0, r1lo, r1hi);
-    load_planes<N, W>(p, w0, w0 < p.n_words, 2 * N, r2lo, r2hi);
-  }
-  for (;;) {
-    const uint64_t w0 = (uint64_t)tile * kTileWords + tw0;
-    const bool active = w0 < p.n_words;
-    const uint32_t next = tile + G;
-    const bool has_next = next < p.n_tiles;
-    const uint64_t nw0 = (uint64_t)next * kTileWords + tw0;
-
-    // ---- round 1 (engine.rs:495-505)
-    uint32_t r1v1[W], r1vq[W], pend[W];
-    uint32_t vq_count = 0;
+  if (wave == WAVES) {
+    // ---- control wave: tile j's prefix and first ChaCha blocks, for j = 0 .. nt-1
+    lds_barrier();  // A(-1): tile 0's counts are in s_wave[0]
+    for (uint32_t j = 0; j < nt; j++) {
+      const uint32_t tile = g + j * G;
+      uint32_t agg = 0;
 #pragma unroll
-    for (int i = 0; i < W; i++) {
-      const uint32_t vm = valid_mask(w0 + i, p.n_words, p.n_slots);
-      Ctr<B> c0, c1, cp;
-      ctr_zero(c0); ctr_zero(c1); ctr_zero(cp);
-#pragma unroll
-      for (int j = 0; j < N; j++) {
-        const uint32_t lo = r1lo[j][i], hi = r1hi[j][i];
-        ctr_add(c0, ~lo & ~hi);
-        ctr_add(c1, lo & ~hi);
-        ctr_add(cp, ~(lo & hi));
-      }
-      const uint32_t g0 = ctr_ge(c0, p.q), g1 = ctr_ge(c1, p.q), gp = ctr_ge(cp, p.q);
-      r1v1[i] = ~g0 & g1 & vm;
-      r1vq[i] = ~g0 & ~g1 & gp & vm;
-      pend[i] = ~((g0 & vm) | r1v1[i] | r1vq[i]) & vm;
-      uint32_t gt, lt;
-      ctr_cmp(c1, c0, gt, lt);
-      s_cls[2 * i][tid] = gt & r1vq[i];
-      s_cls[2 * i + 1][tid] = lt & r1vq[i];
-      vq_count += __builtin_popcount(r1vq[i]);
-    }
-    const uint32_t incl = wave_incl_scan32(vq_count, lane);
-    if (lane == 63) s_wave[wave] = incl;
-    lds_barrier();
-    uint32_t wave_off = 0, tile_total = 0;
-#pragma unroll
-    for (int w = 0; w < WAVES; w++) {
-      wave_off += (w < wave) ? s_wave[w] : 0u;
-      tile_total += s_wave[w];
-    }
-    // ---- look-back (wave 0) while waves 1.. prefetch the next tile's R1 planes
-    if (wave == 0) {
-      const uint32_t e = (p.diag & 1u) ? 0u
-                                       : lookback_exclusive(p.lookback, tile, p.seq, tile_total, lane, &rec->error.v);
-      if (lane == 0) s_excl = e;
-    } else if (PREF && has_next) {
-      load_planes<N, W>(p, nw0, nw0 < p.n_words, 0, r1lo, r1hi);
-    }
-    lds_barrier();
-    if (PREF && wave == 0 && has_next) load_planes<N, W>(p, nw0, nw0 < p.n_words, 0, r1lo, r1hi);
-
-    // ---- own round-2 vote: one StdRng draw per VQ slot (engine.rs:523-537, 567-611)
-    const unsigned long long k_tile = k_base + s_excl;
-    const unsigned long long k_first = k_tile + wave_off + incl - vq_count;
-    unsigned long long k = k_first;
-    uint32_t own_lo[W], mq[W];
-#pragma unroll
-    for (int i = 0; i < W; i++) {
-      own_lo[i] = r1v1[i];
-      mq[i] = r1vq[i];
-    }
-    if (tile_total) {
-      const unsigned long long b_first = k_tile >> 3, b_last = (k_tile + tile_total - 1) >> 3;
-      for (unsigned long long cb = b_first; cb <= b_last; cb += BLOCK) {
-        if (cb + tid <= b_last) {
+      for (int w = 0; w < WAVES; w++) agg += s_wave[j % 3][w];
+      const uint32_t excl = lookback_exclusive_wide<8>(p.lookback, tile, p.seq, agg, lane, &rec->error.v, 8, 8, 1);
+      if (agg) {
+        const unsigned long long kt = k_base + excl, b0 = kt >> 3, b1 = (kt + agg - 1) >> 3;
+        if (lane < kRingBlk && b0 + lane <= b1) {
           uint32_t x[16];
-          chacha_block<12>(p.key, cb + tid, 0, x);
+          chacha_block<12>(p.key, b0 + lane, 0, x);
 #pragma unroll
-          for (int j = 0; j < 16; j++) s_blk[tid][j] = x[j];
+          for (int k = 0; k < 16; k++) s_blk[j & 1][lane][k] = x[k];
         }
-        lds_barrier();
-        const unsigned long long k_lim = (cb + BLOCK) << 3;
+      }
+      if (lane == 0) s_excl[j & 1] = excl;
+      lds_barrier();  // A(j)
+    }
+  } else {
+    // ---- compute waves
+    const uint32_t tw0 = (uint32_t)tid * W;
+    uint32_t r1lo[N][W], r1hi[N][W], r2lo[N][W], r2hi[N][W];
+    uint32_t m_v1[W], m_vq[W], m_pend[W], m_cnt, m_incl;  // tile j's round-1 results
+    {
+      // The memory operations leave the prologue in the loop's steady-state order
+      // (R1 of the next tile, 8 stores, R2 of the current tile), so the counted
+      // waits hipcc derives at the loop entry (it merges the entry and back-edge
+      // states) are the steady-state ones and keep the prefetch in flight.
+      const uint64_t w0 = (uint64_t)g * kTW + tw0;
+      load_planes_any<N, W>(p, w0, 0, r1lo, r1hi);
+      m_cnt = ring_tally<N, W, BLOCK>(p, w0, r1lo, r1hi, s_cls[0], tid, m_v1, m_vq, m_pend);
+      m_incl = wave_incl_scan32(m_cnt, lane);
+      if (lane == 63) s_wave[0][wave] = m_incl;
+      load_planes_any<N, W>(p, w0 + (uint64_t)G * kTW, 0, r1lo, r1hi);
+      uint32_t* sk = p.sink + 4u * (g & 255u);
+#pragma unroll
+      for (int k = 0; k < 8; k++) store_words_nt<W>(sk, m_v1);  // placeholders, one 16-B slot per WG
+      load_planes_any<N, W>(p, w0, 2 * N, r2lo, r2hi);
+    }
+    lds_barrier();  // A(-1)
+    for (uint32_t j = 0; j < nt; j++) {
+      const uint64_t w0 = (uint64_t)(g + j * G) * kTW + tw0;
+      const uint64_t nw0 = w0 + (uint64_t)G * kTW;
+      uint32_t n_v1[W], n_vq[W], n_pend[W], n_cnt = 0, n_incl = 0;
+      if (j + 1 < nt) {  // round 1 of tile j+1
+        n_cnt = ring_tally<N, W, BLOCK>(p, nw0, r1lo, r1hi, s_cls[(j + 1) & 1], tid, n_v1, n_vq, n_pend);
+        n_incl = wave_incl_scan32(n_cnt, lane);
+        if (lane == 63) s_wave[(j + 1) % 3][wave] = n_incl;
+      }
+      // the R1 loads of tile j+2, unconditional (past the WG's last tile they read
+      // word 0 and are never used): loads under a branch make hipcc wait for every
+      // outstanding load at the next use, which would serialise the pipeline
+      load_planes_any<N, W>(p, nw0 + (uint64_t)G * kTW, 0, r1lo, r1hi);
+      lds_barrier();  // A(j): the control wave has tile j's prefix and first ChaCha blocks
+
+      // ---- own round-2 vote: one StdRng draw per VQ slot (engine.rs:523-537, 567-611)
+      const uint32_t* sw = s_wave[j % 3];
+      uint32_t wave_off = 0;
+#pragma unroll
+      for (int w = 0; w < WAVES - 1; w++) wave_off += (w < wave) ? sw[w] : 0u;
+      const unsigned long long k_tile = k_base + s_excl[j & 1];
+      unsigned long long k = k_tile + wave_off + m_incl - m_cnt;  // this thread's first draw
+      uint32_t own_lo[W];
+#pragma unroll
+      for (int i = 0; i < W; i++) own_lo[i] = m_v1[i];
+      if (m_cnt) {
+        const unsigned long long b0 = k_tile >> 3;
+        unsigned long long cached = ~0ull;
+        uint32_t xb[16];
 #pragma unroll
         for (int i = 0; i < W; i++) {
-          if (!mq[i] || k >= k_lim) continue;
-          const uint32_t gtm = s_cls[2 * i][tid], ltm = s_cls[2 * i + 1][tid];
-          while (mq[i] && k < k_lim) {
-            const int b = __builtin_ctz(mq[i]);
-            mq[i] &= mq[i] - 1;
-            const uint32_t row = (uint32_t)((k >> 3) - cb), ws = (uint32_t)(k & 7u) * 2u;
-            const unsigned long long u =
-                (unsigned long long)s_blk[row][ws] | ((unsigned long long)s_blk[row][ws + 1] << 32);
+          uint32_t mq = m_vq[i];
+          if (!mq) continue;
+          const uint32_t gtm = s_cls[j & 1][2 * i][tid], ltm = s_cls[j & 1][2 * i + 1][tid];
+          while (mq) {
+            const int b = __builtin_ctz(mq);
+            mq &= mq - 1;
+            const unsigned long long blk = k >> 3;
+            const uint32_t ws = (uint32_t)(k & 7u) * 2u;
+            unsigned long long u;
+            if (blk - b0 < (unsigned long long)kRingBlk) {
+              const uint32_t row = (uint32_t)(blk - b0);
+              u = (unsigned long long)s_blk[j & 1][row][ws] | ((unsigned long long)s_blk[j & 1][row][ws + 1] << 32);
+            } else {  // beyond the control wave's blocks: this thread's own (rare: > 512 draws in the tile)
+              if (blk != cached) {
+                chacha_block<12>(p.key, blk, 0, xb);
+                cached = blk;
+              }
+              u = 0;
+#pragma unroll
+              for (int z = 0; z < 8; z++)
+                if ((uint32_t)z * 2u == ws) u = (unsigned long long)xb[2 * z] | ((unsigned long long)xb[2 * z + 1] << 32);
+            }
             const bool gt = (gtm >> b) & 1u, lt = (ltm >> b) & 1u;
             const bool v1 = gt ? (u < kP90) : (lt ? (u >= kP90) : (u < kP80));
             own_lo[i] |= (uint32_t)v1 << b;
             k++;
           }
         }
-        lds_barrier();
       }
-    }
 
-    if (!PREF && has_next) load_planes<N, W>(p, nw0, nw0 < p.n_words, 0, r1lo, r1hi);
-
-    // ---- round 2, one word at a time (engine.rs:540-542, 613-628): only the
-    // decision masks stay live, so the R2 registers free up before the stores
-    unsigned long long kr = k_first - k_base;  // SHARD: local draw number of this thread's first VQ slot
-    uint32_t dlo[W], dhi[W];
+      // ---- own vote joins round2_votes (engine.rs:540-542); decision (613-628)
+      uint32_t dlo[W], dhi[W];
 #pragma unroll
-    for (int i = 0; i < W; i++) {
-      const uint32_t vm = valid_mask(w0 + i, p.n_words, p.n_slots);
-      if constexpr (SHARD) {
-        uint32_t alo = 0, ahi = 0;
-        if (r1vq[i]) {  // the decision under the other own vote, for the draw records
-#pragma unroll
-          for (int j = 0; j < N; j++)
-            if (j == p.self_lane) {
-              const uint32_t l = r2lo[j][i], h = r2hi[j][i];
-              r2lo[j][i] = (l & pend[i]) | ((own_lo[i] ^ r1vq[i]) & ~pend[i]);
-              r2hi[j][i] = h & pend[i];
-              r2_decision<N, W>(r2lo, r2hi, i, p.q, alo, ahi);
-              r2lo[j][i] = l;
-              r2hi[j][i] = h;
-            }
+      for (int i = 0; i < W; i++) {
+        const uint32_t vm = valid_mask(w0 + i, p.n_words, p.n_slots);
+        r2_decision_own<N, W>(r2lo, r2hi, i, p.q, p.self_lane, own_lo[i], m_pend[i], dlo[i], dhi[i]);
+        dlo[i] &= vm;
+        dhi[i] &= vm;
+        const uint32_t d1 = dlo[i] & ~dhi[i], dc = ~dhi[i] & vm;
+        a_dec += __builtin_popcount(dc);
+        a_v1 += __builtin_popcount(d1);
+        a_pend += __builtin_popcount(m_pend[i]);
+        const uint32_t v1l = d1 & phase_limit_mask(p.slot_base, w0 + i, p.max_phase);
+        if (v1l) {
+          const unsigned long long m1 = 32ull * (w0 + i) + (31u - __builtin_clz(v1l)) + 1u;
+          a_max1 = m1 > a_max1 ? m1 : a_max1;
         }
-#pragma unroll
-        for (int j = 0; j < N; j++)
-          if (j == p.self_lane) {
-            r2lo[j][i] = (r2lo[j][i] & pend[i]) | (own_lo[i] & ~pend[i]);
-            r2hi[j][i] &= pend[i];
-          }
-        r2_decision<N, W>(r2lo, r2hi, i, p.q, dlo[i], dhi[i]);
-        uint32_t m = r1vq[i];
-        if (m) {
-          const uint32_t gtm = s_cls[2 * i][tid], ltm = s_cls[2 * i + 1][tid];
-          while (m) {
-            const int b = __builtin_ctz(m);
-            m &= m - 1;
-            const uint32_t own = (own_lo[i] >> b) & 1u;
-            const uint32_t dp = ((dlo[i] >> b) & 1u) | (((dhi[i] >> b) & 1u) << 1);
-            const uint32_t da = ((alo >> b) & 1u) | (((ahi >> b) & 1u) << 1);
-            const uint32_t d_v0 = own ? da : dp, d_v1 = own ? dp : da;
-            const uint32_t cls = ((gtm >> b) & 1u) ? kRecGt : (((ltm >> b) & 1u) ? kRecLt : 0u);
-            const uint32_t info = cls | (d_v0 << 2) | (d_v1 << 4) | (own << 6);
-            const uint32_t off = (uint32_t)(32u * (w0 + i) + b);
-            if (kr < p.vq_cap) p.vq_rec[kr] = ((unsigned long long)info << 32) | off;
-            kr++;
-          }
+        const uint32_t und = ~dc & vm;
+        if (und) {
+          const unsigned long long mn = 32ull * (w0 + i) + __builtin_ctz(und);
+          a_min = mn < a_min ? mn : a_min;
         }
-      } else {
+      }
+      a_draws += m_cnt;
+      if (w0 < p.n_words) {  // plane by plane (include/rabia_gpu.h output planes)
+        uint32_t* ob = p.out + p.lout.base(w0);
+        const uint64_t ps = p.lout.pstride;
+        uint32_t v[W];
 #pragma unroll
-        for (int j = 0; j < N; j++)
-          if (j == p.self_lane) {
-            r2lo[j][i] = (r2lo[j][i] & pend[i]) | (own_lo[i] & ~pend[i]);
-            r2hi[j][i] &= pend[i];
-          }
-        r2_decision<N, W>(r2lo, r2hi, i, p.q, dlo[i], dhi[i]);
+        for (int i = 0; i < W; i++) v[i] = m_v1[i] | m_pend[i];
+        store_words_nt<W>(ob, v);
+#pragma unroll
+        for (int i = 0; i < W; i++) v[i] = m_vq[i] | m_pend[i];
+        store_words_nt<W>(ob + ps, v);
+#pragma unroll
+        for (int i = 0; i < W; i++) v[i] = own_lo[i] | m_pend[i];
+        store_words_nt<W>(ob + 2 * ps, v);
+        store_words_nt<W>(ob + 3 * ps, m_pend);
+        store_words_nt<W>(ob + 4 * ps, dlo);
+        store_words_nt<W>(ob + 5 * ps, dhi);
+#pragma unroll
+        for (int i = 0; i < W; i++) v[i] = ~dhi[i] & valid_mask(w0 + i, p.n_words, p.n_slots);
+        store_words_nt<W>(ob + 6 * ps, v);  // set_decision: committed iff not VQuestion
+#pragma unroll
+        for (int i = 0; i < W; i++) v[i] = dlo[i] & ~dhi[i];
+        store_words_nt<W>(ob + 7 * ps, v);  // V1: apply_batch + commit_phase
       }
-      dlo[i] &= vm;
-      dhi[i] &= vm;
-      const uint32_t d1 = dlo[i] & ~dhi[i], dc = ~dhi[i] & vm;
-      // statistics (SHARD: the fix-up counts the VQ slots)
-      const uint32_t keep = SHARD ? ~r1vq[i] : ~0u;
-      a_dec += __builtin_popcount(dc & keep);
-      const uint32_t v1k = d1 & keep;
-      a_v1 += __builtin_popcount(v1k);
-      a_pend += __builtin_popcount(pend[i]);
-      const uint32_t v1l = v1k & phase_limit_mask(p.slot_base, w0 + i, p.max_phase);
-      if (v1l) {
-        const unsigned long long m1 = 32ull * (w0 + i) + (31u - __builtin_clz(v1l)) + 1u;
-        a_max1 = m1 > a_max1 ? m1 : a_max1;
-      }
-      const uint32_t und = ~dc & vm & keep;
-      if (und) {
-        const unsigned long long mn = 32ull * (w0 + i) + __builtin_ctz(und);
-        a_min = mn < a_min ? mn : a_min;
+      load_planes_any<N, W>(p, nw0, 2 * N, r2lo, r2hi);  // tile j+1's R2 (unconditional, as above)
+      if (j + 1 < nt) {  // tile j+1 becomes current: its round-1 masks
+#pragma unroll
+        for (int i = 0; i < W; i++) {
+          m_v1[i] = n_v1[i];
+          m_vq[i] = n_vq[i];
+          m_pend[i] = n_pend[i];
+        }
+        m_cnt = n_cnt;
+        m_incl = n_incl;
       }
     }
-    a_draws += vq_count;
-    if (active) {  // plane by plane from the masks (include/rabia_gpu.h output planes)
-      uint32_t* ob = p.out + p.lout.base(w0);
-      const uint64_t ps = p.lout.pstride;
-      uint32_t v[W];
-#pragma unroll
-      for (int i = 0; i < W; i++) v[i] = r1v1[i] | pend[i];
-      store_words_nt<W>(ob, v);
-#pragma unroll
-      for (int i = 0; i < W; i++) v[i] = r1vq[i] | pend[i];
-      store_words_nt<W>(ob + ps, v);
-#pragma unroll
-      for (int i = 0; i < W; i++) v[i] = own_lo[i] | pend[i];
-      store_words_nt<W>(ob + 2 * ps, v);
-      store_words_nt<W>(ob + 3 * ps, pend);
-      store_words_nt<W>(ob + 4 * ps, dlo);
-      store_words_nt<W>(ob + 5 * ps, dhi);
-#pragma unroll
-      for (int i = 0; i < W; i++) v[i] = ~dhi[i] & valid_mask(w0 + i, p.n_words, p.n_slots);
-      store_words_nt<W>(ob + 6 * ps, v);  // set_decision: committed iff not VQuestion
-#pragma unroll
-      for (int i = 0; i < W; i++) v[i] = dlo[i] & ~dhi[i];
-      store_words_nt<W>(ob + 7 * ps, v);  // V1: apply_batch + commit_phase
-    }
-    if (!has_next) break;
-    load_planes<N, W>(p, nw0, nw0 < p.n_words, 2 * N, r2lo, r2hi);
-    tile = next;
   }
 
-  // ---- per-WG record, folded by WG 0
+  // ---- per-WG record (every wave; the control wave's counts are zero), folded by WG 0
   if (p.diag & 2u) return;
+  constexpr int TOTAL = BLOCK + 64;
   {
-    __shared__ unsigned long long red[WAVES][4];
-    const unsigned long long packed = (unsigned long long)a_dec | ((unsigned long long)a_v1 << 26);
-    const unsigned long long packed2 = (unsigned long long)a_pend | ((unsigned long long)a_draws << 26);
-    const unsigned long long s0 = wave_sum64(packed), s1 = wave_sum64(packed2);
+    __shared__ unsigned long long red[WAVES + 1][4];
+    const unsigned long long s0 = wave_sum64((unsigned long long)a_dec | ((unsigned long long)a_v1 << 26));
+    const unsigned long long s1 = wave_sum64((unsigned long long)a_pend | ((unsigned long long)a_draws << 26));
     const unsigned long long mx = wave_max64(a_max1), mn = wave_min64(a_min);
     if (lane == 0) { red[wave][0] = s0; red[wave][1] = s1; red[wave][2] = mx; red[wave][3] = mn; }
     lds_barrier();
     if (tid == 0) {
       unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = kOff33;
 #pragma unroll
-      for (int w = 0; w < WAVES; w++) {
+      for (int w = 0; w <= WAVES; w++) {
         t0 += red[w][0]; t1 += red[w][1];
         t2 = red[w][2] > t2 ? red[w][2] : t2;
         t3 = red[w][3] < t3 ? red[w][3] : t3;
       }
       const unsigned long long tag = pstat_tag(p.seq);
-      unsigned long long* g = p.stats + (uint64_t)blockIdx.x * kPersistStatGranules;
-      atomic_store_agent(g + 0, tag | t0);
-      atomic_store_agent(g + 1, tag | t1);
-      atomic_store_agent(g + 2, tag | t2);
-      atomic_store_agent(g + 3, tag | t3);
+      unsigned long long* gr = p.stats + (uint64_t)g * kPersistStatGranules;
+      atomic_store_agent(gr + 0, tag | t0);
+      atomic_store_agent(gr + 1, tag | t1);
+      atomic_store_agent(gr + 2, tag | t2);
+      atomic_store_agent(gr + 3, tag | t3);
     }
   }
-  if (blockIdx.x != 0) return;
+  if (g != 0) return;
   unsigned long long v[7] = {0, 0, 0, 0, 0, ~0ull, 0};  // dec v1 pend draws max(id+1) min(id) fault
   const unsigned long long tag = pstat_tag(p.seq);
   constexpr unsigned long long kTagMask = ~0ull << 52, kMask26 = (1ull << 26) - 1;
-  for (uint32_t wg = tid; wg < G; wg += BLOCK) {
+  for (uint32_t wg = tid; wg < G; wg += TOTAL) {
     unsigned long long* gp = p.stats + (uint64_t)wg * kPersistStatGranules;
-    unsigned long long g[4];
+    unsigned long long gv[4];
 #pragma unroll
-    for (int k2 = 0; k2 < 4; k2++) g[k2] = atomic_load_agent(gp + k2);
+    for (int k2 = 0; k2 < 4; k2++) gv[k2] = atomic_load_agent(gp + k2);
     uint32_t spins = 0;
     for (;;) {
       bool ready = true;
 #pragma unroll
-      for (int k2 = 0; k2 < 4; k2++) ready &= (g[k2] & kTagMask) == tag;
+      for (int k2 = 0; k2 < 4; k2++) ready &= (gv[k2] & kTagMask) == tag;
       if (ready) break;
       if (++spins > kSpinLimit) { v[6] = 2; break; }
       __builtin_amdgcn_s_sleep(2);
 #pragma unroll
       for (int k2 = 0; k2 < 4; k2++)
-        if ((g[k2] & kTagMask) != tag) g[k2] = atomic_load_agent(gp + k2);
+        if ((gv[k2] & kTagMask) != tag) gv[k2] = atomic_load_agent(gp + k2);
     }
-    v[0] += g[0] & kMask26;
-    v[1] += (g[0] >> 26) & kMask26;
-    v[2] += g[1] & kMask26;
-    v[3] += (g[1] >> 26) & kMask26;
-    const unsigned long long mx = g[2] & kOff33, mn = g[3] & kOff33;
+    v[0] += gv[0] & kMask26;
+    v[1] += (gv[0] >> 26) & kMask26;
+    v[2] += gv[1] & kMask26;
+    v[3] += (gv[1] >> 26) & kMask26;
+    const unsigned long long mx = gv[2] & kOff33, mn = gv[3] & kOff33;
     if (mx && p.slot_base + mx > v[4]) v[4] = p.slot_base + mx;
     if (mn != kOff33 && p.slot_base + mn < v[5]) v[5] = p.slot_base + mn;
   }
-  block_reduce_totals<BLOCK>(v, lane, wave);
+  block_reduce_totals<TOTAL>(v, lane, wave);
   if (tid != 0) return;
   const unsigned long long err = atomicAdd(&rec->error.v, 0ull) | v[6];
   DevState st = *p.state;
@@ -1185,28 +1230,19 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_persist_kernel(StepParams p) {
   r.n_draws = v[3];
   const unsigned long long end = p.slot_base + p.n_slots;
   const unsigned long long fu = v[5] < end ? v[5] : end;
-  if constexpr (SHARD) {
-    r.last_committed_max = v[4] ? v[4] - 1 : 0;
-    r.first_undecided = fu;
-    r.rng_next = st.shard_draws + r.n_draws;
-    r.commit_watermark = 0;
-    r.flags = err;
-    st.shard_draws = r.rng_next;
-  } else {
-    unsigned long long lc = st.last_committed;  // commit_phase: monotonic max, state.rs:77-99
-    if (v[4] && v[4] - 1 > lc) lc = v[4] - 1;
-    unsigned long long wm = st.commit_watermark;
-    if (p.slot_base <= wm && wm < fu) wm = fu;
-    r.last_committed_max = lc;
-    r.first_undecided = fu;
-    r.rng_next = st.rng_next + r.n_draws;
-    r.commit_watermark = wm;
-    r.flags = err;
-    st.rng_next = r.rng_next;
-    st.last_committed = lc;
-    st.commit_watermark = wm;
-    st.steps += 1;
-  }
+  unsigned long long lc = st.last_committed;  // commit_phase: monotonic max, state.rs:77-99
+  if (v[4] && v[4] - 1 > lc) lc = v[4] - 1;
+  unsigned long long wm = st.commit_watermark;
+  if (p.slot_base <= wm && wm < fu) wm = fu;
+  r.last_committed_max = lc;
+  r.first_undecided = fu;
+  r.rng_next = st.rng_next + r.n_draws;
+  r.commit_watermark = wm;
+  r.flags = err;
+  st.rng_next = r.rng_next;
+  st.last_committed = lc;
+  st.commit_watermark = wm;
+  st.steps += 1;
   *p.state = st;
   *p.result = r;
   if (p.result_user) *p.result_user = r;

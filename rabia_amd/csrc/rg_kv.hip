@@ -90,8 +90,22 @@ struct KvCounters {
   unsigned long long batch_base;  // heap top before the batch (keyed commit offsets)
 };
 
-// Per-block partials of the plan / commit walks.
+// Per-block partials of the plan walk.
 enum { kPCreated = 0, kPNewSlots, kPOverflow, kPLiveDelta, kPVersion, kPOps, kPNeed, kPCount };
+
+// What the commit writes for one key, decided by the plan (one record per distinct
+// key of a hash run, at the run head's sorted position + the key's rank in the run).
+struct KeyRec {
+  int64_t slot;         // table slot (-1: the key gets a new slot)
+  uint64_t ver1;        // version after the batch (0 = not live)
+  uint64_t hash;        // full key hash (claiming the new slot)
+  uint64_t key_src;     // batch data offset of the key bytes (new slot)
+  uint64_t val_src;     // batch data offset of the final value
+  uint64_t val_dst;     // heap offset of the slot's current value (in-place write)
+  uint32_t key_len, val_len;
+  uint32_t flags, pad;
+};
+enum : uint32_t { kRecNew = 1, kRecValue = 2, kRecInPlace = 4, kRecVersion = 8, kRecLast = 16 };
 constexpr int kWalkPerLane = 4;                              // sorted positions per walker lane
 constexpr int kWalkSpan = 64 * kWalkPerLane;                 // positions per wave
 constexpr int kWalkBlockSpan = kBlock * kWalkPerLane;        // positions per block
@@ -173,8 +187,8 @@ __device__ __forceinline__ void bytes_copy(uint8_t* dst, const uint8_t* src, uin
 // ---- 1 decode ----------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void kv_decode_kernel(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ off, uint64_t n, const uint8_t* __restrict__ mask,
-    uint64_t max_value, uint64_t hmask, uint64_t bmask, uint64_t invalid_bucket, KvOp* __restrict__ ops,
-    uint64_t* __restrict__ sort_key,
+    uint64_t max_value, uint64_t hmask, uint64_t bmask, uint32_t invalid_bucket, KvOp* __restrict__ ops,
+    uint32_t* __restrict__ sort_key,
     uint64_t* __restrict__ full_hash, uint32_t* __restrict__ sort_idx, uint8_t* __restrict__ results,
     unsigned long long* __restrict__ set_part) {
   const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -221,7 +235,7 @@ __global__ __launch_bounds__(kBlock) void kv_decode_kernel(
     }
   }
   ops[c] = op;
-  sort_key[c] = key == kInvalidKey ? invalid_bucket : hash_bucket(key, bmask);
+  sort_key[c] = key == kInvalidKey ? invalid_bucket : (uint32_t)hash_bucket(key, bmask);
   full_hash[c] = key;
   sort_idx[c] = (uint32_t)c;
   if (op.status != kPending) results[c] = (uint8_t)op.status;
@@ -246,17 +260,30 @@ __global__ __launch_bounds__(kBlock) void kv_decode_kernel(
 }
 
 // ---- table lookup ------------------------------------------------------------
-// Returns the slot holding `key` (live or not) or -1. Linear probing; an empty
-// slot ends the chain. Concurrent inserts by other walkers carry other hashes.
+// Returns the slot holding `key` (live or not) or -1, and its entry in *out.
+// Linear probing; an empty slot ends the chain. Concurrent inserts by other walkers
+// carry other hashes. Entries are read with agent-scope loads: plain loads of
+// entries the previous batch's commit wrote field by field were measured to return
+// stale fields on the next batch (a version or value length of 0 on a live key).
 __device__ int64_t table_find(const uint64_t* hashes, const KvEntry* ent, const uint8_t* heap,
-                              uint64_t mask, uint64_t h, const uint8_t* key, uint32_t klen) {
+                              uint64_t mask, uint64_t h, const uint8_t* key, uint32_t klen, KvEntry* out) {
   uint64_t s = h & mask;
   for (uint64_t probes = 0; probes <= mask; probes++) {
     const uint64_t th = __hip_atomic_load(hashes + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (th == kEmpty) return -1;
     if (th == h) {
-      const KvEntry e = ent[s];
-      if (e.key_len == klen && bytes_eq(heap + e.key_off, key, klen)) return (int64_t)s;
+      KvEntry e;
+      const unsigned long long* ep = reinterpret_cast<const unsigned long long*>(ent + s);
+      e.key_off = __hip_atomic_load(ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      e.val_off = __hip_atomic_load(ep + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      e.version = __hip_atomic_load(ep + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long lens = __hip_atomic_load(ep + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      e.key_len = (uint32_t)lens;
+      e.val_len = (uint32_t)(lens >> 32);
+      if (e.key_len == klen && bytes_eq(heap + e.key_off, key, klen)) {
+        *out = e;
+        return (int64_t)s;
+      }
     }
     s = (s + 1) & mask;
   }
@@ -290,15 +317,16 @@ struct StoreView {
 struct BatchView {
   const uint8_t* data;
   const KvOp* ops;
-  const uint64_t* skey;   // sorted hash buckets
+  const uint32_t* skey;   // sorted hash buckets
   const uint64_t* hfull;  // full key hash per command index
   const uint32_t* sidx;   // command index per sorted position
   uint64_t n;
   uint8_t* results;
-  uint8_t* done;          // per sorted position: handled by an earlier key of its run
+  uint8_t* done;          // per sorted position: handled by an earlier key of its run (multi-key runs)
   uint64_t* need;         // per sorted position: plan bytes (run heads only)
   uint64_t* block_base;   // per walk block: heap offset of its first byte (decide's scan)
-  uint64_t invalid_bucket;  // sort key of the commands that are not applied (sorted last)
+  KeyRec* recs;           // per sorted position: plan -> commit records (run head + key rank)
+  uint32_t invalid_bucket;  // sort key of the commands that are not applied (sorted last)
   unsigned long long* part;  // [blocks][kPCount]
 };
 
@@ -306,52 +334,79 @@ __device__ __forceinline__ bool same_key(const BatchView& b, const KvOp& x, cons
   return x.key_len == y.key_len && bytes_eq(b.data + x.key_off, b.data + y.key_off, x.key_len);
 }
 
-// Replay one key's commands [first .. run_end) (those equal to the leader's key)
-// in total order. Returns the final state; writes results when COMMIT.
+// One key's replay state over its commands in total order.
 struct KeyOutcome {
   bool live0, live1, wrote_value, any_set;
-  uint64_t ver1;
+  uint64_t ver0, ver1;
   uint32_t last_set;     // command index of the final value's SET
   uint64_t n_ops, n_version;
 };
 
-template <bool COMMIT>
-__device__ KeyOutcome replay_key(const BatchView& b, const StoreView& st, uint64_t first,
-                                 uint64_t run_end, const KvOp& lead, int64_t slot,
-                                 bool mark_done) {
+__device__ __forceinline__ KeyOutcome key_start(int64_t slot, const KvEntry& e) {
   KeyOutcome o{};
-  o.live0 = slot >= 0 && st.ent[slot].version > 0;
-  bool live = o.live0;
-  uint64_t ver = o.live0 ? st.ent[slot].version : 0;
-  for (uint64_t i = first; i < run_end; i++) {
-    if (b.done[i]) continue;
-    const uint32_t c = b.sidx[i];
-    const KvOp op = b.ops[c];
-    if (i != first && !same_key(b, op, lead)) continue;
-    if (mark_done) b.done[i] = 1;
-    uint8_t r;
-    if (op.kind == 0) {                 // SET: update or insert (store.rs:151-163)
-      ver = live ? ver + 1 : 1;
-      live = true;
-      o.wrote_value = true;
-      o.any_set = true;
-      o.last_set = c;
-      o.n_version += st.notify;
-      r = RG_KV_SUCCESS;
-    } else if (op.kind == 2) {          // DELETE (store.rs:220-251)
-      r = live ? RG_KV_SUCCESS : RG_KV_NOT_FOUND;
-      if (live) o.n_version += st.notify;
-      if (live) o.wrote_value = false;
-      live = false;
-    } else {                            // GET / EXISTS (smr_impl.rs:79-94)
-      r = live ? RG_KV_SUCCESS : RG_KV_NOT_FOUND;
-    }
-    o.n_ops++;
-    if (COMMIT) b.results[c] = r;
-  }
-  o.live1 = live;
-  o.ver1 = ver;
+  o.live0 = o.live1 = slot >= 0 && e.version > 0;
+  o.ver0 = o.ver1 = o.live0 ? e.version : 0;
   return o;
+}
+
+// Applies one command of the key; returns its result code.
+__device__ __forceinline__ uint8_t key_step(KeyOutcome& o, uint32_t kind, uint32_t c, uint32_t notify) {
+  uint8_t r;
+  if (kind == 0) {                    // SET: update or insert (store.rs:151-163)
+    o.ver1 = o.live1 ? o.ver1 + 1 : 1;
+    o.live1 = true;
+    o.wrote_value = true;
+    o.any_set = true;
+    o.last_set = c;
+    o.n_version += notify;
+    r = RG_KV_SUCCESS;
+  } else if (kind == 2) {             // DELETE (store.rs:220-251)
+    r = o.live1 ? RG_KV_SUCCESS : RG_KV_NOT_FOUND;
+    if (o.live1) {
+      o.n_version += notify;
+      o.wrote_value = false;
+    }
+    o.live1 = false;
+    o.ver1 = 0;
+  } else {                            // GET / EXISTS (smr_impl.rs:79-94)
+    r = o.live1 ? RG_KV_SUCCESS : RG_KV_NOT_FOUND;
+  }
+  o.n_ops++;
+  return r;
+}
+
+// Folds a replayed key into the block partials and its commit record; returns the
+// heap bytes the commit will take for it (new key bytes + a new value allocation).
+__device__ uint64_t plan_key(const BatchView& b, const KeyOutcome& o, int64_t slot, const KvEntry& e,
+                             const KvOp& lead, uint64_t hl, unsigned long long (&acc)[kPCount], KeyRec& r) {
+  acc[kPOps] += o.n_ops;
+  acc[kPVersion] += o.n_version;
+  acc[kPLiveDelta] += (unsigned long long)((int64_t)o.live1 - (int64_t)o.live0);
+  acc[kPCreated] += !o.live0 && o.any_set;  // keys live at some point of the batch (bound on data.len())
+  const bool new_slot = slot < 0 && o.live1;
+  acc[kPNewSlots] += new_slot;
+  const bool value = o.live1 && o.wrote_value;
+  uint64_t vsrc = 0;
+  uint32_t vlen = 0;
+  if (value) {
+    const KvOp v = b.ops[o.last_set];
+    vsrc = v.val_off;
+    vlen = v.val_len;
+  }
+  // in place when the final value's class fits the slot's current allocation
+  const bool in_place = value && slot >= 0 && val_class(vlen) <= val_class(e.val_len);
+  r.slot = slot;
+  r.ver1 = o.live1 ? o.ver1 : 0;
+  r.hash = hl;
+  r.key_src = lead.key_off;
+  r.val_src = vsrc;
+  r.val_dst = e.val_off;
+  r.key_len = lead.key_len;
+  r.val_len = vlen;
+  r.flags = (new_slot ? kRecNew : 0u) | (value ? kRecValue : 0u) | (in_place ? kRecInPlace : 0u) |
+            ((slot >= 0 || new_slot) && (o.any_set || o.live0 != o.live1) ? kRecVersion : 0u);
+  r.pad = 0;
+  return (new_slot ? lead.key_len : 0) + (value && !in_place ? val_class(vlen) : 0);
 }
 
 __device__ __forceinline__ void block_add_partials(unsigned long long (&v)[kPCount],
@@ -373,129 +428,226 @@ __device__ __forceinline__ void block_add_partials(unsigned long long (&v)[kPCou
 }
 
 // ---- 3 plan / 5 commit -------------------------------------------------------
-// Each wave owns kWalkSpan consecutive sorted positions; its lanes find the run
-// heads among them (ballots), compact them into LDS and each lane walks one head
-// at a time, so every lane has a run (a run starts at a head and may extend past
-// the wave's span). Plan sizes the heap bytes each run writes; the block totals go
-// to the partials and decide scans them into per-block bases; commit re-derives
-// the same lanes' offsets by a block scan of their plan sizes.
-template <bool COMMIT>
-__global__ __launch_bounds__(kBlock) void kv_walk_kernel(BatchView b, StoreView st) {
-  __shared__ uint16_t s_heads[kBlock / 64][kWalkSpan];
-  __shared__ unsigned long long s_wsum[kBlock / 64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  unsigned long long acc[kPCount] = {0, 0, 0, 0, 0, 0, 0};
-  const bool go = !COMMIT || st.ctr->mode == 0;
-  const uint64_t wbase = ((uint64_t)blockIdx.x * (kBlock / 64) + wave) * kWalkSpan;
+// Each wave owns kWalkSpan consecutive sorted positions (a block kWalkBlockSpan).
+// Plan: every lane first loads its positions' command index and kind and whether
+// the command's key equals the previous position's (phase A, all loads in
+// parallel, kept in LDS); the run heads are compacted per wave and each lane then
+// replays one head's run at a time out of LDS (phase B): one table lookup per key,
+// results written, and a KeyRec telling the commit what to write. A run that holds
+// several keys (a bucket collision) or continues past the block takes the general
+// path over global memory. The block totals go to the partials; decide scans the
+// plan bytes into per-block bases and commit, a separate launch over the same
+// heads, writes table entries and heap bytes from the records at offsets from a
+// block scan of the plan sizes: no lookups, no replay.
+__device__ __forceinline__ uint32_t collect_heads(const BatchView& b, uint64_t wbase, int lane, bool go,
+                                                  uint16_t* heads) {
   uint32_t nh = 0;
 #pragma unroll
   for (int k = 0; k < kWalkPerLane; k++) {
     const uint64_t i = wbase + 64 * k + lane;
     bool head = false;
     if (go && i < b.n) {
-      const uint64_t h = b.skey[i];
+      const uint32_t h = b.skey[i];
       head = h != b.invalid_bucket && (i == 0 || b.skey[i - 1] != h);
     }
+    const unsigned long long m = __ballot(head);
+    if (head) heads[nh + __builtin_popcountll(m & ((1ull << lane) - 1ull))] = (uint16_t)(64 * k + lane);
+    nh += (uint32_t)__builtin_popcountll(m);
+  }
+  __builtin_amdgcn_wave_barrier();
+  return nh;
+}
+
+enum : uint8_t { kInfCont = 4, kInfSame = 8 };  // bits 0-1: kind
+
+__global__ __launch_bounds__(kBlock) void kv_plan_kernel(BatchView b, StoreView st) {
+  __shared__ uint32_t s_c[kWalkBlockSpan];
+  __shared__ uint8_t s_inf[kWalkBlockSpan];
+  __shared__ uint16_t s_heads[kBlock / 64][kWalkSpan];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  unsigned long long acc[kPCount] = {0, 0, 0, 0, 0, 0, 0};
+  const uint64_t bbase = (uint64_t)blockIdx.x * kWalkBlockSpan;
+  const uint32_t wl = (uint32_t)wave * kWalkSpan;
+  // phase A: per position, command index, kind, continues / same key as previous
+  uint32_t nh = 0;
+#pragma unroll
+  for (int k = 0; k < kWalkPerLane; k++) {
+    const uint32_t l = wl + 64 * k + lane;
+    const uint64_t i = bbase + l;
+    bool head = false;
+    uint32_t c = 0, inf = 0;
+    if (i < b.n) {
+      const uint32_t h = b.skey[i];
+      if (h != b.invalid_bucket) {
+        const bool cont = i > 0 && b.skey[i - 1] == h;
+        head = !cont;
+        c = b.sidx[i];
+        const KvOp op = b.ops[c];
+        inf = op.kind & 3u;
+        if (cont) {
+          const uint32_t cp = b.sidx[i - 1];
+          const KvOp pp = b.ops[cp];
+          const bool eq = b.hfull[c] == b.hfull[cp] && same_key(b, op, pp);
+          inf |= kInfCont | (eq ? kInfSame : 0u);
+        }
+      }
+    }
+    s_c[l] = c;
+    s_inf[l] = (uint8_t)inf;
     const unsigned long long m = __ballot(head);
     if (head) s_heads[wave][nh + __builtin_popcountll(m & ((1ull << lane) - 1ull))] = (uint16_t)(64 * k + lane);
     nh += (uint32_t)__builtin_popcountll(m);
   }
-  __builtin_amdgcn_wave_barrier();
-  uint64_t heap_pos = 0;
-  if (COMMIT) {  // this lane's heap offset: block base + exclusive prefix of plan sizes over (wave, lane)
-    unsigned long long mine = 0;
-    for (uint32_t h = lane; h < nh; h += 64) mine += b.need[wbase + s_heads[wave][h]];
-    unsigned long long incl = mine;
-    for (int o = 1; o < 64; o <<= 1) {
-      const unsigned long long t = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += t;
-    }
-    if (lane == 63) s_wsum[wave] = incl;
-    __syncthreads();
-    unsigned long long before = 0;
-    for (int w = 0; w < wave; w++) before += s_wsum[w];
-    if (go) heap_pos = st.ctr->batch_base + b.block_base[blockIdx.x] + before + incl - mine;
-  }
+  __syncthreads();
+  // phase B: one run per lane at a time
   for (uint32_t h = lane; h < nh; h += 64) {
-    const uint64_t i = wbase + s_heads[wave][h];
-    const uint64_t hb = b.skey[i];
-    uint64_t end = i + 1;
-    while (end < b.n && b.skey[end] == hb) end++;
+    const uint32_t l0 = wl + s_heads[wave][h];
+    const uint64_t i = bbase + l0;
+    uint32_t l = l0 + 1;
+    bool single = true;
+    while (l < (uint32_t)kWalkBlockSpan && (s_inf[l] & kInfCont)) {
+      single = single && (s_inf[l] & kInfSame);
+      l++;
+    }
+    if (l == (uint32_t)kWalkBlockSpan && bbase + l < b.n && b.skey[bbase + l] == b.skey[i]) single = false;
     uint64_t need = 0;
-    int keys = 0;
-    for (uint64_t first = i; first < end; first++) {
-      if (b.done[first]) continue;
-      if (++keys > kMaxRunKeys) { acc[kPOverflow] = 1; break; }
-      const KvOp lead = b.ops[b.sidx[first]];
-      const uint64_t hl = b.hfull[b.sidx[first]];
-      const uint8_t* kp = b.data + lead.key_off;
-      const int64_t slot = table_find(st.hashes, st.ent, st.heap, st.mask, hl, kp, lead.key_len);
-      const KeyOutcome o = replay_key<COMMIT>(b, st, first, end, lead, slot, true);
-      acc[kPOps] += o.n_ops;
-      acc[kPVersion] += o.n_version;
-      acc[kPLiveDelta] += (unsigned long long)((int64_t)o.live1 - (int64_t)o.live0);
-      // keys that become live at some point of the batch (bound on data.len())
-      acc[kPCreated] += !o.live0 && o.any_set;
-      const bool new_slot = slot < 0 && o.live1;
-      acc[kPNewSlots] += new_slot;
-      const uint64_t kbytes = new_slot ? lead.key_len : 0;
-      const uint64_t vlen = (o.live1 && o.wrote_value) ? b.ops[o.last_set].val_len : 0;
-      // in place when the final value's class fits the slot's current allocation
-      const bool in_place = slot >= 0 && o.live1 && o.wrote_value && val_class(vlen) <= val_class(st.ent[slot].val_len);
-      const uint64_t vbytes = (o.live1 && o.wrote_value && !in_place) ? val_class(vlen) : 0;
-      need += kbytes + vbytes;
-      if (COMMIT) {
-        int64_t s = slot;
-        if (new_slot) {
-          s = table_claim(st.hashes, st.mask, hl);
-          if (s < 0) { atomicOr(&st.ctr->flags, kFaultTable); continue; }
-          bytes_copy(st.heap + heap_pos, kp, lead.key_len);
-          st.ent[s].key_off = heap_pos;
-          st.ent[s].key_len = lead.key_len;
-          st.ent[s].val_len = 0;
-          heap_pos += kbytes;
+    if (single) {  // one key, every command in LDS
+      const uint32_t c0 = s_c[l0];
+      const KvOp lead = b.ops[c0];
+      const uint64_t hl = b.hfull[c0];
+      KvEntry e{};
+      const int64_t slot = table_find(st.hashes, st.ent, st.heap, st.mask, hl, b.data + lead.key_off,
+                                      lead.key_len, &e);
+      KeyOutcome o = key_start(slot, e);
+      for (uint32_t q = l0; q < l; q++) {
+        const uint32_t c = s_c[q];
+        b.results[c] = key_step(o, s_inf[q] & 3u, c, st.notify);
+      }
+      KeyRec r;
+      need = plan_key(b, o, slot, e, lead, hl, acc, r);
+      r.flags |= kRecLast;
+      b.recs[i] = r;
+    } else {       // general: split the bucket run into keys by their bytes
+      const uint32_t hb = b.skey[i];
+      uint64_t end = i + 1;
+      while (end < b.n && b.skey[end] == hb) end++;
+      uint32_t keys = 0;
+      KeyRec r;
+      for (uint64_t first = i; first < end; first++) {
+        if (b.done[first]) continue;
+        if (keys == (uint32_t)kMaxRunKeys) { acc[kPOverflow] = 1; break; }
+        if (keys) b.recs[i + keys - 1] = r;
+        keys++;
+        const uint32_t c0 = b.sidx[first];
+        const KvOp lead = b.ops[c0];
+        const uint64_t hl = b.hfull[c0];
+        KvEntry e{};
+        const int64_t slot = table_find(st.hashes, st.ent, st.heap, st.mask, hl, b.data + lead.key_off,
+                                        lead.key_len, &e);
+        KeyOutcome o = key_start(slot, e);
+        for (uint64_t q = first; q < end; q++) {
+          if (b.done[q]) continue;
+          const uint32_t c = b.sidx[q];
+          const KvOp op = b.ops[c];
+          if (q != first && !(b.hfull[c] == hl && same_key(b, op, lead))) continue;
+          b.done[q] = 1;
+          b.results[c] = key_step(o, op.kind, c, st.notify);
         }
-        if (s >= 0 && (o.live0 || o.live1)) {
-          if (o.live1 && o.wrote_value) {
-            const KvOp& sop = b.ops[o.last_set];
-            if (!in_place) {
-              st.ent[s].val_off = heap_pos;
-              heap_pos += vbytes;
-            }
-            bytes_copy(st.heap + st.ent[s].val_off, b.data + sop.val_off, sop.val_len);
-            st.ent[s].val_len = sop.val_len;
-          }
-          st.ent[s].version = o.live1 ? o.ver1 : 0;
-        }
+        need += plan_key(b, o, slot, e, lead, hl, acc, r);
+      }
+      if (keys) {
+        r.flags |= kRecLast;
+        b.recs[i + keys - 1] = r;
       }
     }
-    if (!COMMIT) b.need[i] = need;
+    b.need[i] = need;
     acc[kPNeed] += need;
   }
   block_add_partials(acc, b.part);
 }
 
+__global__ __launch_bounds__(kBlock) void kv_commit_kernel(BatchView b, StoreView st) {
+  __shared__ uint16_t s_heads[kBlock / 64][kWalkSpan];
+  __shared__ unsigned long long s_wsum[kBlock / 64];
+  if (st.ctr->mode != 0) return;  // uniform over the grid
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t wbase = (uint64_t)blockIdx.x * kWalkBlockSpan + (uint64_t)wave * kWalkSpan;
+  const uint32_t nh = collect_heads(b, wbase, lane, true, s_heads[wave]);
+  // this lane's heap offset: block base + exclusive prefix of plan sizes over (wave, lane)
+  unsigned long long mine = 0;
+  for (uint32_t h = lane; h < nh; h += 64) mine += b.need[wbase + s_heads[wave][h]];
+  unsigned long long incl = mine;
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63) s_wsum[wave] = incl;
+  __syncthreads();
+  unsigned long long before = 0;
+  for (int w = 0; w < wave; w++) before += s_wsum[w];
+  uint64_t heap_pos = st.ctr->batch_base + b.block_base[blockIdx.x] + before + incl - mine;
+  for (uint32_t h = lane; h < nh; h += 64) {
+    const uint64_t i = wbase + s_heads[wave][h];
+    // a run holds at most kMaxRunKeys records (more sends the batch to the ordered
+    // path); the bounds below only guard against a plan/commit mismatch
+    for (uint64_t k = i; k < b.n && k < i + kMaxRunKeys; k++) {
+      const KeyRec r = b.recs[k];
+      int64_t s = r.slot;
+      if (r.flags & kRecNew) {
+        s = table_claim(st.hashes, st.mask, r.hash);
+        if (s < 0 || heap_pos + r.key_len > st.heap_cap) {
+          atomicOr(&st.ctr->flags, s < 0 ? kFaultTable : kFaultHeap);
+          s = -1;
+        } else {
+          bytes_copy(st.heap + heap_pos, b.data + r.key_src, r.key_len);
+          st.ent[s].key_off = heap_pos;
+          st.ent[s].key_len = r.key_len;
+        }
+        heap_pos += r.key_len;
+      }
+      if (s >= 0 && (r.flags & kRecValue)) {
+        uint64_t dst = r.val_dst;
+        if (!(r.flags & kRecInPlace)) {
+          dst = heap_pos;
+          heap_pos += val_class(r.val_len);
+        }
+        if (dst + r.val_len > st.heap_cap) {
+          atomicOr(&st.ctr->flags, kFaultHeap);
+        } else {
+          bytes_copy(st.heap + dst, b.data + r.val_src, r.val_len);
+          st.ent[s].val_off = dst;
+          st.ent[s].val_len = r.val_len;
+        }
+      }
+      if (s >= 0 && (r.flags & kRecVersion)) st.ent[s].version = r.ver1;
+      if (r.flags & kRecLast) break;
+    }
+  }
+}
+
 // ---- 4 decide ----------------------------------------------------------------
-// One 1024-thread block folds the per-block partials (16 loads per thread in
+// One 1024-thread block folds the per-block partials (8 loads per thread in
 // flight, wave shuffles, one LDS step) and picks the batch's path:
 //   0 keyed commit: StoreFull unreachable (live + keys created <= max_keys);
 //   1 ordered replay: exact in-order path;
 //   2 refused: a capacity (table slots or heap bytes) cannot hold the batch's
 //     worst case — nothing is written, every pending command gets RG_KV_E_CAPACITY.
 constexpr int kFoldBlock = 1024;
-template <int K>
-__device__ __forceinline__ void fold_block(unsigned long long (&v)[K], const unsigned long long* src, uint32_t rows,
-                                           uint32_t stride, const int (&field)[K]) {
-  for (uint32_t r0 = threadIdx.x; r0 < rows; r0 += kFoldBlock * 16) {
-    unsigned long long x[16][K];
+template <int... F>
+__device__ __forceinline__ void fold_block(unsigned long long (&v)[sizeof...(F)], const unsigned long long* src,
+                                           uint32_t rows, uint32_t stride) {
+  constexpr int K = sizeof...(F);
+  constexpr int field[K] = {F...};
+  for (uint32_t r0 = threadIdx.x; r0 < rows; r0 += kFoldBlock * 8) {
+    unsigned long long x[8][K];
 #pragma unroll
-    for (int u = 0; u < 16; u++) {
+    for (int u = 0; u < 8; u++) {
       const uint32_t r = r0 + (uint32_t)u * kFoldBlock;
 #pragma unroll
       for (int k = 0; k < K; k++) x[u][k] = r < rows ? src[(uint64_t)r * stride + field[k]] : 0ull;
     }
 #pragma unroll
-    for (int u = 0; u < 16; u++)
+    for (int u = 0; u < 8; u++)
 #pragma unroll
       for (int k = 0; k < K; k++) v[k] = field[k] == kPOverflow ? (v[k] | x[u][k]) : v[k] + x[u][k];
   }
@@ -508,12 +660,14 @@ __device__ __forceinline__ void fold_block(unsigned long long (&v)[K], const uns
     if (lane == 0) red[wave][k] = t;
   }
   __syncthreads();
-#pragma unroll
-  for (int k = 0; k < K; k++) {
+  if (threadIdx.x < (uint32_t)K) {  // column k folded by thread k
     unsigned long long t = 0;
-    for (int w = 0; w < kFoldBlock / 64; w++) t += red[w][k];
-    v[k] = t;
+    for (int w = 0; w < kFoldBlock / 64; w++) t += red[w][threadIdx.x];
+    red[0][threadIdx.x] = t;
   }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; k++) v[k] = red[0][k];
 }
 
 __global__ __launch_bounds__(kFoldBlock) void kv_decide_kernel(StoreView st, const unsigned long long* part,
@@ -521,11 +675,9 @@ __global__ __launch_bounds__(kFoldBlock) void kv_decide_kernel(StoreView st, con
                                                                const unsigned long long* set_part, uint32_t blocks,
                                                                uint64_t* block_base) {
   unsigned long long v[3] = {0, 0, 0};
-  const int f3[3] = {kPCreated, kPNewSlots, kPOverflow};
-  fold_block<3>(v, part, walk_blocks, kPCount, f3);
+  fold_block<kPCreated, kPNewSlots, kPOverflow>(v, part, walk_blocks, kPCount);
   unsigned long long w[2] = {0, 0};
-  const int f2[2] = {0, 1};
-  fold_block<2>(w, set_part, blocks, 2, f2);
+  fold_block<0, 1>(w, set_part, blocks, 2);
   // exclusive scan of the walk blocks' plan bytes -> block_base; total = the batch's bytes
   __shared__ unsigned long long s_scan[kFoldBlock];
   const uint32_t per = (walk_blocks + kFoldBlock - 1) / kFoldBlock;
@@ -588,8 +740,9 @@ __global__ void kv_ordered_kernel(const uint8_t* data, const KvOp* ops, const ui
     if (op.status != kPending) continue;
     const uint8_t* kp = data + op.key_off;
     const uint64_t h = okey[c];
-    int64_t s = table_find(st.hashes, st.ent, st.heap, st.mask, h, kp, op.key_len);
-    const bool is_live = s >= 0 && st.ent[s].version > 0;
+    KvEntry e{};
+    int64_t s = table_find(st.hashes, st.ent, st.heap, st.mask, h, kp, op.key_len, &e);
+    const bool is_live = s >= 0 && e.version > 0;
     uint8_t r;
     if (op.kind == 0) {
       if (!is_live && live >= st.max_keys) {     // store.rs:153-158
@@ -608,15 +761,17 @@ __global__ void kv_ordered_kernel(const uint8_t* data, const KvOp* ops, const ui
         st.ent[s].version = 0;
         top += op.key_len;
       } else {
-        fits = val_class(op.val_len) <= val_class(st.ent[s].val_len);
+        fits = val_class(op.val_len) <= val_class(e.val_len);
       }
+      uint64_t voff = e.val_off;
       if (!fits) {
+        voff = top;
         st.ent[s].val_off = top;
         top += val_class(op.val_len);
       }
-      bytes_copy(st.heap + st.ent[s].val_off, data + op.val_off, op.val_len);
+      bytes_copy(st.heap + voff, data + op.val_off, op.val_len);
       st.ent[s].val_len = op.val_len;
-      st.ent[s].version = is_live ? st.ent[s].version + 1 : 1;
+      st.ent[s].version = is_live ? e.version + 1 : 1;
       if (!is_live) live++;
       ver += st.notify;
       r = RG_KV_SUCCESS;
@@ -642,8 +797,7 @@ __global__ __launch_bounds__(kFoldBlock) void kv_finish_kernel(KvCounters* k, co
                                                                uint32_t blocks) {
   if (k->mode != 0) return;
   unsigned long long v[3] = {0, 0, 0};
-  const int f3[3] = {kPLiveDelta, kPVersion, kPOps};
-  fold_block<3>(v, part, blocks, kPCount, f3);
+  fold_block<kPLiveDelta, kPVersion, kPOps>(v, part, blocks, kPCount);
   if (threadIdx.x != 0) return;
   k->live += v[0];  // two's-complement sum of +-1 deltas
   k->version += v[1];
@@ -721,8 +875,9 @@ struct rg_kv {
   // per-batch scratch
   uint64_t cap_cmds = 0;
   KvOp* ops = nullptr;
-  uint64_t *key_a = nullptr, *key_b = nullptr, *hfull = nullptr, *need = nullptr, *block_base = nullptr;
-  uint32_t *idx_a = nullptr, *idx_b = nullptr;
+  uint64_t *hfull = nullptr, *need = nullptr, *block_base = nullptr;
+  uint32_t *key_a = nullptr, *key_b = nullptr, *idx_a = nullptr, *idx_b = nullptr;
+  KeyRec* recs = nullptr;
   uint8_t* done = nullptr;
   unsigned long long* part = nullptr;
   unsigned long long* set_part = nullptr;  // [blocks][2] decode partials: pending SETs, worst-case bytes
@@ -755,10 +910,10 @@ void free_scratch(rg_kv* kv) {
   (void)hipFree(kv->ops); (void)hipFree(kv->key_a); (void)hipFree(kv->key_b); (void)hipFree(kv->hfull);
   (void)hipFree(kv->need); (void)hipFree(kv->block_base); (void)hipFree(kv->idx_a);
   (void)hipFree(kv->idx_b); (void)hipFree(kv->done); (void)hipFree(kv->part); (void)hipFree(kv->tmp);
-  (void)hipFree(kv->set_part);
-  kv->set_part = nullptr;
-  kv->ops = nullptr; kv->key_a = kv->key_b = kv->hfull = kv->need = kv->block_base = nullptr;
-  kv->idx_a = kv->idx_b = nullptr; kv->done = nullptr; kv->part = nullptr; kv->tmp = nullptr;
+  (void)hipFree(kv->set_part); (void)hipFree(kv->recs);
+  kv->set_part = nullptr; kv->recs = nullptr;
+  kv->ops = nullptr; kv->hfull = kv->need = kv->block_base = nullptr;
+  kv->key_a = kv->key_b = kv->idx_a = kv->idx_b = nullptr; kv->done = nullptr; kv->part = nullptr; kv->tmp = nullptr;
   kv->cap_cmds = 0; kv->tmp_bytes = 0;
 }
 
@@ -770,8 +925,9 @@ int ensure_scratch(rg_kv* kv, uint64_t n) {
   while (cap < n) cap *= 2;
   const uint64_t blocks = (cap + kBlock - 1) / kBlock;
   KV_HIP(kv, hipMalloc(&kv->ops, cap * sizeof(KvOp)));
-  KV_HIP(kv, hipMalloc(&kv->key_a, cap * 8));
-  KV_HIP(kv, hipMalloc(&kv->key_b, cap * 8));
+  KV_HIP(kv, hipMalloc(&kv->key_a, cap * 4));
+  KV_HIP(kv, hipMalloc(&kv->key_b, cap * 4));
+  KV_HIP(kv, hipMalloc(&kv->recs, cap * sizeof(KeyRec)));
   KV_HIP(kv, hipMalloc(&kv->hfull, cap * 8));
   KV_HIP(kv, hipMalloc(&kv->need, cap * 8));
   KV_HIP(kv, hipMalloc(&kv->block_base, (cap / kWalkBlockSpan + 1) * 8));
@@ -783,7 +939,7 @@ int ensure_scratch(rg_kv* kv, uint64_t n) {
   size_t t1 = 0, t2 = 0;
   KV_HIP(kv, hipcub::DeviceRadixSort::SortPairs(nullptr, t1, kv->key_a, kv->key_b, kv->idx_a, kv->idx_b,
                                                   (int)cap, 0, 32, kv->stream));
-  KV_HIP(kv, hipcub::DeviceScan::ExclusiveSum(nullptr, t2, kv->need, kv->key_b, (int)cap, kv->stream));
+  KV_HIP(kv, hipcub::DeviceScan::ExclusiveSum(nullptr, t2, kv->need, kv->hfull, (int)cap, kv->stream));
   kv->tmp_bytes = t1 > t2 ? t1 : t2;
   KV_HIP(kv, hipMalloc(&kv->tmp, kv->tmp_bytes));
   kv->cap_cmds = cap;
@@ -884,17 +1040,18 @@ int rg_kv_apply_async(rg_kv* kv, const uint8_t* data_dev, const uint64_t* cmd_of
   if (int rc = ensure_scratch(kv, n_cmds)) return rc;
   hipStream_t s = stream ? (hipStream_t)stream : kv->stream;
   const uint32_t blocks = (uint32_t)((n_cmds + kBlock - 1) / kBlock);
-  // sort width: bucket bits enough that distinct keys rarely share a bucket (load
-  // <= 1/4), at most 31 (+1 bit for the invalid bucket): 24 + 1 bits up to 2^22 commands
+  // sort width: bucket bits enough that distinct keys rarely share a bucket (about
+  // 2^8 buckets per command, so a run rarely needs the multi-key path), at most 31
+  // (+1 bit for the invalid bucket, so the sort key is a u32)
   int vbits = 14;
-  while (vbits < 31 && (1ull << (vbits - 2)) < n_cmds) vbits++;
+  while (vbits < 31 && (1ull << (vbits - 8)) < n_cmds) vbits++;
   if (kv->cfg.bucket_bits && (int)kv->cfg.bucket_bits < vbits) vbits = (int)kv->cfg.bucket_bits;
   const int sbits = vbits + 1;
-  const uint64_t invalid_bucket = 1ull << vbits;
+  const uint32_t invalid_bucket = 1u << vbits;
   hipLaunchKernelGGL(kv_decode_kernel, dim3(blocks), dim3(kBlock), 0, s, data_dev, cmd_off_dev, n_cmds,
                      apply_mask_dev, kv->cfg.max_value_size,
                      kv->cfg.hash_bits && kv->cfg.hash_bits < 64 ? (1ull << kv->cfg.hash_bits) - 1 : ~0ull,
-                     invalid_bucket - 1, invalid_bucket, kv->ops, kv->key_a, kv->hfull, kv->idx_a,
+                     (uint64_t)invalid_bucket - 1, invalid_bucket, kv->ops, kv->key_a, kv->hfull, kv->idx_a,
                      results_dev, kv->set_part);
   KV_HIP(kv, hipGetLastError());
   size_t tb = kv->tmp_bytes;
@@ -902,15 +1059,14 @@ int rg_kv_apply_async(rg_kv* kv, const uint8_t* data_dev, const uint64_t* cmd_of
                                                   (int)n_cmds, 0, sbits, s));
   KV_HIP(kv, hipMemsetAsync(kv->done, 0, n_cmds, s));
   BatchView b{data_dev, kv->ops, kv->key_b, kv->hfull, kv->idx_b, n_cmds, results_dev, kv->done, kv->need,
-              kv->block_base, invalid_bucket, kv->part};
+              kv->block_base, kv->recs, invalid_bucket, kv->part};
   const StoreView st = view(kv);
   const uint32_t walk_blocks = (uint32_t)((n_cmds + kWalkBlockSpan - 1) / kWalkBlockSpan);
-  hipLaunchKernelGGL(kv_walk_kernel<false>, dim3(walk_blocks), dim3(kBlock), 0, s, b, st);
+  hipLaunchKernelGGL(kv_plan_kernel, dim3(walk_blocks), dim3(kBlock), 0, s, b, st);
   KV_HIP(kv, hipGetLastError());
   hipLaunchKernelGGL(kv_decide_kernel, dim3(1), dim3(kFoldBlock), 0, s, st, kv->part, walk_blocks, kv->set_part,
                      blocks, kv->block_base);
-  KV_HIP(kv, hipMemsetAsync(kv->done, 0, n_cmds, s));
-  hipLaunchKernelGGL(kv_walk_kernel<true>, dim3(walk_blocks), dim3(kBlock), 0, s, b, st);
+  hipLaunchKernelGGL(kv_commit_kernel, dim3(walk_blocks), dim3(kBlock), 0, s, b, st);
   hipLaunchKernelGGL(kv_ordered_kernel, dim3(1), dim3(64), 0, s, data_dev, kv->ops, kv->hfull, n_cmds,
                      results_dev, st);
   hipLaunchKernelGGL(kv_finish_kernel, dim3(1), dim3(kFoldBlock), 0, s, kv->ctr, kv->part, walk_blocks);

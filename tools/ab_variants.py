@@ -1,5 +1,5 @@
 """Interleaved A/B of experiment builds of librabia_gpu.so (tools/build_variants.sh)
-on the bench's REF step (n=5, 2^28 slots, slot-tiled 1024). Each variant runs in
+and of rg_debug_set diagnostic switches (AB_DIAGS="name:0x600,...") on the bench's REF step (n=5, 2^28 slots, slot-tiled 1024). Each variant runs in
 its own process (RABIA_GPU_LIB), rounds interleave the variants, and every
 variant's output buffer and step result must equal the default build's
 (checksums). Run on the GPU box: python tools/ab_variants.py > gpurun_out/ab.json"""
@@ -23,6 +23,7 @@ n, T, S = 5, 1024, int(os.environ.get("AB_SLOTS", 1 << 28))
 nw = S // 32
 stream = torch.cuda.Stream(); torch.cuda.set_stream(stream); sp = stream.cuda_stream
 ev = PhaseEvaluator(n, self_lane=4, seed=42, tile_words=T)
+N.check(ev.lib.rg_debug_set(ev.ctx, int(os.environ.get("AB_DIAG", "0"), 0)), ev.ctx)
 sets = []
 for i in range(3):
     v = torch.empty(((nw + T - 1) // T) * (4 * n + 1) * T, dtype=torch.int32, device="cuda")
@@ -49,14 +50,19 @@ print(json.dumps({"median_us": float(np.median(ts)), "min_us": float(np.min(ts))
 
 
 def main():
-    libs = {"default": os.path.join(ROOT, "rabia_amd", "lib", "librabia_gpu.so")}
+    lib0 = os.path.join(ROOT, "rabia_amd", "lib", "librabia_gpu.so")
+    libs = {"default": (lib0, "0")}
     for p in sorted(glob.glob(os.path.join(ROOT, "rabia_amd", "lib", "variants", "*.so"))):
-        libs[os.path.basename(p)[len("librabia_gpu_"):-3]] = p
+        libs[os.path.basename(p)[len("librabia_gpu_"):-3]] = (p, "0")
+    # AB_DIAGS="name:diag,name:diag": the default library under rg_debug_set(diag)
+    for item in filter(None, os.environ.get("AB_DIAGS", "").split(",")):
+        name, diag = item.split(":")
+        libs[name] = (lib0, diag)
     rounds = int(os.environ.get("AB_ROUNDS", 3))
     got = {k: [] for k in libs}
     for r in range(rounds):
-        for name, path in libs.items():
-            env = dict(os.environ, ROOT=ROOT, RABIA_GPU_LIB=path)
+        for name, (path, diag) in libs.items():
+            env = dict(os.environ, ROOT=ROOT, RABIA_GPU_LIB=path, AB_DIAG=diag)
             out = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True,
                                  timeout=300)
             if out.returncode != 0:
