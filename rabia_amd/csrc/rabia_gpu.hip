@@ -13,6 +13,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <vector>
 
 #include "rg_kernels.h"
 
@@ -83,17 +84,20 @@ constexpr int wmax_for(int n) { return n <= 5 ? 4 : (n <= 10 ? 2 : 1); }
 // Tile shapes: {threads, words per thread}. Big tiles keep the per-launch count
 // of tiles and look-back hand-offs low on large windows; small tiles fill
 // the 256 CUs on single 2^20-slot windows.
-// kCfgRing: the pipelined persistent kernel (ref_ring_kernel, 256 compute threads x W
-// words per tile + one control wave), REF rg_phase_step_async only.
-enum TileCfg { kCfgBig = 0, kCfgMid = 1, kCfgSmall = 2, kCfgBigW2 = 3, kCfgMidW2 = 4, kCfgRing = 5 };
-constexpr int kRingBlock = 256;
+// kCfgRing: the persistent software-pipelined kernel (ref_pipe_kernel, 512 threads x W
+// words per tile), large REF rg_phase_step_async launches.
+enum TileCfg { kCfgBig = 0, kCfgMid = 1, kCfgSmall = 2, kCfgBigW2 = 3, kCfgMidW2 = 4, kCfgRing = 5,
+               kCfgLegacyBig = 6, kCfgDefBig6 = 7 };
+constexpr int kRingBlock = 512;
 #ifndef RG_RING_DEFAULT
 #define RG_RING_DEFAULT 0
 #endif
 constexpr int cfg_block(int c) {
-  return (c == kCfgBig || c == kCfgBigW2) ? 512 : (c == kCfgSmall ? 128 : 256);
+  return (c == kCfgBig || c == kCfgBigW2 || c == kCfgLegacyBig || c == kCfgDefBig6) ? 512 : (c == kCfgSmall ? 128 : 256);
 }
-inline int cfg_words(int c, int n) { return c == kCfgSmall ? 1 : (c >= kCfgBigW2 ? 2 : wmax_for(n)); }
+inline int cfg_words(int c, int n) {
+  return c == kCfgSmall ? 1 : (c >= kCfgLegacyBig ? 4 : (c >= kCfgBigW2 ? 2 : wmax_for(n)));
+}
 
 int pick_cfg(int n, uint64_t n_words) {
   const uint64_t wm = (uint64_t)wmax_for(n);
@@ -118,22 +122,32 @@ struct Disp {
         return;
       }
     }
-    if (c == kCfgBig) hipLaunchKernelGGL((ref_step_kernel<N, WM, 512, false>), dim3(grid), dim3(512), 0, s, p);
-    else if (c == kCfgMid) hipLaunchKernelGGL((ref_step_kernel<N, WM, 256, false>), dim3(grid), dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((ref_step_kernel<N, 1, 128, false>), dim3(grid), dim3(128), 0, s, p);
+    if constexpr (N == 5) {  // A/B shapes (rg_debug_set bits 16-18)
+      if (c == kCfgLegacyBig) {  // round-1 kernel: both rounds' planes live across the look-back
+        hipLaunchKernelGGL((ref_step_kernel<N, 4, 512, false, 0, 4>), dim3(grid), dim3(512), 0, s, p);
+        return;
+      }
+      if (c == kCfgDefBig6) {  // 6 waves per SIMD (a few spills)
+        hipLaunchKernelGGL((ref_step_kernel<N, 4, 512, false, 1, 6>), dim3(grid), dim3(512), 0, s, p);
+        return;
+      }
+    }
+    if (c == kCfgBig) hipLaunchKernelGGL((ref_step_kernel<N, WM, 512, false, 1>), dim3(grid), dim3(512), 0, s, p);
+    else if (c == kCfgMid) hipLaunchKernelGGL((ref_step_kernel<N, WM, 256, false, 1>), dim3(grid), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((ref_step_kernel<N, 1, 128, false, 1>), dim3(grid), dim3(128), 0, s, p);
   }
   // ring grid: every WG resident (forward progress of the look-back), at most
   // `per_cu` per CU, never more WGs than tiles
   static uint32_t ring_grid(uint32_t cus, uint32_t per_cu, uint32_t n_tiles) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ref_ring_kernel<N, WM, kRingBlock>, kRingBlock + 64, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ref_pipe_kernel<N, WM, kRingBlock>, kRingBlock, 0) !=
             hipSuccess || nb < 1)
       nb = 1;
     const uint32_t g = cus * ((uint32_t)nb < per_cu ? (uint32_t)nb : per_cu);
     return g < n_tiles ? g : n_tiles;
   }
   static void ring(uint32_t grid, hipStream_t s, const StepParams& p) {
-    hipLaunchKernelGGL((ref_ring_kernel<N, WM, kRingBlock>), dim3(grid), dim3(kRingBlock + 64), 0, s, p);
+    hipLaunchKernelGGL((ref_pipe_kernel<N, WM, kRingBlock>), dim3(grid), dim3(kRingBlock), 0, s, p);
   }
   static void wmvc(int c, uint32_t grid, hipStream_t s, const StepParams& p) {
     if (c == kCfgBig) hipLaunchKernelGGL((wmvc_step_kernel<N, WM, 512>), dim3(grid), dim3(512), 0, s, p);
@@ -204,12 +218,18 @@ int ensure_tiles(rg_ctx* ctx, uint64_t n_tiles, bool force_zero) {
   if (n_tiles > ctx->tile_cap) {
     uint64_t cap = ctx->tile_cap ? ctx->tile_cap : 4096;
     while (cap < n_tiles) cap *= 2;
-    (void)hipFree(ctx->lookback);
+    if (ctx->lookback) (void)hipFree(ctx->lookback - kLookbackGuard);
     (void)hipFree(ctx->stats);
     ctx->lookback = nullptr;
     ctx->stats = nullptr;
     ctx->tile_cap = 0;
-    RG_HIP(ctx, hipMalloc(&ctx->lookback, cap * 8));
+    // kLookbackGuard granules in front of tile 0 read as "inclusive, 0" (rg_kernels.h
+    // lookback_pipe reads a fixed window without bounds checks); never rewritten
+    unsigned long long* base = nullptr;
+    RG_HIP(ctx, hipMalloc(&base, (cap + kLookbackGuard) * 8));
+    ctx->lookback = base + kLookbackGuard;
+    std::vector<unsigned long long> guard(kLookbackGuard, kGuardGranule);
+    RG_HIP(ctx, hipMemcpy(base, guard.data(), kLookbackGuard * 8, hipMemcpyHostToDevice));
     RG_HIP(ctx, hipMalloc(&ctx->stats, cap * kStatGranules * 8));
     ctx->tile_cap = cap;
   }
@@ -335,7 +355,7 @@ int rg_destroy(rg_ctx* ctx) {
   (void)hipFree(ctx->rec);
   (void)hipFree(ctx->state);
   (void)hipFree(ctx->result);
-  (void)hipFree(ctx->lookback);
+  if (ctx->lookback) (void)hipFree(ctx->lookback - kLookbackGuard);
   (void)hipFree(ctx->stats);
   (void)hipFree(ctx->dbg);
   (void)hipFree(ctx->r1v_cells);
@@ -412,7 +432,9 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
   uint32_t force = (ctx->diag >> 8) & 7u;  // diagnostics: force a tile shape
   if ((force == 4 || force == 5) && (n != 5 || wmvc || shard)) force = 0;
   if (force == 6 && (wmvc || shard)) force = 0;
-  int cfg = force ? (int)force - 1 : pick_cfg(n, n_words);
+  const uint32_t dforce = (ctx->diag >> 16) & 7u;  // diagnostics: A/B shapes (REF, n = 5)
+  if (dforce && (dforce > 2 || n != 5 || wmvc || shard)) return fail(ctx, RG_EINVAL, "rg_debug_set: bad shape");
+  int cfg = dforce ? kCfgLegacyBig + (int)dforce - 1 : force ? (int)force - 1 : pick_cfg(n, n_words);
   uint64_t tile_words = (uint64_t)cfg_block(cfg) * cfg_words(cfg, n);
   uint64_t n_tiles = (n_words + tile_words - 1) / tile_words;
   uint32_t ring_grid = 0;
@@ -426,15 +448,17 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
     const uint64_t rt = (n_words + (uint64_t)kRingBlock * wmax_for(n) - 1) / ((uint64_t)kRingBlock * wmax_for(n));
     const uint32_t per_cu = (ctx->diag >> 12) & 3u ? (ctx->diag >> 12) & 3u : 2u;
     const uint32_t gr = kRingGrid[n](ctx->cus, per_cu, (uint32_t)(rt < 0xFFFFFFFFull ? rt : 0xFFFFFFFFull));
-    // the pipeline pays off once every WG has a few tiles (forced: any size)
-    if (cfg == kCfgRing || rt >= 4ull * gr) {
+    // the pipeline pays off once every WG has a few tiles (forced: any size); the
+    // kernel's per-thread counters are 16-bit: at most 65535 slots per thread
+    const uint64_t per_wg = gr ? (rt + gr - 1) / gr : 0;
+    if (gr && per_wg * wmax_for(n) * 32 < 65536 && (cfg == kCfgRing || rt >= 4ull * gr)) {
       cfg = kCfgRing;
       tile_words = (uint64_t)kRingBlock * wmax_for(n);
       n_tiles = rt;
       ring_grid = gr;
     }
   }
-  // (the ring's per-WG records take 4 granules per WG of the 2 per tile allocated)
+  // (the pipe kernel's per-WG records take 4 granules per WG of the 2 per tile allocated)
   const uint64_t gran_tiles = n_tiles > 2ull * ring_grid ? n_tiles : 2ull * ring_grid;
   if (int rc = ensure_tiles(ctx, gran_tiles, false)) return rc;
   // Statistics granules carry 12 bits of seq and look-back granules 31: start a

@@ -353,6 +353,67 @@ __device__ __forceinline__ uint32_t lookback_exclusive_wide(unsigned long long* 
   return excl;
 }
 
+// Look-back of the persistent pipelined kernel: the caller published the tile's
+// aggregate already; one poll reads the 512 predecessor granules at constant
+// offsets from one address (8 loads per lane in flight). Indices below 0 read the
+// guard granules the host keeps in front of tile 0 (tag 0xFFFFFFFF = inclusive 0).
+constexpr int kLookbackGuard = 512;
+constexpr unsigned long long kGuardGranule = 0xFFFFFFFFull << 32;
+__device__ __forceinline__ uint32_t lookback_pipe(unsigned long long* status, uint32_t tile, uint32_t seq,
+                                                  uint32_t agg, int lane, unsigned long long* err) {
+  constexpr int K = 8;
+  const uint32_t tag_inc = (seq << 1) | 1u;
+  if (tile == 0) {
+    if (lane == 0) atomic_store_agent(status, ((unsigned long long)tag_inc << 32) | agg);
+    return 0;
+  }
+  uint32_t excl = 0;
+  int64_t pos = (int64_t)tile - 1;  // distance 0 = tile - 1
+  uint32_t spins = 0;
+  for (;;) {
+    unsigned long long* b = status + (pos - lane);
+    unsigned long long g[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) g[k] = atomic_load_agent(b - 64 * k);
+    int first = 64 * K;
+    bool blocked = false;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const uint32_t tag = (uint32_t)(g[k] >> 32);
+      const bool guard = tag == 0xFFFFFFFFu;
+      const bool ready = guard || (tag >> 1) == seq;
+      const unsigned long long im = __ballot(ready && (tag & 1u));
+      const unsigned long long nr = __ballot(!ready);
+      if (first == 64 * K) {
+        const int f = im ? __builtin_ctzll(im) : 64;
+        const unsigned long long need = f >= 63 ? ~0ull : ((2ull << f) - 1ull);
+        if (nr & need) { blocked = true; break; }
+        if (f < 64) first = 64 * k + f;
+      }
+    }
+    if (blocked) {
+      if (++spins > (1u << 22)) {  // ~seconds: a protocol fault, not a wait
+        if (lane == 0) {
+          atomicOr(err, 1ull);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    uint32_t v = 0;
+#pragma unroll
+    for (int k = 0; k < K; k++)
+      if (64 * k + lane <= first) v += (uint32_t)g[k];
+    excl += (uint32_t)wave_sum64(v);
+    if (first < 64 * K) break;
+    pos -= 64 * K;
+  }
+  if (lane == 0) atomic_store_agent(status + tile, ((unsigned long long)tag_inc << 32) | (agg + excl));
+  return excl;
+}
+
 // ---- per-tile statistics -> granules; the last tile reduces them ------------
 // Per tile, two 8-B granules written with agent-scope stores by one lane:
 //   g0 = tag:13 | n_decided:17 | n_v1:17 | n_pending_r1:17
@@ -443,7 +504,7 @@ __device__ __forceinline__ void block_reduce_totals(unsigned long long (&v)[7], 
     for (int k = 0; k < 7; k++) red[wave][k] = v[k];
   lds_barrier();
   unsigned long long r[7] = {0, 0, 0, 0, 0, ~0ull, 0};
-#pragma unroll
+#pragma unroll 1  // one wave's row at a time: unrolled, the rows' 64-bit reads set the kernel's VGPR peak
   for (int w = 0; w < WAVES; w++) {
 #pragma unroll
     for (int k = 0; k < 4; k++) r[k] += red[w][k];
@@ -457,11 +518,10 @@ __device__ __forceinline__ void block_reduce_totals(unsigned long long (&v)[7], 
 
 // Publish this tile's statistics; the tile with the last index folds every
 // tile's granules, advances the device engine state and writes the step result.
-template <int FIN, int BLOCK, int W>
+template <int FIN, int BLOCK, int W, int kBatch = 8>  // kBatch: tiles per thread with loads in flight together
 __device__ __forceinline__ void finish_tile(const StepParams& p, Record* rec, TileStats ts,
                                             uint32_t tile, int tid, int lane, int wave) {
   constexpr uint64_t kTileSlots = (uint64_t)BLOCK * W * 32;
-  constexpr int kBatch = 8;  // tiles per thread with loads in flight together
   static_assert(64 * W * 32 <= 0xFFFF, "per-wave sums must fit the 16-bit packed fields");
   const TileStats b = block_reduce_stats<BLOCK>(ts, lane, wave);
   const unsigned long long tag = stat_tag(p.seq);
@@ -629,6 +689,93 @@ __device__ __forceinline__ void load_planes(const StepParams& p, uint64_t w0, bo
   }
 }
 
+// per-WG statistics record: 4 tagged granules (tag 12 bits at [52, 64))
+//   g0 = dec:26 | v1:26 << 26      g1 = pend:26 | draws:26 << 26
+//   g2 = (largest accepted V1 offset + 1, 0 = none):33   g3 = smallest undecided offset (2^33-1 = none):33
+constexpr int kPersistStatGranules = 4;
+constexpr unsigned long long kOff33 = (1ull << 33) - 1;
+__device__ __forceinline__ unsigned long long pstat_tag(uint32_t seq) {
+  return (unsigned long long)(0x800u | (seq & 0x7FFu)) << 52;
+}
+
+// WG 0 of a persistent launch: fold the G per-WG records, advance the engine
+// state, write the step result (TOTAL = threads per WG).
+template <int TOTAL>
+__device__ __forceinline__ void persist_fold(const StepParams& p, Record* rec, uint32_t G, int tid, int lane,
+                                             int wave) {
+  unsigned long long v[7] = {0, 0, 0, 0, 0, ~0ull, 0};  // dec v1 pend draws max(id+1) min(id) fault
+  const unsigned long long tag = pstat_tag(p.seq);
+  constexpr unsigned long long kTagMask = ~0ull << 52, kMask26 = (1ull << 26) - 1;
+  for (uint32_t wg = tid; wg < G; wg += TOTAL) {
+    unsigned long long* gp = p.stats + (uint64_t)wg * kPersistStatGranules;
+    unsigned long long gv[4];
+#pragma unroll
+    for (int k2 = 0; k2 < 4; k2++) gv[k2] = atomic_load_agent(gp + k2);
+    uint32_t spins = 0;
+    for (;;) {
+      bool ready = true;
+#pragma unroll
+      for (int k2 = 0; k2 < 4; k2++) ready &= (gv[k2] & kTagMask) == tag;
+      if (ready) break;
+      if (++spins > kSpinLimit) { v[6] = 2; break; }
+      __builtin_amdgcn_s_sleep(2);
+#pragma unroll
+      for (int k2 = 0; k2 < 4; k2++)
+        if ((gv[k2] & kTagMask) != tag) gv[k2] = atomic_load_agent(gp + k2);
+    }
+    v[0] += gv[0] & kMask26;
+    v[1] += (gv[0] >> 26) & kMask26;
+    v[2] += gv[1] & kMask26;
+    v[3] += (gv[1] >> 26) & kMask26;
+    const unsigned long long mx = gv[2] & kOff33, mn = gv[3] & kOff33;
+    if (mx && p.slot_base + mx > v[4]) v[4] = p.slot_base + mx;
+    if (mn != kOff33 && p.slot_base + mn < v[5]) v[5] = p.slot_base + mn;
+  }
+  block_reduce_totals<TOTAL>(v, lane, wave);
+  if (tid != 0) return;
+  const unsigned long long err = atomicAdd(&rec->error.v, 0ull) | v[6];
+  DevState st = *p.state;
+  DevResult r;
+  r.n_slots = p.n_slots;
+  r.n_decided = v[0];
+  r.n_v1 = v[1];
+  r.n_pending_r1 = v[2];
+  r.n_draws = v[3];
+  const unsigned long long end = p.slot_base + p.n_slots;
+  const unsigned long long fu = v[5] < end ? v[5] : end;
+  unsigned long long lc = st.last_committed;  // commit_phase: monotonic max, state.rs:77-99
+  if (v[4] && v[4] - 1 > lc) lc = v[4] - 1;
+  unsigned long long wm = st.commit_watermark;
+  if (p.slot_base <= wm && wm < fu) wm = fu;
+  r.last_committed_max = lc;
+  r.first_undecided = fu;
+  r.rng_next = st.rng_next + r.n_draws;
+  r.commit_watermark = wm;
+  r.flags = err;
+  st.rng_next = r.rng_next;
+  st.last_committed = lc;
+  st.commit_watermark = wm;
+  st.steps += 1;
+  *p.state = st;
+  *p.result = r;
+  if (p.result_user) *p.result_user = r;
+}
+
+// Plane loads without a branch: a thread past the window loads word 0 instead
+// (its valid masks are 0, so the values are never used). A conditional load makes
+// hipcc wait for it right away, which would drain the ring's prefetch.
+template <int N, int W>
+__device__ __forceinline__ void load_planes_any(const StepParams& p, uint64_t w0, int first_plane,
+                                                uint32_t (&lo)[N][W], uint32_t (&hi)[N][W]) {
+  const uint32_t* base = p.votes + p.lin.base(w0 < p.n_words ? w0 : 0);
+  const uint64_t ps = p.lin.pstride;
+#pragma unroll
+  for (int j = 0; j < N; j++) {
+    load_words<W>(base + (first_plane + 2 * j) * ps, lo[j]);
+    load_words<W>(base + (first_plane + 2 * j + 1) * ps, hi[j]);
+  }
+}
+
 // Decision code masks (lo, hi) of count_votes over the round-2 lanes of word i
 // (messages.rs:185-211; 3 = None): V0 0/0, V1 1/0, VQ 0/1, None 1/1.
 template <int N, int W>
@@ -680,12 +827,56 @@ __device__ __forceinline__ void r2_decision_own(const uint32_t (&lo)[N][W], cons
   dhi = dq | dn;
 }
 
+// Decisions of count_votes(R2') for both possible own votes at once (DEF path):
+// A = own V0 on the VQ slots, B = own V1 (engine.rs:540-542, 613-628). The other
+// lanes are tallied once; the self lane is added per variant. On non-VQ slots the
+// own vote is already known (V0, V1, or none when round 1 is pending), so A == B.
+template <int N, int W>
+__device__ __forceinline__ void r2_decision_ab(const uint32_t (&lo)[N][W], const uint32_t (&hi)[N][W], int i,
+                                               uint32_t q, int self, uint32_t v1, uint32_t vq, uint32_t pend,
+                                               uint32_t& alo, uint32_t& ahi, uint32_t& blo, uint32_t& bhi) {
+  constexpr int B = ctr_bits(N);
+  Ctr<B> c0, c1, cq;
+  ctr_zero(c0); ctr_zero(c1); ctr_zero(cq);
+  uint32_t sl = 0, sh = 0;
+#pragma unroll
+  for (int j = 0; j < N; j++) {
+    const bool me = j == self;
+    const uint32_t l = lo[j][i], h = hi[j][i];
+    sl |= me ? l : 0u;
+    sh |= me ? h : 0u;
+    const uint32_t ol = me ? ~0u : l, oh = me ? ~0u : h;  // the self lane counts as absent here
+    ctr_add(c0, ~ol & ~oh);
+    ctr_add(c1, ol & ~oh);
+    ctr_add(cq, ~ol & oh);
+  }
+  const bool has_self = (unsigned)self < (unsigned)N;  // self_lane -1: no own vote joins R2
+#pragma unroll
+  for (int v = 0; v < 2; v++) {
+    const uint32_t own = v ? (v1 | vq) : v1;
+    const uint32_t l = has_self ? (sl & pend) | (own & ~pend) : ~0u, h = has_self ? sh & pend : ~0u;
+    Ctr<B> d0c = c0, d1c = c1, dqc = cq;
+    ctr_add(d0c, ~l & ~h);
+    ctr_add(d1c, l & ~h);
+    ctr_add(dqc, ~l & h);
+    const uint32_t d0 = ctr_ge(d0c, q);
+    const uint32_t d1 = ~d0 & ctr_ge(d1c, q);
+    const uint32_t dq = ~d0 & ~d1 & ctr_ge(dqc, q);
+    const uint32_t dn = ~(d0 | d1 | dq);
+    (v ? blo : alo) = d1 | dn;
+    (v ? bhi : ahi) = dq | dn;
+  }
+}
+
 // SHARD = the sharded-REF flavour (rg_phase_step_shard_async): the draws come from
 // the shard's provisional stream position, every VQ slot also leaves a draw
 // record (its decision under both own votes) for rg_shard_fixup_async, and the
 // tile statistics leave the VQ slots out.
-template <int N, int W, int BLOCK, bool SHARD>
-__global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
+// DEF = issue the R2 loads after the round-1 tally (the R1 registers are dead by
+// then), so that the kernel fits OCC waves per SIMD and more tiles are resident per
+// CU while one waits in the look-back; the ChaCha12 staging rows shrink to 128.
+template <int N, int W, int BLOCK, bool SHARD, int DEF = 0, int OCC = 4>
+__global__ __launch_bounds__(BLOCK, OCC) void ref_step_kernel(StepParams p) {
   constexpr int B = ctr_bits(N);
   constexpr int WAVES = BLOCK / 64;
   __shared__ uint32_t s_wave[WAVES];
@@ -702,21 +893,29 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
 
   // Issue every plane load up front (R2 stays in flight across the look-back).
   uint32_t r1lo[N][W], r1hi[N][W], r2lo[N][W], r2hi[N][W];
-  load_planes<N, W>(p, w0, active, 0, r1lo, r1hi);
-#ifdef RG_R1_BARRIER  // build-time experiment: every wave's R1 loads queue ahead of any R2 load
-  __builtin_amdgcn_s_barrier();
-#endif
-  load_planes<N, W>(p, w0, active, 2 * N, r2lo, r2hi);
+  if constexpr (DEF == 1) {
+    load_planes_any<N, W>(p, w0, 0, r1lo, r1hi);  // branchless: past the window they read word 0
+  } else if constexpr (DEF == 2) {  // both rounds up front, decisions still before the barrier
+    load_planes_any<N, W>(p, w0, 0, r1lo, r1hi);
+    load_planes_any<N, W>(p, w0, 2 * N, r2lo, r2hi);
+  } else {
+    load_planes<N, W>(p, w0, active, 0, r1lo, r1hi);
+    load_planes<N, W>(p, w0, active, 2 * N, r2lo, r2hi);
+  }
 
   // ---- round 1: count_votes + |votes| >= quorum fallback (engine.rs:495-505).
   // Only what the draws need survives the tally: per-slot (c1 > c0), (c1 < c0).
   uint32_t r1v1[W], r1vq[W], pend[W];
   uint32_t vq_count = 0;
+  uint32_t seq0 = 0;  // DEF: a zero the compiler cannot see through, chaining word i+1 after word i
 #pragma unroll
   for (int i = 0; i < W; i++) {
     const uint32_t vm = valid_mask(w0 + i, p.n_words, p.n_slots);
     Ctr<B> c0, c1, cp;
     ctr_zero(c0); ctr_zero(c1); ctr_zero(cp);
+    if constexpr (DEF != 0) {
+      c0.b[0] = c1.b[0] = cp.b[0] = seq0;  // (the word tallies one after another: no 4-word ILP)
+    }
 #pragma unroll
     for (int j = 0; j < N; j++) {
       const uint32_t lo = r1lo[j][i], hi = r1hi[j][i];
@@ -734,17 +933,30 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
     s_cls[2 * i][tid] = gt & r1vq[i];
     s_cls[2 * i + 1][tid] = lt & r1vq[i];
     vq_count += __builtin_popcount(r1vq[i]);
+    if constexpr (DEF != 0) asm volatile("" : "+v"(seq0), "+v"(r1v1[i]), "+v"(r1vq[i]), "+v"(pend[i]));
   }
+  if constexpr (DEF == 1) load_planes_any<N, W>(p, w0, 2 * N, r2lo, r2hi);
 
   // ---- exclusive prefix of VQ slots: block scan + cross-tile look-back
   const uint32_t incl = wave_incl_scan32(vq_count, lane);
   if (lane == 63) s_wave[wave] = incl;
   lds_barrier();
   uint32_t wave_off = 0, tile_total = 0;
+  if constexpr (DEF != 0) {  // one LDS read per lane, the sums as wave-uniform scalars
+    const uint32_t sw = lane < WAVES ? s_wave[lane] : 0u;
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
 #pragma unroll
-  for (int w = 0; w < WAVES; w++) {
-    wave_off += (w < wave) ? s_wave[w] : 0u;
-    tile_total += s_wave[w];
+    for (int w = 0; w < WAVES; w++) {
+      const uint32_t x = __builtin_amdgcn_readlane(sw, w);
+      wave_off += (w < wv) ? x : 0u;
+      tile_total += x;
+    }
+  } else {
+#pragma unroll
+    for (int w = 0; w < WAVES; w++) {
+      wave_off += (w < wave) ? s_wave[w] : 0u;
+      tile_total += s_wave[w];
+    }
   }
   stamp(p, tile, 1, tid);
   if (wave == 0) {
@@ -757,6 +969,20 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
                                      : lookback_exclusive(p.lookback, tile, p.seq, tile_total, lane, &rec->error.v);
 #endif
     if (lane == 0) s_excl = e;
+  }
+  // DEF: both-outcome decisions while wave 0 looks back; the R2 registers die here,
+  // before the ChaCha12 blocks need theirs
+  uint32_t dalo[W], dahi[W], dblo[W], dbhi[W];
+  if constexpr (DEF != 0) {
+#pragma unroll
+    for (int i = 0; i < W; i++)
+    {
+      r2_decision_ab<N, W>(r2lo, r2hi, i, p.q, p.self_lane, r1v1[i], r1vq[i], pend[i], dalo[i], dahi[i], dblo[i],
+                           dbhi[i]);
+      // pin the results here (volatile asm keeps its order with the barrier below):
+      // otherwise the decisions sink to their use and R2 stays live across ChaCha
+      asm volatile("" : "+v"(dalo[i]), "+v"(dahi[i]), "+v"(dblo[i]), "+v"(dbhi[i]));
+    }
   }
   lds_barrier();
   stamp(p, tile, 2, tid);
@@ -775,17 +1001,18 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
     mq[i] = r1vq[i];
   }
   if (tile_total) {
-    __shared__ uint32_t s_blk[BLOCK][17];  // +1 word: conflict-free rows
+    constexpr int kRows = DEF ? (BLOCK < 128 ? BLOCK : 128) : BLOCK;
+    __shared__ uint32_t s_blk[kRows][17];  // +1 word: conflict-free rows
     const unsigned long long b_first = k_tile >> 3, b_last = (k_tile + tile_total - 1) >> 3;
-    for (unsigned long long cb = b_first; cb <= b_last; cb += BLOCK) {
-      if (cb + tid <= b_last) {
+    for (unsigned long long cb = b_first; cb <= b_last; cb += kRows) {
+      if (tid < kRows && cb + tid <= b_last) {
         uint32_t x[16];
         chacha_block<12>(p.key, cb + tid, 0, x);
 #pragma unroll
         for (int j = 0; j < 16; j++) s_blk[tid][j] = x[j];
       }
       lds_barrier();
-      const unsigned long long k_lim = (cb + BLOCK) << 3;
+      const unsigned long long k_lim = (cb + kRows) << 3;
 #pragma unroll
       for (int i = 0; i < W; i++) {
         if (!mq[i] || k >= k_lim) continue;
@@ -848,6 +1075,10 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
         if (kr < p.vq_cap) p.vq_rec[kr] = ((unsigned long long)info << 32) | off;
         kr++;
       }
+    } else if constexpr (DEF != 0) {
+      const uint32_t sel = own_lo[i] & r1vq[i];  // VQ slots whose draw gave V1
+      dlo[i] = (dalo[i] & ~sel) | (dblo[i] & sel);
+      dhi[i] = (dahi[i] & ~sel) | (dbhi[i] & sel);
     } else {
 #pragma unroll
       for (int j = 0; j < N; j++)
@@ -897,286 +1128,285 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
     st_vm[i] = valid_mask(w0 + i, p.n_words, p.n_slots) & keep;
   }
   const TileStats ts = thread_stats<W>(st_dec, st_v1, pend, st_vm, vq_count, w0, tw0, p);
-  finish_tile<SHARD ? kFinShard : kFinRef, BLOCK, W>(p, rec, ts, tile, tid, lane, wave);
+  finish_tile<SHARD ? kFinShard : kFinRef, BLOCK, W, (OCC > 4 ? 2 : 8)>(p, rec, ts, tile, tid, lane, wave);
   stamp(p, tile, 4, tid);
 }
 
 // ============================================================================
-// Pipelined persistent REF step (large launches of rg_phase_step_async). G
-// workgroups, all resident (G <= CUs x resident WGs per CU); WG g owns the tiles
-// g, g + G, g + 2G, ... in order. Each WG has BLOCK compute threads plus ONE
-// control wave and runs every tile in two halves one iteration apart:
-//   iteration j, compute waves: round 1 of tile j+1 (its R1 planes were loaded
-//     during iteration j-1), issue the R1 loads of tile j+2; barrier A(j); then
-//     draws + round 2 + stores of tile j (its R2 planes were loaded during
-//     iteration j-1) and issue the R2 loads of tile j+1.
-//   control wave, between A(j-1) and A(j): publish tile j's VQ count, look back
-//     for its exclusive prefix (one poll of up to 512 predecessor granules: the
-//     same-iteration predecessors publish theirs at about the same time and the
-//     previous iteration's last tile already holds an inclusive value), publish
-//     the inclusive value and compute tile j's first ChaCha12 blocks into LDS.
-// The look-back so has a whole tile period of slack and runs on a wave that holds
-// no plane loads (its polls never drain them), and the compute waves always have
-// the next tile's R1 or R2 planes in flight. Forward progress: a tile's look-back
-// needs only tiles published in the same or an earlier iteration, every WG is
-// resident (the host sizes G from the occupancy), and the spin is bounded
-// (Record.error -> RG_ESTATE). Statistics accumulate per WG in registers; WG 0
-// folds the G per-WG records.
+// Persistent software-pipelined REF step (large rg_phase_step_async launches).
+// G workgroups, all resident (the host sizes G from the occupancy query); WG g
+// owns tiles g, g + G, g + 2G, ... A tile's round-1 tally and both-outcome
+// round-2 decisions (r2_decision_ab) run as soon as its planes land, which leaves
+// 7 words of state per thread word (V1/VQ/pending masks, decision A and B); the
+// planes of the WG's NEXT tile are then in flight while wave 0 looks back for the
+// current tile's VQ prefix, so the look-back's round trip (which queues behind
+// the CU's own plane loads) overlaps HBM traffic instead of holding an idle tile.
+// Per iteration:
+//   issue the next tile's R1 + R2 loads | wave 0: look back (one wide poll over the
+//   512 predecessors: this iteration's tiles published aggregates one step earlier,
+//   the previous iteration's tiles are inclusive) | tally + decisions of the next
+//   tile | barrier | wave 0 publishes the next tile's aggregate | ChaCha12 blocks,
+//   draws, own votes and the 8 output planes of the current tile.
+// Forward progress: a tile's look-back needs only aggregates published before the
+// previous barrier of every WG and inclusives of the previous iteration; every WG
+// is resident; the spin is bounded (Record.error -> RG_ESTATE). Statistics
+// accumulate per WG in registers and WG 0 folds the G per-WG records.
 // ============================================================================
-// per-WG statistics record: 4 tagged granules (tag 12 bits at [52, 64))
-//   g0 = dec:26 | v1:26 << 26      g1 = pend:26 | draws:26 << 26
-//   g2 = (largest accepted V1 offset + 1, 0 = none):33   g3 = smallest undecided offset (2^33-1 = none):33
-constexpr int kPersistStatGranules = 4;
-constexpr unsigned long long kOff33 = (1ull << 33) - 1;
-constexpr int kRingBlk = 64;  // ChaCha12 blocks (512 draws) per tile prepared by the control wave
-__device__ __forceinline__ unsigned long long pstat_tag(uint32_t seq) {
-  return (unsigned long long)(0x800u | (seq & 0x7FFu)) << 52;
-}
+template <int W>
+struct PipeTile {  // one tile's round-1 state between its tally and its stores
+  uint32_t v1[W], vq[W], pd[W];
+  uint32_t cnt, incl;
+};
 
-// Plane loads without a branch: a thread past the window loads word 0 instead
-// (its valid masks are 0, so the values are never used). A conditional load makes
-// hipcc wait for it right away, which would drain the ring's prefetch.
-template <int N, int W>
-__device__ __forceinline__ void load_planes_any(const StepParams& p, uint64_t w0, int first_plane,
-                                                uint32_t (&lo)[N][W], uint32_t (&hi)[N][W]) {
-  const uint32_t* base = p.votes + p.lin.base(w0 < p.n_words ? w0 : 0);
-  const uint64_t ps = p.lin.pstride;
-#pragma unroll
-  for (int j = 0; j < N; j++) {
-    load_words<W>(base + (first_plane + 2 * j) * ps, lo[j]);
-    load_words<W>(base + (first_plane + 2 * j + 1) * ps, hi[j]);
-  }
-}
-
-// Round 1 of one tile (engine.rs:495-505) from the R1 registers: V1 / VQ /
-// pending masks, the VQ slots' (c1 > c0), (c1 < c0) masks into LDS, VQ count.
+// Round 1 of one tile (engine.rs:495-505) word after word: V1 / VQ / pending masks,
+// the VQ slots' (c1 > c0), (c1 < c0) masks into LDS, the VQ count and its wave scan.
 template <int N, int W, int BLOCK>
-__device__ __forceinline__ uint32_t ring_tally(const StepParams& p, uint64_t w0, const uint32_t (&lo)[N][W],
-                                               const uint32_t (&hi)[N][W], uint32_t (*cls)[BLOCK], int tid,
-                                               uint32_t (&v1)[W], uint32_t (&vq)[W], uint32_t (&pd)[W]) {
+__device__ __forceinline__ void pipe_tally(const StepParams& p, uint64_t w0, const uint32_t (&r1lo)[N][W],
+                                           const uint32_t (&r1hi)[N][W], uint32_t (*cls)[BLOCK], int tid, int lane,
+                                           PipeTile<W>& t) {
   constexpr int B = ctr_bits(N);
-  uint32_t cnt = 0;
+  uint32_t seq0 = 0, cnt = 0;
 #pragma unroll
   for (int i = 0; i < W; i++) {
     const uint32_t vm = valid_mask(w0 + i, p.n_words, p.n_slots);
     Ctr<B> c0, c1, cp;
     ctr_zero(c0); ctr_zero(c1); ctr_zero(cp);
+    c0.b[0] = c1.b[0] = cp.b[0] = seq0;  // word i+1 after word i (no 4-word ILP: registers)
 #pragma unroll
     for (int j = 0; j < N; j++) {
-      const uint32_t l = lo[j][i], h = hi[j][i];
-      ctr_add(c0, ~l & ~h);
-      ctr_add(c1, l & ~h);
-      ctr_add(cp, ~(l & h));
+      const uint32_t lo = r1lo[j][i], hi = r1hi[j][i];
+      ctr_add(c0, ~lo & ~hi);
+      ctr_add(c1, lo & ~hi);
+      ctr_add(cp, ~(lo & hi));
     }
     const uint32_t g0 = ctr_ge(c0, p.q), g1 = ctr_ge(c1, p.q), gp = ctr_ge(cp, p.q);
-    v1[i] = ~g0 & g1 & vm;
-    vq[i] = ~g0 & ~g1 & gp & vm;  // cq >= q implies present >= q
-    pd[i] = ~((g0 & vm) | v1[i] | vq[i]) & vm;
+    t.v1[i] = ~g0 & g1 & vm;
+    t.vq[i] = ~g0 & ~g1 & gp & vm;
+    t.pd[i] = ~((g0 & vm) | t.v1[i] | t.vq[i]) & vm;
     uint32_t gt, lt;
     ctr_cmp(c1, c0, gt, lt);
-    cls[2 * i][tid] = gt & vq[i];
-    cls[2 * i + 1][tid] = lt & vq[i];
-    cnt += __builtin_popcount(vq[i]);
+    cls[2 * i][tid] = gt & t.vq[i];
+    cls[2 * i + 1][tid] = lt & t.vq[i];
+    cnt += __builtin_popcount(t.vq[i]);
+    asm volatile("" : "+v"(seq0), "+v"(t.v1[i]), "+v"(t.vq[i]), "+v"(t.pd[i]));
   }
-  return cnt;
+  t.cnt = cnt;
+  t.incl = wave_incl_scan32(cnt, lane);
 }
 
+// Both-outcome round-2 decisions of one tile into LDS (4 words per thread word).
 template <int N, int W, int BLOCK>
-__global__ __launch_bounds__(BLOCK + 64) void ref_ring_kernel(StepParams p) {
-  constexpr int WAVES = BLOCK / 64;  // compute waves; wave WAVES is the control wave
+__device__ __forceinline__ void pipe_decide(const StepParams& p, const uint32_t (&r2lo)[N][W],
+                                            const uint32_t (&r2hi)[N][W], const PipeTile<W>& t,
+                                            uint32_t (*dec)[BLOCK], int tid) {
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    uint32_t alo, ahi, blo, bhi;
+    r2_decision_ab<N, W>(r2lo, r2hi, i, p.q, p.self_lane, t.v1[i], t.vq[i], t.pd[i], alo, ahi, blo, bhi);
+    dec[4 * i][tid] = alo;
+    dec[4 * i + 1][tid] = ahi;
+    dec[4 * i + 2][tid] = blo;
+    dec[4 * i + 3][tid] = bhi;
+  }
+}
+
+template <int BLOCK>
+__device__ __forceinline__ uint32_t pipe_tile_total(const uint32_t* sw_lds, int lane) {
+  constexpr int WAVES = BLOCK / 64;
+  const uint32_t sw = lane < WAVES ? sw_lds[lane] : 0u;
+  uint32_t t = 0;
+#pragma unroll
+  for (int w = 0; w < WAVES; w++) t += __builtin_amdgcn_readlane(sw, w);
+  return t;
+}
+
+template <int N, int W, int BLOCK, int OCC = 4>
+__global__ __launch_bounds__(BLOCK, OCC) void ref_pipe_kernel(StepParams p) {
+  constexpr int WAVES = BLOCK / 64;
   constexpr uint64_t kTW = (uint64_t)BLOCK * W;
-  __shared__ uint32_t s_wave[3][WAVES];        // per-wave inclusive VQ counts, by tile j % 3
-  __shared__ uint32_t s_excl[2];               // the tile's exclusive VQ prefix, by j % 2
-  __shared__ uint32_t s_cls[2][2 * W][BLOCK];  // (c1 > c0), (c1 < c0) of the VQ slots, by j % 2
-  __shared__ uint32_t s_blk[2][kRingBlk][17];  // the tile's first ChaCha12 blocks, by j % 2
+  constexpr int kRows = 128;                   // ChaCha12 blocks (1024 draws) staged per pass
+  __shared__ uint32_t s_wave[2][WAVES];        // per-wave inclusive VQ counts, by tile parity
+  __shared__ uint32_t s_excl;                  // the current tile's exclusive VQ prefix
+  __shared__ uint32_t s_cls[2][2 * W][BLOCK];  // (c1 > c0), (c1 < c0) of the VQ slots, by tile parity
+  __shared__ uint32_t s_dec[4 * W][BLOCK];     // the current tile's decisions for own V0 / own V1
+  __shared__ uint32_t s_blk[kRows][17];
   Record* rec = p.rec + (p.seq & 1u);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid0 = threadIdx.x, lane0 = tid0 & 63, wave = tid0 >> 6;
+  const int tid = tid0, lane = lane0;
   const uint32_t G = gridDim.x, g = blockIdx.x;
   const uint32_t nt = (p.n_tiles - g + G - 1) / G;  // this WG's tiles (>= 1: the host keeps G <= n_tiles)
   if (g == 0 && tid == 0) atomic_store_agent(&p.rec[(p.seq + 1) & 1u].error.v, 0ull);
   const unsigned long long k_base = p.state->rng_next;
-  uint32_t a_dec = 0, a_v1 = 0, a_pend = 0, a_draws = 0;
-  unsigned long long a_max1 = 0, a_min = kOff33;
+  const uint32_t tw0 = (uint32_t)tid * W;
+  uint32_t a_cnt0 = 0, a_cnt1 = 0;                 // dec | v1 << 16, pend | draws << 16 (per thread <= 2^16)
+  uint32_t a_max1 = 0, a_min = 0xFFFFFFFFu;        // launch-relative slot offsets (n_slots < 2^32)
 
-  if (wave == WAVES) {
-    // ---- control wave: tile j's prefix and first ChaCha blocks, for j = 0 .. nt-1
-    lds_barrier();  // A(-1): tile 0's counts are in s_wave[0]
-    for (uint32_t j = 0; j < nt; j++) {
-      const uint32_t tile = g + j * G;
-      uint32_t agg = 0;
-#pragma unroll
-      for (int w = 0; w < WAVES; w++) agg += s_wave[j % 3][w];
-      const uint32_t excl = lookback_exclusive_wide<8>(p.lookback, tile, p.seq, agg, lane, &rec->error.v, 8, 8, 1);
-      if (agg) {
-        const unsigned long long kt = k_base + excl, b0 = kt >> 3, b1 = (kt + agg - 1) >> 3;
-        if (lane < kRingBlk && b0 + lane <= b1) {
-          uint32_t x[16];
-          chacha_block<12>(p.key, b0 + lane, 0, x);
-#pragma unroll
-          for (int k = 0; k < 16; k++) s_blk[j & 1][lane][k] = x[k];
-        }
-      }
-      if (lane == 0) s_excl[j & 1] = excl;
-      lds_barrier();  // A(j)
-    }
-  } else {
-    // ---- compute waves
-    const uint32_t tw0 = (uint32_t)tid * W;
+  PipeTile<W> cur;
+  {  // prologue: tile g
     uint32_t r1lo[N][W], r1hi[N][W], r2lo[N][W], r2hi[N][W];
-    uint32_t m_v1[W], m_vq[W], m_pend[W], m_cnt, m_incl;  // tile j's round-1 results
-    {
-      // The memory operations leave the prologue in the loop's steady-state order
-      // (R1 of the next tile, 8 stores, R2 of the current tile), so the counted
-      // waits hipcc derives at the loop entry (it merges the entry and back-edge
-      // states) are the steady-state ones and keep the prefetch in flight.
-      const uint64_t w0 = (uint64_t)g * kTW + tw0;
-      load_planes_any<N, W>(p, w0, 0, r1lo, r1hi);
-      m_cnt = ring_tally<N, W, BLOCK>(p, w0, r1lo, r1hi, s_cls[0], tid, m_v1, m_vq, m_pend);
-      m_incl = wave_incl_scan32(m_cnt, lane);
-      if (lane == 63) s_wave[0][wave] = m_incl;
-      load_planes_any<N, W>(p, w0 + (uint64_t)G * kTW, 0, r1lo, r1hi);
-      uint32_t* sk = p.sink + 4u * (g & 255u);
-#pragma unroll
-      for (int k = 0; k < 8; k++) store_words_nt<W>(sk, m_v1);  // placeholders, one 16-B slot per WG
-      load_planes_any<N, W>(p, w0, 2 * N, r2lo, r2hi);
-    }
-    lds_barrier();  // A(-1)
-    for (uint32_t j = 0; j < nt; j++) {
-      const uint64_t w0 = (uint64_t)(g + j * G) * kTW + tw0;
-      const uint64_t nw0 = w0 + (uint64_t)G * kTW;
-      uint32_t n_v1[W], n_vq[W], n_pend[W], n_cnt = 0, n_incl = 0;
-      if (j + 1 < nt) {  // round 1 of tile j+1
-        n_cnt = ring_tally<N, W, BLOCK>(p, nw0, r1lo, r1hi, s_cls[(j + 1) & 1], tid, n_v1, n_vq, n_pend);
-        n_incl = wave_incl_scan32(n_cnt, lane);
-        if (lane == 63) s_wave[(j + 1) % 3][wave] = n_incl;
-      }
-      // the R1 loads of tile j+2, unconditional (past the WG's last tile they read
-      // word 0 and are never used): loads under a branch make hipcc wait for every
-      // outstanding load at the next use, which would serialise the pipeline
-      load_planes_any<N, W>(p, nw0 + (uint64_t)G * kTW, 0, r1lo, r1hi);
-      lds_barrier();  // A(j): the control wave has tile j's prefix and first ChaCha blocks
+    const uint64_t w0 = (uint64_t)g * kTW + tw0;
+    load_planes_any<N, W>(p, w0, 0, r1lo, r1hi);
+    load_planes_any<N, W>(p, w0, 2 * N, r2lo, r2hi);
+    pipe_tally<N, W, BLOCK>(p, w0, r1lo, r1hi, s_cls[0], tid, lane, cur);
+    if (lane == 63) s_wave[0][wave] = cur.incl;
+    pipe_decide<N, W, BLOCK>(p, r2lo, r2hi, cur, s_dec, tid);
+  }
+  lds_barrier();
+  uint32_t cur_total = pipe_tile_total<BLOCK>(s_wave[0], lane);
+  if (wave == 0 && lane == 0 && !(p.diag & 1u))
+    atomic_store_agent(p.lookback + g, ((unsigned long long)(p.seq << 1) << 32) | cur_total);
 
-      // ---- own round-2 vote: one StdRng draw per VQ slot (engine.rs:523-537, 567-611)
-      const uint32_t* sw = s_wave[j % 3];
-      uint32_t wave_off = 0;
+  for (uint32_t j = 0; j < nt; j++) {
+    // Loop-variant copies of the thread index and the key: otherwise LICM hoists the
+    // LDS / shuffle addresses and the key-only part of ChaCha's first round out of
+    // the loop and keeps ~40 of them live across it (spills at 128 VGPRs).
+    int tid = tid0, lane = lane0;
+    asm volatile("" : "+v"(tid), "+v"(lane));
+    Key key = p.key;
 #pragma unroll
-      for (int w = 0; w < WAVES - 1; w++) wave_off += (w < wave) ? sw[w] : 0u;
-      const unsigned long long k_tile = k_base + s_excl[j & 1];
-      unsigned long long k = k_tile + wave_off + m_incl - m_cnt;  // this thread's first draw
-      uint32_t own_lo[W];
+    for (int z = 0; z < 8; z++) asm volatile("" : "+s"(key.k[z]));
+    const uint32_t tw0 = (uint32_t)tid * W;
+    const uint32_t tile = g + j * G;
+    const uint64_t w0 = (uint64_t)tile * kTW + tw0;
+    const uint64_t nw0 = w0 + (uint64_t)G * kTW;
+    const bool more = j + 1 < nt;
+    // ---- the next tile's planes in flight (unconditional: past the end they read word 0)
+    uint32_t r1lo[N][W], r1hi[N][W], r2lo[N][W], r2hi[N][W];
+    load_planes_any<N, W>(p, nw0, 0, r1lo, r1hi);
+    // ---- look-back for the current tile (its aggregate is published already)
+    if (wave == 0) {
+      uint32_t e = 0;
+      if (!(p.diag & 1u))
+        e = lookback_pipe(p.lookback, tile, p.seq, cur_total, lane, &rec->error.v);
+      if (lane == 0) s_excl = e;
+    }
+    // ---- round 1 of the next tile; then its R2 planes (in flight across the draws
+    // and stores of the current tile; the R1 registers are free by then)
+    PipeTile<W> nxt;
+    pipe_tally<N, W, BLOCK>(p, nw0, r1lo, r1hi, s_cls[(j + 1) & 1], tid, lane, nxt);
+    load_planes_any<N, W>(p, nw0, 2 * N, r2lo, r2hi);
+    if (lane == 63) s_wave[(j + 1) & 1][wave] = more ? nxt.incl : 0u;
+    lds_barrier();  // s_excl of the current tile, s_wave of the next
+    const uint32_t nxt_total = pipe_tile_total<BLOCK>(s_wave[(j + 1) & 1], lane);
+    if (more && wave == 0 && lane == 0 && !(p.diag & 1u))
+      atomic_store_agent(p.lookback + tile + G, ((unsigned long long)(p.seq << 1) << 32) | nxt_total);
+
+    // ---- own round-2 votes of the current tile (engine.rs:523-537, 567-611)
+    uint32_t wave_off = 0;
+    {
+      const uint32_t sw = lane < WAVES ? s_wave[j & 1][lane] : 0u;
+      const int wv = __builtin_amdgcn_readfirstlane(wave);
 #pragma unroll
-      for (int i = 0; i < W; i++) own_lo[i] = m_v1[i];
-      if (m_cnt) {
-        const unsigned long long b0 = k_tile >> 3;
-        unsigned long long cached = ~0ull;
-        uint32_t xb[16];
+      for (int w = 0; w < WAVES; w++) wave_off += (w < wv) ? __builtin_amdgcn_readlane(sw, w) : 0u;
+    }
+    const unsigned long long k_tile = k_base + s_excl;
+    unsigned long long k = k_tile + wave_off + cur.incl - cur.cnt;
+    uint32_t own_lo[W], mq[W];
+#pragma unroll
+    for (int i = 0; i < W; i++) {
+      own_lo[i] = cur.v1[i];
+      mq[i] = cur.vq[i];
+    }
+    if (cur_total) {
+      const unsigned long long b_first = k_tile >> 3, b_last = (k_tile + cur_total - 1) >> 3;
+      for (unsigned long long cb = b_first; cb <= b_last; cb += kRows) {
+        if (tid < kRows && cb + tid <= b_last) {
+          uint32_t x[16];
+          chacha_block<12>(key, cb + tid, 0, x);
+#pragma unroll
+          for (int z = 0; z < 16; z++) s_blk[tid][z] = x[z];
+        }
+        lds_barrier();
+        const unsigned long long k_lim = (cb + kRows) << 3;
 #pragma unroll
         for (int i = 0; i < W; i++) {
-          uint32_t mq = m_vq[i];
-          if (!mq) continue;
+          if (!mq[i] || k >= k_lim) continue;
           const uint32_t gtm = s_cls[j & 1][2 * i][tid], ltm = s_cls[j & 1][2 * i + 1][tid];
-          while (mq) {
-            const int b = __builtin_ctz(mq);
-            mq &= mq - 1;
-            const unsigned long long blk = k >> 3;
-            const uint32_t ws = (uint32_t)(k & 7u) * 2u;
-            unsigned long long u;
-            if (blk - b0 < (unsigned long long)kRingBlk) {
-              const uint32_t row = (uint32_t)(blk - b0);
-              u = (unsigned long long)s_blk[j & 1][row][ws] | ((unsigned long long)s_blk[j & 1][row][ws + 1] << 32);
-            } else {  // beyond the control wave's blocks: this thread's own (rare: > 512 draws in the tile)
-              if (blk != cached) {
-                chacha_block<12>(p.key, blk, 0, xb);
-                cached = blk;
-              }
-              u = 0;
-#pragma unroll
-              for (int z = 0; z < 8; z++)
-                if ((uint32_t)z * 2u == ws) u = (unsigned long long)xb[2 * z] | ((unsigned long long)xb[2 * z + 1] << 32);
-            }
+          while (mq[i] && k < k_lim) {
+            const int b = __builtin_ctz(mq[i]);
+            mq[i] &= mq[i] - 1;
+            const uint32_t row = (uint32_t)((k >> 3) - cb), ws = (uint32_t)(k & 7u) * 2u;
+            const unsigned long long u =
+                (unsigned long long)s_blk[row][ws] | ((unsigned long long)s_blk[row][ws + 1] << 32);
             const bool gt = (gtm >> b) & 1u, lt = (ltm >> b) & 1u;
             const bool v1 = gt ? (u < kP90) : (lt ? (u >= kP90) : (u < kP80));
             own_lo[i] |= (uint32_t)v1 << b;
             k++;
           }
         }
-      }
-
-      // ---- own vote joins round2_votes (engine.rs:540-542); decision (613-628)
-      uint32_t dlo[W], dhi[W];
-#pragma unroll
-      for (int i = 0; i < W; i++) {
-        const uint32_t vm = valid_mask(w0 + i, p.n_words, p.n_slots);
-        r2_decision_own<N, W>(r2lo, r2hi, i, p.q, p.self_lane, own_lo[i], m_pend[i], dlo[i], dhi[i]);
-        dlo[i] &= vm;
-        dhi[i] &= vm;
-        const uint32_t d1 = dlo[i] & ~dhi[i], dc = ~dhi[i] & vm;
-        a_dec += __builtin_popcount(dc);
-        a_v1 += __builtin_popcount(d1);
-        a_pend += __builtin_popcount(m_pend[i]);
-        const uint32_t v1l = d1 & phase_limit_mask(p.slot_base, w0 + i, p.max_phase);
-        if (v1l) {
-          const unsigned long long m1 = 32ull * (w0 + i) + (31u - __builtin_clz(v1l)) + 1u;
-          a_max1 = m1 > a_max1 ? m1 : a_max1;
-        }
-        const uint32_t und = ~dc & vm;
-        if (und) {
-          const unsigned long long mn = 32ull * (w0 + i) + __builtin_ctz(und);
-          a_min = mn < a_min ? mn : a_min;
-        }
-      }
-      a_draws += m_cnt;
-      if (w0 < p.n_words) {  // plane by plane (include/rabia_gpu.h output planes)
-        uint32_t* ob = p.out + p.lout.base(w0);
-        const uint64_t ps = p.lout.pstride;
-        uint32_t v[W];
-#pragma unroll
-        for (int i = 0; i < W; i++) v[i] = m_v1[i] | m_pend[i];
-        store_words_nt<W>(ob, v);
-#pragma unroll
-        for (int i = 0; i < W; i++) v[i] = m_vq[i] | m_pend[i];
-        store_words_nt<W>(ob + ps, v);
-#pragma unroll
-        for (int i = 0; i < W; i++) v[i] = own_lo[i] | m_pend[i];
-        store_words_nt<W>(ob + 2 * ps, v);
-        store_words_nt<W>(ob + 3 * ps, m_pend);
-        store_words_nt<W>(ob + 4 * ps, dlo);
-        store_words_nt<W>(ob + 5 * ps, dhi);
-#pragma unroll
-        for (int i = 0; i < W; i++) v[i] = ~dhi[i] & valid_mask(w0 + i, p.n_words, p.n_slots);
-        store_words_nt<W>(ob + 6 * ps, v);  // set_decision: committed iff not VQuestion
-#pragma unroll
-        for (int i = 0; i < W; i++) v[i] = dlo[i] & ~dhi[i];
-        store_words_nt<W>(ob + 7 * ps, v);  // V1: apply_batch + commit_phase
-      }
-      load_planes_any<N, W>(p, nw0, 2 * N, r2lo, r2hi);  // tile j+1's R2 (unconditional, as above)
-      if (j + 1 < nt) {  // tile j+1 becomes current: its round-1 masks
-#pragma unroll
-        for (int i = 0; i < W; i++) {
-          m_v1[i] = n_v1[i];
-          m_vq[i] = n_vq[i];
-          m_pend[i] = n_pend[i];
-        }
-        m_cnt = n_cnt;
-        m_incl = n_incl;
+        lds_barrier();
       }
     }
+    // ---- decision with the own vote (engine.rs:540-542, 613-628), stores, statistics
+    uint32_t dlo[W], dhi[W];
+    const uint32_t toff = (uint32_t)(32u * (uint64_t)tile * kTW) + 32u * tw0;  // launch-relative slot offset
+#pragma unroll
+    for (int i = 0; i < W; i++) {
+      const uint32_t sel = own_lo[i] & cur.vq[i];
+      dlo[i] = (s_dec[4 * i][tid] & ~sel) | (s_dec[4 * i + 2][tid] & sel);
+      dhi[i] = (s_dec[4 * i + 1][tid] & ~sel) | (s_dec[4 * i + 3][tid] & sel);
+      const uint32_t vm = valid_mask(w0 + i, p.n_words, p.n_slots);
+      dlo[i] &= vm;
+      dhi[i] &= vm;
+      const uint32_t d1 = dlo[i] & ~dhi[i], dc = ~dhi[i] & vm;
+      a_cnt0 += __builtin_popcount(dc) | (__builtin_popcount(d1) << 16);
+      a_cnt1 += __builtin_popcount(cur.pd[i]);
+      const uint32_t v1l = d1 & phase_limit_mask(p.slot_base, w0 + i, p.max_phase);
+      if (v1l) {
+        const uint32_t m1 = toff + 32u * i + (31u - __builtin_clz(v1l)) + 1u;
+        a_max1 = m1 > a_max1 ? m1 : a_max1;
+      }
+      const uint32_t und = ~dc & vm;
+      if (und) {
+        const uint32_t mn = toff + 32u * i + __builtin_ctz(und);
+        a_min = mn < a_min ? mn : a_min;
+      }
+    }
+    a_cnt1 += cur.cnt << 16;
+    if (w0 < p.n_words) {  // plane by plane (include/rabia_gpu.h output planes)
+      uint32_t* ob = p.out + p.lout.base(w0);
+      const uint64_t ps = p.lout.pstride;
+      uint32_t v[W];
+#pragma unroll
+      for (int i = 0; i < W; i++) v[i] = cur.v1[i] | cur.pd[i];
+      store_words_nt<W>(ob, v);
+#pragma unroll
+      for (int i = 0; i < W; i++) v[i] = cur.vq[i] | cur.pd[i];
+      store_words_nt<W>(ob + ps, v);
+#pragma unroll
+      for (int i = 0; i < W; i++) v[i] = own_lo[i] | cur.pd[i];
+      store_words_nt<W>(ob + 2 * ps, v);
+      store_words_nt<W>(ob + 3 * ps, cur.pd);
+      store_words_nt<W>(ob + 4 * ps, dlo);
+      store_words_nt<W>(ob + 5 * ps, dhi);
+#pragma unroll
+      for (int i = 0; i < W; i++) v[i] = ~dhi[i] & valid_mask(w0 + i, p.n_words, p.n_slots);
+      store_words_nt<W>(ob + 6 * ps, v);  // set_decision: committed iff not VQuestion
+#pragma unroll
+      for (int i = 0; i < W; i++) v[i] = dlo[i] & ~dhi[i];
+      store_words_nt<W>(ob + 7 * ps, v);  // V1: apply_batch + commit_phase
+    }
+    lds_barrier();  // every thread read the current tile's s_dec
+    pipe_decide<N, W, BLOCK>(p, r2lo, r2hi, nxt, s_dec, tid);  // the next tile's, from its R2 planes
+    cur = nxt;
+    cur_total = nxt_total;
   }
 
-  // ---- per-WG record (every wave; the control wave's counts are zero), folded by WG 0
+  // ---- per-WG record (persist_fold), folded by WG 0
   if (p.diag & 2u) return;
-  constexpr int TOTAL = BLOCK + 64;
   {
-    __shared__ unsigned long long red[WAVES + 1][4];
-    const unsigned long long s0 = wave_sum64((unsigned long long)a_dec | ((unsigned long long)a_v1 << 26));
-    const unsigned long long s1 = wave_sum64((unsigned long long)a_pend | ((unsigned long long)a_draws << 26));
-    const unsigned long long mx = wave_max64(a_max1), mn = wave_min64(a_min);
+    __shared__ unsigned long long red[WAVES][4];
+    const unsigned long long c0 = a_cnt0, c1 = a_cnt1;
+    const unsigned long long s0 = wave_sum64((c0 & 0xFFFFu) | ((c0 >> 16) << 26));
+    const unsigned long long s1 = wave_sum64((c1 & 0xFFFFu) | ((c1 >> 16) << 26));
+    const unsigned long long mx = wave_max64(a_max1);
+    const unsigned long long mn = wave_min64(a_min == 0xFFFFFFFFu ? kOff33 : (unsigned long long)a_min);
     if (lane == 0) { red[wave][0] = s0; red[wave][1] = s1; red[wave][2] = mx; red[wave][3] = mn; }
     lds_barrier();
     if (tid == 0) {
       unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = kOff33;
-#pragma unroll
-      for (int w = 0; w <= WAVES; w++) {
+#pragma unroll 1
+      for (int w = 0; w < WAVES; w++) {
         t0 += red[w][0]; t1 += red[w][1];
         t2 = red[w][2] > t2 ? red[w][2] : t2;
         t3 = red[w][3] < t3 ? red[w][3] : t3;
@@ -1190,62 +1420,7 @@ __global__ __launch_bounds__(BLOCK + 64) void ref_ring_kernel(StepParams p) {
     }
   }
   if (g != 0) return;
-  unsigned long long v[7] = {0, 0, 0, 0, 0, ~0ull, 0};  // dec v1 pend draws max(id+1) min(id) fault
-  const unsigned long long tag = pstat_tag(p.seq);
-  constexpr unsigned long long kTagMask = ~0ull << 52, kMask26 = (1ull << 26) - 1;
-  for (uint32_t wg = tid; wg < G; wg += TOTAL) {
-    unsigned long long* gp = p.stats + (uint64_t)wg * kPersistStatGranules;
-    unsigned long long gv[4];
-#pragma unroll
-    for (int k2 = 0; k2 < 4; k2++) gv[k2] = atomic_load_agent(gp + k2);
-    uint32_t spins = 0;
-    for (;;) {
-      bool ready = true;
-#pragma unroll
-      for (int k2 = 0; k2 < 4; k2++) ready &= (gv[k2] & kTagMask) == tag;
-      if (ready) break;
-      if (++spins > kSpinLimit) { v[6] = 2; break; }
-      __builtin_amdgcn_s_sleep(2);
-#pragma unroll
-      for (int k2 = 0; k2 < 4; k2++)
-        if ((gv[k2] & kTagMask) != tag) gv[k2] = atomic_load_agent(gp + k2);
-    }
-    v[0] += gv[0] & kMask26;
-    v[1] += (gv[0] >> 26) & kMask26;
-    v[2] += gv[1] & kMask26;
-    v[3] += (gv[1] >> 26) & kMask26;
-    const unsigned long long mx = gv[2] & kOff33, mn = gv[3] & kOff33;
-    if (mx && p.slot_base + mx > v[4]) v[4] = p.slot_base + mx;
-    if (mn != kOff33 && p.slot_base + mn < v[5]) v[5] = p.slot_base + mn;
-  }
-  block_reduce_totals<TOTAL>(v, lane, wave);
-  if (tid != 0) return;
-  const unsigned long long err = atomicAdd(&rec->error.v, 0ull) | v[6];
-  DevState st = *p.state;
-  DevResult r;
-  r.n_slots = p.n_slots;
-  r.n_decided = v[0];
-  r.n_v1 = v[1];
-  r.n_pending_r1 = v[2];
-  r.n_draws = v[3];
-  const unsigned long long end = p.slot_base + p.n_slots;
-  const unsigned long long fu = v[5] < end ? v[5] : end;
-  unsigned long long lc = st.last_committed;  // commit_phase: monotonic max, state.rs:77-99
-  if (v[4] && v[4] - 1 > lc) lc = v[4] - 1;
-  unsigned long long wm = st.commit_watermark;
-  if (p.slot_base <= wm && wm < fu) wm = fu;
-  r.last_committed_max = lc;
-  r.first_undecided = fu;
-  r.rng_next = st.rng_next + r.n_draws;
-  r.commit_watermark = wm;
-  r.flags = err;
-  st.rng_next = r.rng_next;
-  st.last_committed = lc;
-  st.commit_watermark = wm;
-  st.steps += 1;
-  *p.state = st;
-  *p.result = r;
-  if (p.result_user) *p.result_user = r;
+  persist_fold<BLOCK>(p, rec, G, tid, lane, wave);
 }
 
 // ============================================================================

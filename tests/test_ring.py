@@ -1,9 +1,10 @@
-"""The pipelined persistent REF kernel (ref_ring_kernel, rg_kernels.h) vs the oracle
-and vs the tiled kernel. Large REF launches pick it on their own; these tests force
-it (rg_debug_set bits 8-10 = 6) at every size so the small and ragged cases, the
-per-thread ChaCha fallback (> 512 draws in a tile) and 1 or 2 workgroups per CU
-are all exercised, and compare a bench-shaped 2^26-slot launch with the tiled kernel
-bit for bit (outputs, step result, device state over consecutive steps)."""
+"""The persistent software-pipelined REF kernel (ref_pipe_kernel, rg_kernels.h) vs the
+oracle and vs the default tiled kernel. It is a diagnostic path (rg_debug_set bits
+8-10 = 6 force it at any size; measured slower than the tiled kernel),
+kept bit-exact: small and ragged cases, more than 1024 draws in a tile (several
+ChaCha12 staging passes), 1 or 2 workgroups per CU, and a bench-shaped 2^26-slot
+launch compared with the tiled kernel bit for bit (outputs, step result, device state
+over consecutive steps)."""
 import numpy as np
 import pytest
 
@@ -53,8 +54,8 @@ def test_ring_vs_oracle(oracle, n, S):
 
 
 def test_ring_many_draws_per_tile(oracle):
-    """Every slot VQ at round 1 (all lanes '?'): 32768 draws per tile, far past the
-    control wave's 512, so nearly all draws take the per-thread ChaCha path."""
+    """Every slot VQ at round 1 (all lanes '?'): 65536 draws per tile, 64 ChaCha12
+    staging passes of 1024 draws each."""
     n, q, S = 5, 3, (1 << 20) + 5
     rng = np.random.default_rng(5)
     r1 = np.full((S, n), 2, np.uint8)
