@@ -87,16 +87,20 @@ constexpr int wmax_for(int n) { return n <= 5 ? 4 : (n <= 10 ? 2 : 1); }
 // kCfgRing: the persistent software-pipelined kernel (ref_pipe_kernel, 512 threads x W
 // words per tile), large REF rg_phase_step_async launches.
 enum TileCfg { kCfgBig = 0, kCfgMid = 1, kCfgSmall = 2, kCfgBigW2 = 3, kCfgMidW2 = 4, kCfgRing = 5,
-               kCfgLegacyBig = 6, kCfgDefBig6 = 7 };
+               kCfgPair = 6, kCfgLegacyBig = 7, kCfgDefBig6 = 8 };
+#ifndef RG_PAIR_DEFAULT
+#define RG_PAIR_DEFAULT 0
+#endif
 constexpr int kRingBlock = 512;
 #ifndef RG_RING_DEFAULT
 #define RG_RING_DEFAULT 0
 #endif
 constexpr int cfg_block(int c) {
-  return (c == kCfgBig || c == kCfgBigW2 || c == kCfgLegacyBig || c == kCfgDefBig6) ? 512 : (c == kCfgSmall ? 128 : 256);
+  return (c == kCfgBig || c == kCfgBigW2 || c == kCfgPair || c == kCfgLegacyBig || c == kCfgDefBig6) ? 512
+                                                                                                 : (c == kCfgSmall ? 128 : 256);
 }
 inline int cfg_words(int c, int n) {
-  return c == kCfgSmall ? 1 : (c >= kCfgLegacyBig ? 4 : (c >= kCfgBigW2 ? 2 : wmax_for(n)));
+  return c == kCfgSmall ? 1 : (c >= kCfgLegacyBig ? 4 : (c == kCfgPair ? wmax_for(n) : (c >= kCfgBigW2 ? 2 : wmax_for(n))));
 }
 
 int pick_cfg(int n, uint64_t n_words) {
@@ -146,6 +150,9 @@ struct Disp {
     const uint32_t g = cus * ((uint32_t)nb < per_cu ? (uint32_t)nb : per_cu);
     return g < n_tiles ? g : n_tiles;
   }
+  static void pair(uint32_t grid, hipStream_t s, const StepParams& p) {
+    hipLaunchKernelGGL((ref_pair_kernel<N, WM, 512>), dim3(grid), dim3(512), 0, s, p);
+  }
   static void ring(uint32_t grid, hipStream_t s, const StepParams& p) {
     hipLaunchKernelGGL((ref_pipe_kernel<N, WM, kRingBlock>), dim3(grid), dim3(kRingBlock), 0, s, p);
   }
@@ -191,6 +198,7 @@ const StepLaunch kRefLaunch[17] = RG_TABLE(ref);
 using RingLaunch = void (*)(uint32_t, hipStream_t, const StepParams&);
 using RingGrid = uint32_t (*)(uint32_t, uint32_t, uint32_t);
 const RingLaunch kRingLaunch[17] = RG_TABLE(ring);
+const RingLaunch kPairLaunch[17] = RG_TABLE(pair);
 const RingGrid kRingGrid[17] = RG_TABLE(ring_grid);
 const StepLaunch kWmvcLaunch[17] = RG_TABLE(wmvc);
 const DigestLaunch kDigestLaunch[17] = RG_TABLE(digest);
@@ -431,7 +439,7 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
   if (int rc = make_layout(ctx, kOutPlanes, n_words, stride_words, &lout, &need_out, "rg_phase_step")) return rc;
   uint32_t force = (ctx->diag >> 8) & 7u;  // diagnostics: force a tile shape
   if ((force == 4 || force == 5) && (n != 5 || wmvc || shard)) force = 0;
-  if (force == 6 && (wmvc || shard)) force = 0;
+  if ((force == 6 || force == 7) && (wmvc || shard)) force = 0;
   const uint32_t dforce = (ctx->diag >> 16) & 7u;  // diagnostics: A/B shapes (REF, n = 5)
   if (dforce && (dforce > 2 || n != 5 || wmvc || shard)) return fail(ctx, RG_EINVAL, "rg_debug_set: bad shape");
   int cfg = dforce ? kCfgLegacyBig + (int)dforce - 1 : force ? (int)force - 1 : pick_cfg(n, n_words);
@@ -458,8 +466,19 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
       ring_grid = gr;
     }
   }
-  // (the pipe kernel's per-WG records take 4 granules per WG of the 2 per tile allocated)
-  const uint64_t gran_tiles = n_tiles > 2ull * ring_grid ? n_tiles : 2ull * ring_grid;
+  // paired tiles: one workgroup per two consecutive tiles of the look-back chain
+  uint32_t pair_grid = 0;
+  if (!wmvc && !shard && !dforce && (cfg == kCfgPair || (!force && cfg == kCfgBig && RG_PAIR_DEFAULT &&
+                                                         !(ctx->diag & 0x8000u)))) {
+    cfg = kCfgPair;
+    tile_words = 512ull * wmax_for(n);
+    n_tiles = (n_words + tile_words - 1) / tile_words;
+    pair_grid = (uint32_t)((n_tiles + 1) / 2);
+  }
+  // (the persistent and paired kernels' per-WG records take 4 granules per WG of the
+  // 2 per tile allocated)
+  uint64_t gran_tiles = n_tiles > 2ull * ring_grid ? n_tiles : 2ull * ring_grid;
+  if (pair_grid && gran_tiles < 2ull * pair_grid) gran_tiles = 2ull * pair_grid;
   if (int rc = ensure_tiles(ctx, gran_tiles, false)) return rc;
   // Statistics granules carry 12 bits of seq and look-back granules 31: start a
   // fresh epoch on zeroed granules whenever either wraps.
@@ -509,6 +528,7 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
   hipStream_t s = pick_stream(ctx, stream);
   if (shard) launch_ref_shard(n, cfg_block(cfg), cfg_words(cfg, n), (uint32_t)n_tiles, s, p);
   else if (cfg == kCfgRing) kRingLaunch[n](ring_grid, s, p);
+  else if (cfg == kCfgPair) kPairLaunch[n](pair_grid, s, p);
   else (wmvc ? kWmvcLaunch : kRefLaunch)[n](cfg, (uint32_t)n_tiles, s, p);
   RG_HIP(ctx, hipGetLastError());
   return RG_OK;

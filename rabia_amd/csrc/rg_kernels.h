@@ -1424,6 +1424,235 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_pipe_kernel(StepParams p) {
 }
 
 // ============================================================================
+// Paired REF step (large rg_phase_step_async launches): each workgroup owns two
+// consecutive tiles A = 2b, B = 2b + 1 of the look-back chain. A is tallied and its
+// both-outcome decisions parked in LDS; then B's planes are loaded while wave 0
+// looks back for A, so A's wait for its predecessors overlaps B's HBM traffic, and
+// B needs no look-back of its own (its prefix is A's inclusive value). Half as many
+// look-backs as tiles, each hidden behind a tile's loads.
+// ============================================================================
+struct SubAcc {  // per-thread statistics over a workgroup's tiles
+  uint32_t cnt0 = 0, cnt1 = 0;                   // dec | v1 << 16, pend | draws << 16
+  uint32_t max1 = 0, min = 0xFFFFFFFFu;          // launch-relative slot offsets (+1 for max)
+};
+
+// Draws, own votes, decisions, stores and statistics of one tile whose exclusive VQ
+// prefix is known. Decisions for own V0 / V1 come from LDS (dec != nullptr) or from
+// the register arrays.
+template <int N, int W, int BLOCK>
+__device__ __forceinline__ void ref_finish_sub(const StepParams& p, const Key& key, uint64_t w0, uint32_t toff,
+                                               int tid, const PipeTile<W>& t, unsigned long long k_tile,
+                                               uint32_t wave_off, uint32_t total, uint32_t (*cls)[BLOCK],
+                                               uint32_t (*blk)[17], uint32_t (*dec)[BLOCK],
+                                               const uint32_t (&alo)[W], const uint32_t (&ahi)[W],
+                                               const uint32_t (&blo)[W], const uint32_t (&bhi)[W], SubAcc& acc) {
+  constexpr int kRows = 128;
+  unsigned long long k = k_tile + wave_off + t.incl - t.cnt;
+  uint32_t own_lo[W], mq[W];
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    own_lo[i] = t.v1[i];
+    mq[i] = t.vq[i];
+  }
+  if (total) {  // ChaCha12 blocks of the tile's draw range, staged in LDS (engine.rs:567-611)
+    const unsigned long long b_first = k_tile >> 3, b_last = (k_tile + total - 1) >> 3;
+    for (unsigned long long cb = b_first; cb <= b_last; cb += kRows) {
+      if (tid < kRows && cb + tid <= b_last) {
+        uint32_t x[16];
+        chacha_block<12>(key, cb + tid, 0, x);
+#pragma unroll
+        for (int z = 0; z < 16; z++) blk[tid][z] = x[z];
+      }
+      lds_barrier();
+      const unsigned long long k_lim = (cb + kRows) << 3;
+#pragma unroll
+      for (int i = 0; i < W; i++) {
+        if (!mq[i] || k >= k_lim) continue;
+        const uint32_t gtm = cls[2 * i][tid], ltm = cls[2 * i + 1][tid];
+        while (mq[i] && k < k_lim) {
+          const int b = __builtin_ctz(mq[i]);
+          mq[i] &= mq[i] - 1;
+          const uint32_t row = (uint32_t)((k >> 3) - cb), ws = (uint32_t)(k & 7u) * 2u;
+          const unsigned long long u = (unsigned long long)blk[row][ws] | ((unsigned long long)blk[row][ws + 1] << 32);
+          const bool gt = (gtm >> b) & 1u, lt = (ltm >> b) & 1u;
+          const bool v1 = gt ? (u < kP90) : (lt ? (u >= kP90) : (u < kP80));
+          own_lo[i] |= (uint32_t)v1 << b;
+          k++;
+        }
+      }
+      lds_barrier();
+    }
+  }
+  // the own vote joins round2_votes (engine.rs:540-542); decision (613-628)
+  uint32_t dlo[W], dhi[W];
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    const uint32_t sel = own_lo[i] & t.vq[i];
+    const uint32_t al = dec ? dec[4 * i][tid] : alo[i], ah = dec ? dec[4 * i + 1][tid] : ahi[i];
+    const uint32_t bl = dec ? dec[4 * i + 2][tid] : blo[i], bh = dec ? dec[4 * i + 3][tid] : bhi[i];
+    const uint32_t vm = valid_mask(w0 + i, p.n_words, p.n_slots);
+    dlo[i] = ((al & ~sel) | (bl & sel)) & vm;
+    dhi[i] = ((ah & ~sel) | (bh & sel)) & vm;
+    const uint32_t d1 = dlo[i] & ~dhi[i], dc = ~dhi[i] & vm;
+    acc.cnt0 += __builtin_popcount(dc) | (__builtin_popcount(d1) << 16);
+    acc.cnt1 += __builtin_popcount(t.pd[i]);
+    const uint32_t v1l = d1 & phase_limit_mask(p.slot_base, w0 + i, p.max_phase);
+    if (v1l) {
+      const uint32_t m1 = toff + 32u * i + (31u - __builtin_clz(v1l)) + 1u;
+      acc.max1 = m1 > acc.max1 ? m1 : acc.max1;
+    }
+    const uint32_t und = ~dc & vm;
+    if (und) {
+      const uint32_t mn = toff + 32u * i + __builtin_ctz(und);
+      acc.min = mn < acc.min ? mn : acc.min;
+    }
+  }
+  acc.cnt1 += t.cnt << 16;
+  if (w0 < p.n_words) {  // plane by plane (include/rabia_gpu.h output planes)
+    uint32_t* ob = p.out + p.lout.base(w0);
+    const uint64_t ps = p.lout.pstride;
+    uint32_t v[W];
+#pragma unroll
+    for (int i = 0; i < W; i++) v[i] = t.v1[i] | t.pd[i];
+    store_words_nt<W>(ob, v);
+#pragma unroll
+    for (int i = 0; i < W; i++) v[i] = t.vq[i] | t.pd[i];
+    store_words_nt<W>(ob + ps, v);
+#pragma unroll
+    for (int i = 0; i < W; i++) v[i] = own_lo[i] | t.pd[i];
+    store_words_nt<W>(ob + 2 * ps, v);
+    store_words_nt<W>(ob + 3 * ps, t.pd);
+    store_words_nt<W>(ob + 4 * ps, dlo);
+    store_words_nt<W>(ob + 5 * ps, dhi);
+#pragma unroll
+    for (int i = 0; i < W; i++) v[i] = ~dhi[i] & valid_mask(w0 + i, p.n_words, p.n_slots);
+    store_words_nt<W>(ob + 6 * ps, v);  // set_decision: committed iff not VQuestion
+#pragma unroll
+    for (int i = 0; i < W; i++) v[i] = dlo[i] & ~dhi[i];
+    store_words_nt<W>(ob + 7 * ps, v);  // V1: apply_batch + commit_phase
+  }
+}
+
+// Per-WG statistics record (persist_fold's format) from the threads' SubAcc.
+template <int BLOCK>
+__device__ __forceinline__ void publish_wg_record(const StepParams& p, uint32_t g, const SubAcc& acc, int tid,
+                                                  int lane, int wave) {
+  constexpr int WAVES = BLOCK / 64;
+  __shared__ unsigned long long red[WAVES][4];
+  const unsigned long long c0 = acc.cnt0, c1 = acc.cnt1;
+  const unsigned long long s0 = wave_sum64((c0 & 0xFFFFu) | ((c0 >> 16) << 26));
+  const unsigned long long s1 = wave_sum64((c1 & 0xFFFFu) | ((c1 >> 16) << 26));
+  const unsigned long long mx = wave_max64(acc.max1);
+  const unsigned long long mn = wave_min64(acc.min == 0xFFFFFFFFu ? kOff33 : (unsigned long long)acc.min);
+  if (lane == 0) { red[wave][0] = s0; red[wave][1] = s1; red[wave][2] = mx; red[wave][3] = mn; }
+  lds_barrier();
+  if (tid == 0) {
+    unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = kOff33;
+#pragma unroll 1
+    for (int w = 0; w < WAVES; w++) {
+      t0 += red[w][0]; t1 += red[w][1];
+      t2 = red[w][2] > t2 ? red[w][2] : t2;
+      t3 = red[w][3] < t3 ? red[w][3] : t3;
+    }
+    const unsigned long long tag = pstat_tag(p.seq);
+    unsigned long long* gr = p.stats + (uint64_t)g * kPersistStatGranules;
+    atomic_store_agent(gr + 0, tag | t0);
+    atomic_store_agent(gr + 1, tag | t1);
+    atomic_store_agent(gr + 2, tag | t2);
+    atomic_store_agent(gr + 3, tag | t3);
+  }
+}
+
+template <int N, int W, int BLOCK>
+__global__ __launch_bounds__(BLOCK, 4) void ref_pair_kernel(StepParams p) {
+  constexpr int WAVES = BLOCK / 64;
+  constexpr uint64_t kTW = (uint64_t)BLOCK * W;
+  __shared__ uint32_t s_wave[2][WAVES];
+  __shared__ uint32_t s_excl;
+  __shared__ uint32_t s_cls[2][2 * W][BLOCK];
+  __shared__ uint32_t s_dec[4 * W][BLOCK];     // A's decisions for own V0 / own V1
+  __shared__ uint32_t s_blk[128][17];
+  __shared__ uint32_t s_arrive;                // waves done with B's tally
+  Record* rec = p.rec + (p.seq & 1u);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t g = blockIdx.x, G = gridDim.x;
+  if (tid == 0) s_arrive = 0;  // (ordered before any arrival by the barrier after A's tally)
+  const uint32_t ta = 2 * g, tb = ta + 1;      // p.n_tiles = look-back tiles (2 per WG)
+  if (g == G - 1 && tid == 0) atomic_store_agent(&p.rec[(p.seq + 1) & 1u].error.v, 0ull);
+  const uint32_t tw0 = (uint32_t)tid * W;
+  const uint64_t wa = (uint64_t)ta * kTW + tw0, wb = wa + kTW;
+  const uint32_t toff_a = (uint32_t)(32u * (uint64_t)ta * kTW) + 32u * tw0, toff_b = toff_a + (uint32_t)(32u * kTW);
+  uint32_t r1lo[N][W], r1hi[N][W], r2lo[N][W], r2hi[N][W];
+  uint32_t z0[W], z1[W], z2[W], z3[W];         // (unused register decisions of tile A)
+  PipeTile<W> A, Bt;
+  SubAcc acc;
+
+  // ---- tile A: round 1, aggregate, both-outcome decisions into LDS
+  load_planes_any<N, W>(p, wa, 0, r1lo, r1hi);
+  pipe_tally<N, W, BLOCK>(p, wa, r1lo, r1hi, s_cls[0], tid, lane, A);
+  load_planes_any<N, W>(p, wa, 2 * N, r2lo, r2hi);
+  if (lane == 63) s_wave[0][wave] = A.incl;
+  lds_barrier();
+  const uint32_t tot_a = pipe_tile_total<BLOCK>(s_wave[0], lane);
+  if (wave == 0 && lane == 0 && ta > 0 && !(p.diag & 1u))
+    atomic_store_agent(p.lookback + ta, ((unsigned long long)(p.seq << 1) << 32) | tot_a);
+  pipe_decide<N, W, BLOCK>(p, r2lo, r2hi, A, s_dec, tid);
+  // ---- tile B's round 1; its aggregate goes out as soon as every wave has tallied
+  // (the next workgroup's A looks back through it), without a workgroup barrier:
+  // the last wave to arrive on an LDS counter publishes it
+  load_planes_any<N, W>(p, wb, 0, r1lo, r1hi);
+  pipe_tally<N, W, BLOCK>(p, wb, r1lo, r1hi, s_cls[1], tid, lane, Bt);
+  load_planes_any<N, W>(p, wb, 2 * N, r2lo, r2hi);
+  if (lane == 63) {
+    s_wave[1][wave] = Bt.incl;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (atomicAdd(&s_arrive, 1u) == WAVES - 1 && tb < p.n_tiles && !(p.diag & 1u)) {
+      uint32_t t = 0;
+#pragma unroll
+      for (int w = 0; w < WAVES; w++) t += __hip_atomic_load(&s_wave[1][w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      atomic_store_agent(p.lookback + tb, ((unsigned long long)(p.seq << 1) << 32) | t);
+    }
+  }
+  // ---- A's prefix while B's R2 planes are in flight
+  if (wave == 0) {
+    uint32_t e = 0;
+    if (!(p.diag & 1u)) e = lookback_pipe(p.lookback, ta, p.seq, tot_a, lane, &rec->error.v);
+    if (lane == 0) s_excl = e;
+  }
+  lds_barrier();  // A's prefix, B's wave counts
+  const uint32_t tot_b = pipe_tile_total<BLOCK>(s_wave[1], lane);
+  const uint32_t excl_a = s_excl;
+  if (wave == 0 && lane == 0 && tb < p.n_tiles && !(p.diag & 1u))  // B's inclusive: no look-back of its own
+    atomic_store_agent(p.lookback + tb,
+                       ((unsigned long long)((p.seq << 1) | 1u) << 32) | (excl_a + tot_a + tot_b));
+  const unsigned long long k_a = p.state->rng_next + excl_a;
+  uint32_t off_a = 0, off_b = 0;
+  {
+    const uint32_t sa = lane < WAVES ? s_wave[0][lane] : 0u, sb = lane < WAVES ? s_wave[1][lane] : 0u;
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+#pragma unroll
+    for (int w = 0; w < WAVES; w++) {
+      off_a += (w < wv) ? __builtin_amdgcn_readlane(sa, w) : 0u;
+      off_b += (w < wv) ? __builtin_amdgcn_readlane(sb, w) : 0u;
+    }
+  }
+  ref_finish_sub<N, W, BLOCK>(p, p.key, wa, toff_a, tid, A, k_a, off_a, tot_a, s_cls[0], s_blk, s_dec, z0, z1, z2,
+                              z3, acc);
+  // ---- tile B: decisions in registers (its R2 planes landed meanwhile), then the same
+  uint32_t blo_a[W], bhi_a[W], blo_b[W], bhi_b[W];
+#pragma unroll
+  for (int i = 0; i < W; i++)
+    r2_decision_ab<N, W>(r2lo, r2hi, i, p.q, p.self_lane, Bt.v1[i], Bt.vq[i], Bt.pd[i], blo_a[i], bhi_a[i],
+                         blo_b[i], bhi_b[i]);
+  ref_finish_sub<N, W, BLOCK>(p, p.key, wb, toff_b, tid, Bt, k_a + tot_a, off_b, tot_b, s_cls[1], s_blk, nullptr,
+                              blo_a, bhi_a, blo_b, bhi_b, acc);
+  if (p.diag & 2u) return;
+  publish_wg_record<BLOCK>(p, g, acc, tid, lane, wave);
+  if (g != G - 1) return;
+  persist_fold<BLOCK>(p, rec, G, tid, lane, wave);
+}
+
+// ============================================================================
 // Sharded REF: one engine (one StdRng stream) over a window split into
 // contiguous shards, one per GPU. Draw k of shard r sits at global
 // stream position  rng_next(window start) + VQ slots of shards 0..r-1 + k

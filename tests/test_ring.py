@@ -14,6 +14,7 @@ from rabia_amd.engine import PhaseEvaluator, PhaseWindow, decode_outputs
 pytestmark = pytest.mark.gpu
 
 RING = 6 << 8
+PAIR = 7 << 8
 TILED = 0x8000
 RES_CMP = ["n_slots", "n_decided", "n_v1", "n_pending_r1", "n_draws", "last_committed_max",
            "first_undecided", "rng_next", "commit_watermark"]
@@ -36,6 +37,21 @@ def run_ref(diag, n, q, self_lane, seed, rng_base, slot_base, r1, r2, max_phase=
     assert res["flags"] == 0
     assert st["rng_next"] == res["rng_next"] and st["last_committed"] == res["last_committed_max"]
     return decode_outputs(out, r1.shape[0]), res
+
+
+@pytest.mark.parametrize("S", [1, 33, 4097, 100003, (1 << 20) + 17, 3 << 20])
+@pytest.mark.parametrize("n", [3, 5, 9, 16])
+def test_pair_vs_oracle(oracle, n, S):
+    """The paired-tile kernel (two consecutive look-back tiles per workgroup, the
+    second without a look-back of its own), forced at every size."""
+    q = n // 2 + 1
+    for kind in (0, 1, 2):
+        r1, r2, _ = oracle.trace(kind, n, 3000 + S + n, 7, S)
+        exp, eres = oracle.ref_step(n, q, n // 2, 42, 123, 7, r1, r2, max_phase=7 + S // 2, lc_in=2, wm_in=7)
+        got, res = run_ref(PAIR, n, q, n // 2, 42, 123, 7, r1, r2, max_phase=7 + S // 2, lc_in=2, wm_in=7)
+        for k in exp:
+            np.testing.assert_array_equal(got[k], exp[k], err_msg=f"{k} kind {kind}")
+        assert {k: res[k] for k in RES_CMP} == {k: eres[k] for k in RES_CMP}
 
 
 @pytest.mark.parametrize("S", [1, 33, 4097, 100003, (1 << 20) + 17, 3 << 20])
@@ -69,6 +85,22 @@ def test_ring_many_draws_per_tile(oracle):
     assert {k: res[k] for k in RES_CMP} == {k: eres[k] for k in RES_CMP}
 
 
+def test_pair_many_draws_per_tile(oracle):
+    """All-'?' round 1 with the paired kernel: both tiles of every workgroup draw
+    65536 times (several ChaCha12 staging passes each)."""
+    n, q, S = 5, 3, (3 << 20) + 5
+    rng = np.random.default_rng(6)
+    r1 = np.full((S, n), 2, np.uint8)
+    r1[rng.random(S) < 0.01, 0] = 0
+    r1[rng.random(S) < 0.01, 1] = 1
+    r2 = rng.integers(0, 4, (S, n)).astype(np.uint8)
+    exp, eres = oracle.ref_step(n, q, 4, 9, 10 ** 9 + 3, 1, r1, r2)
+    got, res = run_ref(PAIR, n, q, 4, 9, 10 ** 9 + 3, 1, r1, r2)
+    for k in exp:
+        np.testing.assert_array_equal(got[k], exp[k], err_msg=k)
+    assert {k: res[k] for k in RES_CMP} == {k: eres[k] for k in RES_CMP}
+
+
 def test_ring_equals_tiled_bench_shape():
     """The bench's layout (slot-tiled 1024, n=5, agree90) at 2^26 slots, three
     consecutive steps on each kernel: identical output planes, step results and state."""
@@ -77,9 +109,9 @@ def test_ring_equals_tiled_bench_shape():
     nw = S // 32
     votes = [torch.empty((nw // T) * (4 * n + 1) * T, dtype=torch.int32, device="cuda") for _ in range(3)]
     outs = {d: [torch.empty((nw // T) * 8 * T, dtype=torch.int32, device="cuda") for _ in range(3)]
-            for d in (RING, TILED)}
+            for d in (RING, PAIR, TILED)}
     res, st = {}, {}
-    for d in (RING, TILED):
+    for d in (RING, PAIR, TILED):
         with PhaseEvaluator(n, self_lane=4, seed=42, tile_words=T) as ev:
             N.check(ev.lib.rg_debug_set(ev.ctx, d), ev.ctx)
             if d == RING:
@@ -92,8 +124,9 @@ def test_ring_equals_tiled_bench_shape():
                                     max_phase=3 * S - 999)
                 res[d].append(ev.last_result())
             st[d] = ev.get_state()
-    for i in range(3):
-        assert torch.equal(outs[RING][i], outs[TILED][i]), f"step {i}"
-        assert res[RING][i] == res[TILED][i], f"step {i}"
-        assert res[RING][i]["flags"] == 0 and res[RING][i]["n_draws"] > 0
-    assert st[RING] == st[TILED]
+    for d in (RING, PAIR):
+        for i in range(3):
+            assert torch.equal(outs[d][i], outs[TILED][i]), f"{d:#x} step {i}"
+            assert res[d][i] == res[TILED][i], f"{d:#x} step {i}"
+            assert res[d][i]["flags"] == 0 and res[d][i]["n_draws"] > 0
+        assert st[d] == st[TILED]
