@@ -12,11 +12,7 @@ extern "C" {
 /* diag bits: 1 skip the look-back wait (wrong draws), 2 skip per-tile statistics
  * and the step result, 4 record per-tile s_memrealtime stamps (100 MHz);
  * bits 8-10: 0 = automatic tile shape, 1 big (512 x W), 2 mid (256 x W), 3 small (128 x 1),
- *            4 big (512 x 2), 5 mid (256 x 2) (REF, n = 5 only),
- *            6 the persistent pipelined kernel (ref_pipe_kernel) at any size (REF rg_phase_step_async),
- *            7 the paired-tile kernel (ref_pair_kernel) at any size;
- * bits 12-13: pipe-kernel workgroups per CU (0 = up to 2); bit 15: large REF launches
- * use the tiled kernel even in a build that defaults to the pipe kernel;
+ *            4 big (512 x 2), 5 mid (256 x 2) (REF, n = 5 only);
  * bits 16-18 (REF, n = 5): 1 the round-1 tiled kernel (both rounds' planes live
  * across the look-back), 2 the tiled kernel at 6 waves per SIMD. */
 int rg_debug_set(rg_ctx* ctx, uint32_t diag);

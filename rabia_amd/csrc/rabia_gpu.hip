@@ -13,7 +13,6 @@
 #include <cstring>
 #include <new>
 #include <string>
-#include <vector>
 
 #include "rg_kernels.h"
 
@@ -53,8 +52,6 @@ struct rg_ctx {
   unsigned long long* cluster_part = nullptr;  // [blocks][kClusterStats]
   unsigned long long* cluster_stats = nullptr;  // [kClusterStats]
   unsigned long long* fix_acc = nullptr;        // sharded REF fix-up accumulator [4]
-  uint32_t cus = 0;                             // compute units (ring-kernel grid)
-  uint32_t* sink = nullptr;                     // 4 KiB for the ring kernel's placeholder stores
   std::string err;
 };
 
@@ -84,23 +81,13 @@ constexpr int wmax_for(int n) { return n <= 5 ? 4 : (n <= 10 ? 2 : 1); }
 // Tile shapes: {threads, words per thread}. Big tiles keep the per-launch count
 // of tiles and look-back hand-offs low on large windows; small tiles fill
 // the 256 CUs on single 2^20-slot windows.
-// kCfgRing: the persistent software-pipelined kernel (ref_pipe_kernel, 512 threads x W
-// words per tile), large REF rg_phase_step_async launches.
-enum TileCfg { kCfgBig = 0, kCfgMid = 1, kCfgSmall = 2, kCfgBigW2 = 3, kCfgMidW2 = 4, kCfgRing = 5,
-               kCfgPair = 6, kCfgLegacyBig = 7, kCfgDefBig6 = 8 };
-#ifndef RG_PAIR_DEFAULT
-#define RG_PAIR_DEFAULT 0
-#endif
-constexpr int kRingBlock = 512;
-#ifndef RG_RING_DEFAULT
-#define RG_RING_DEFAULT 0
-#endif
+enum TileCfg { kCfgBig = 0, kCfgMid = 1, kCfgSmall = 2, kCfgBigW2 = 3, kCfgMidW2 = 4, kCfgLegacyBig = 5,
+               kCfgDefBig6 = 6 };
 constexpr int cfg_block(int c) {
-  return (c == kCfgBig || c == kCfgBigW2 || c == kCfgPair || c == kCfgLegacyBig || c == kCfgDefBig6) ? 512
-                                                                                                 : (c == kCfgSmall ? 128 : 256);
+  return (c == kCfgBig || c == kCfgBigW2 || c == kCfgLegacyBig || c == kCfgDefBig6) ? 512 : (c == kCfgSmall ? 128 : 256);
 }
 inline int cfg_words(int c, int n) {
-  return c == kCfgSmall ? 1 : (c >= kCfgLegacyBig ? 4 : (c == kCfgPair ? wmax_for(n) : (c >= kCfgBigW2 ? 2 : wmax_for(n))));
+  return c == kCfgSmall ? 1 : (c >= kCfgLegacyBig ? 4 : (c >= kCfgBigW2 ? 2 : wmax_for(n)));
 }
 
 int pick_cfg(int n, uint64_t n_words) {
@@ -139,22 +126,6 @@ struct Disp {
     if (c == kCfgBig) hipLaunchKernelGGL((ref_step_kernel<N, WM, 512, false, 1>), dim3(grid), dim3(512), 0, s, p);
     else if (c == kCfgMid) hipLaunchKernelGGL((ref_step_kernel<N, WM, 256, false, 1>), dim3(grid), dim3(256), 0, s, p);
     else hipLaunchKernelGGL((ref_step_kernel<N, 1, 128, false, 1>), dim3(grid), dim3(128), 0, s, p);
-  }
-  // ring grid: every WG resident (forward progress of the look-back), at most
-  // `per_cu` per CU, never more WGs than tiles
-  static uint32_t ring_grid(uint32_t cus, uint32_t per_cu, uint32_t n_tiles) {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ref_pipe_kernel<N, WM, kRingBlock>, kRingBlock, 0) !=
-            hipSuccess || nb < 1)
-      nb = 1;
-    const uint32_t g = cus * ((uint32_t)nb < per_cu ? (uint32_t)nb : per_cu);
-    return g < n_tiles ? g : n_tiles;
-  }
-  static void pair(uint32_t grid, hipStream_t s, const StepParams& p) {
-    hipLaunchKernelGGL((ref_pair_kernel<N, WM, 512>), dim3(grid), dim3(512), 0, s, p);
-  }
-  static void ring(uint32_t grid, hipStream_t s, const StepParams& p) {
-    hipLaunchKernelGGL((ref_pipe_kernel<N, WM, kRingBlock>), dim3(grid), dim3(kRingBlock), 0, s, p);
   }
   static void wmvc(int c, uint32_t grid, hipStream_t s, const StepParams& p) {
     if (c == kCfgBig) hipLaunchKernelGGL((wmvc_step_kernel<N, WM, 512>), dim3(grid), dim3(512), 0, s, p);
@@ -195,11 +166,6 @@ using DigestLaunch = void (*)(uint32_t, hipStream_t, const uint64_t*, uint64_t, 
    &Disp<12>::fn, &Disp<13>::fn, &Disp<14>::fn, &Disp<15>::fn, &Disp<16>::fn}
 
 const StepLaunch kRefLaunch[17] = RG_TABLE(ref);
-using RingLaunch = void (*)(uint32_t, hipStream_t, const StepParams&);
-using RingGrid = uint32_t (*)(uint32_t, uint32_t, uint32_t);
-const RingLaunch kRingLaunch[17] = RG_TABLE(ring);
-const RingLaunch kPairLaunch[17] = RG_TABLE(pair);
-const RingGrid kRingGrid[17] = RG_TABLE(ring_grid);
 const StepLaunch kWmvcLaunch[17] = RG_TABLE(wmvc);
 const DigestLaunch kDigestLaunch[17] = RG_TABLE(digest);
 const ClusterLaunch kClusterLaunch[17] = RG_TABLE(cluster);
@@ -226,18 +192,12 @@ int ensure_tiles(rg_ctx* ctx, uint64_t n_tiles, bool force_zero) {
   if (n_tiles > ctx->tile_cap) {
     uint64_t cap = ctx->tile_cap ? ctx->tile_cap : 4096;
     while (cap < n_tiles) cap *= 2;
-    if (ctx->lookback) (void)hipFree(ctx->lookback - kLookbackGuard);
+    (void)hipFree(ctx->lookback);
     (void)hipFree(ctx->stats);
     ctx->lookback = nullptr;
     ctx->stats = nullptr;
     ctx->tile_cap = 0;
-    // kLookbackGuard granules in front of tile 0 read as "inclusive, 0" (rg_kernels.h
-    // lookback_pipe reads a fixed window without bounds checks); never rewritten
-    unsigned long long* base = nullptr;
-    RG_HIP(ctx, hipMalloc(&base, (cap + kLookbackGuard) * 8));
-    ctx->lookback = base + kLookbackGuard;
-    std::vector<unsigned long long> guard(kLookbackGuard, kGuardGranule);
-    RG_HIP(ctx, hipMemcpy(base, guard.data(), kLookbackGuard * 8, hipMemcpyHostToDevice));
+    RG_HIP(ctx, hipMalloc(&ctx->lookback, cap * 8));
     RG_HIP(ctx, hipMalloc(&ctx->stats, cap * kStatGranules * 8));
     ctx->tile_cap = cap;
   }
@@ -363,7 +323,7 @@ int rg_destroy(rg_ctx* ctx) {
   (void)hipFree(ctx->rec);
   (void)hipFree(ctx->state);
   (void)hipFree(ctx->result);
-  if (ctx->lookback) (void)hipFree(ctx->lookback - kLookbackGuard);
+  (void)hipFree(ctx->lookback);
   (void)hipFree(ctx->stats);
   (void)hipFree(ctx->dbg);
   (void)hipFree(ctx->r1v_cells);
@@ -373,7 +333,6 @@ int rg_destroy(rg_ctx* ctx) {
   (void)hipFree(ctx->cluster_part);
   (void)hipFree(ctx->cluster_stats);
   (void)hipFree(ctx->fix_acc);
-  (void)hipFree(ctx->sink);
   (void)hipFree(ctx->d_votes);
   (void)hipFree(ctx->d_out);
   (void)hipFree(ctx->d_user_result);
@@ -410,9 +369,6 @@ int rg_get_state(rg_ctx* ctx, rg_engine_state* st) {
   return RG_OK;
 }
 
-// Large REF launches take the ring kernel unless diag bit 15 asks for the tiled one.
-static bool ring_default(const rg_ctx* ctx) { return RG_RING_DEFAULT && !(ctx->diag & 0x8000u); }
-
 static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, uint64_t n_slots, uint64_t stride_words,
               uint64_t slot_base, uint64_t phase, uint64_t max_phase, rg_step_result* result_dev, void* stream,
               bool shard, uint64_t* records_dev, uint64_t records_cap) {
@@ -439,46 +395,13 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
   if (int rc = make_layout(ctx, kOutPlanes, n_words, stride_words, &lout, &need_out, "rg_phase_step")) return rc;
   uint32_t force = (ctx->diag >> 8) & 7u;  // diagnostics: force a tile shape
   if ((force == 4 || force == 5) && (n != 5 || wmvc || shard)) force = 0;
-  if ((force == 6 || force == 7) && (wmvc || shard)) force = 0;
+  if (force > 5) force = 0;
   const uint32_t dforce = (ctx->diag >> 16) & 7u;  // diagnostics: A/B shapes (REF, n = 5)
   if (dforce && (dforce > 2 || n != 5 || wmvc || shard)) return fail(ctx, RG_EINVAL, "rg_debug_set: bad shape");
   int cfg = dforce ? kCfgLegacyBig + (int)dforce - 1 : force ? (int)force - 1 : pick_cfg(n, n_words);
   uint64_t tile_words = (uint64_t)cfg_block(cfg) * cfg_words(cfg, n);
   uint64_t n_tiles = (n_words + tile_words - 1) / tile_words;
-  uint32_t ring_grid = 0;
-  if (!wmvc && !shard && (cfg == kCfgRing || (!force && ring_default(ctx)))) {
-    if (!ctx->sink) RG_HIP(ctx, hipMalloc(&ctx->sink, 4096));
-    if (!ctx->cus) {
-      int cus = 0;
-      RG_HIP(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->cfg.device));
-      ctx->cus = cus > 0 ? (uint32_t)cus : 1u;
-    }
-    const uint64_t rt = (n_words + (uint64_t)kRingBlock * wmax_for(n) - 1) / ((uint64_t)kRingBlock * wmax_for(n));
-    const uint32_t per_cu = (ctx->diag >> 12) & 3u ? (ctx->diag >> 12) & 3u : 2u;
-    const uint32_t gr = kRingGrid[n](ctx->cus, per_cu, (uint32_t)(rt < 0xFFFFFFFFull ? rt : 0xFFFFFFFFull));
-    // the pipeline pays off once every WG has a few tiles (forced: any size); the
-    // kernel's per-thread counters are 16-bit: at most 65535 slots per thread
-    const uint64_t per_wg = gr ? (rt + gr - 1) / gr : 0;
-    if (gr && per_wg * wmax_for(n) * 32 < 65536 && (cfg == kCfgRing || rt >= 4ull * gr)) {
-      cfg = kCfgRing;
-      tile_words = (uint64_t)kRingBlock * wmax_for(n);
-      n_tiles = rt;
-      ring_grid = gr;
-    }
-  }
-  // paired tiles: one workgroup per two consecutive tiles of the look-back chain
-  uint32_t pair_grid = 0;
-  if (!wmvc && !shard && !dforce && (cfg == kCfgPair || (!force && cfg == kCfgBig && RG_PAIR_DEFAULT &&
-                                                         !(ctx->diag & 0x8000u)))) {
-    cfg = kCfgPair;
-    tile_words = 512ull * wmax_for(n);
-    n_tiles = (n_words + tile_words - 1) / tile_words;
-    pair_grid = (uint32_t)((n_tiles + 1) / 2);
-  }
-  // (the persistent and paired kernels' per-WG records take 4 granules per WG of the
-  // 2 per tile allocated)
-  uint64_t gran_tiles = n_tiles > 2ull * ring_grid ? n_tiles : 2ull * ring_grid;
-  if (pair_grid && gran_tiles < 2ull * pair_grid) gran_tiles = 2ull * pair_grid;
+  const uint64_t gran_tiles = n_tiles;
   if (int rc = ensure_tiles(ctx, gran_tiles, false)) return rc;
   // Statistics granules carry 12 bits of seq and look-back granules 31: start a
   // fresh epoch on zeroed granules whenever either wraps.
@@ -513,7 +436,6 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
   p.dbg = nullptr;
   p.vq_rec = reinterpret_cast<unsigned long long*>(records_dev);
   p.vq_cap = records_cap;
-  p.sink = ctx->sink;
   if (ctx->diag & 4u) {
     if (ctx->dbg_cap < n_tiles * 8) {
       RG_HIP(ctx, hipDeviceSynchronize());
@@ -527,8 +449,6 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
   }
   hipStream_t s = pick_stream(ctx, stream);
   if (shard) launch_ref_shard(n, cfg_block(cfg), cfg_words(cfg, n), (uint32_t)n_tiles, s, p);
-  else if (cfg == kCfgRing) kRingLaunch[n](ring_grid, s, p);
-  else if (cfg == kCfgPair) kPairLaunch[n](pair_grid, s, p);
   else (wmvc ? kWmvcLaunch : kRefLaunch)[n](cfg, (uint32_t)n_tiles, s, p);
   RG_HIP(ctx, hipGetLastError());
   return RG_OK;

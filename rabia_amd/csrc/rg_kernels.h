@@ -53,7 +53,6 @@ struct StepParams {
   unsigned long long* dbg;        // [n_tiles][8] s_memrealtime stamps when diag & 4
   unsigned long long* vq_rec;     // sharded REF: draw records [vq_cap] (rg_common.h)
   uint64_t vq_cap;
-  uint32_t* sink;                 // ring kernel: 4 KiB the prologue's placeholder stores go to
 };
 
 // finish_tile flavours
@@ -353,67 +352,6 @@ __device__ __forceinline__ uint32_t lookback_exclusive_wide(unsigned long long* 
   return excl;
 }
 
-// Look-back of the persistent pipelined kernel: the caller published the tile's
-// aggregate already; one poll reads the 512 predecessor granules at constant
-// offsets from one address (8 loads per lane in flight). Indices below 0 read the
-// guard granules the host keeps in front of tile 0 (tag 0xFFFFFFFF = inclusive 0).
-constexpr int kLookbackGuard = 512;
-constexpr unsigned long long kGuardGranule = 0xFFFFFFFFull << 32;
-__device__ __forceinline__ uint32_t lookback_pipe(unsigned long long* status, uint32_t tile, uint32_t seq,
-                                                  uint32_t agg, int lane, unsigned long long* err) {
-  constexpr int K = 8;
-  const uint32_t tag_inc = (seq << 1) | 1u;
-  if (tile == 0) {
-    if (lane == 0) atomic_store_agent(status, ((unsigned long long)tag_inc << 32) | agg);
-    return 0;
-  }
-  uint32_t excl = 0;
-  int64_t pos = (int64_t)tile - 1;  // distance 0 = tile - 1
-  uint32_t spins = 0;
-  for (;;) {
-    unsigned long long* b = status + (pos - lane);
-    unsigned long long g[K];
-#pragma unroll
-    for (int k = 0; k < K; k++) g[k] = atomic_load_agent(b - 64 * k);
-    int first = 64 * K;
-    bool blocked = false;
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-      const uint32_t tag = (uint32_t)(g[k] >> 32);
-      const bool guard = tag == 0xFFFFFFFFu;
-      const bool ready = guard || (tag >> 1) == seq;
-      const unsigned long long im = __ballot(ready && (tag & 1u));
-      const unsigned long long nr = __ballot(!ready);
-      if (first == 64 * K) {
-        const int f = im ? __builtin_ctzll(im) : 64;
-        const unsigned long long need = f >= 63 ? ~0ull : ((2ull << f) - 1ull);
-        if (nr & need) { blocked = true; break; }
-        if (f < 64) first = 64 * k + f;
-      }
-    }
-    if (blocked) {
-      if (++spins > (1u << 22)) {  // ~seconds: a protocol fault, not a wait
-        if (lane == 0) {
-          atomicOr(err, 1ull);
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-      continue;
-    }
-    uint32_t v = 0;
-#pragma unroll
-    for (int k = 0; k < K; k++)
-      if (64 * k + lane <= first) v += (uint32_t)g[k];
-    excl += (uint32_t)wave_sum64(v);
-    if (first < 64 * K) break;
-    pos -= 64 * K;
-  }
-  if (lane == 0) atomic_store_agent(status + tile, ((unsigned long long)tag_inc << 32) | (agg + excl));
-  return excl;
-}
-
 // ---- per-tile statistics -> granules; the last tile reduces them ------------
 // Per tile, two 8-B granules written with agent-scope stores by one lane:
 //   g0 = tag:13 | n_decided:17 | n_v1:17 | n_pending_r1:17
@@ -687,78 +625,6 @@ __device__ __forceinline__ void load_planes(const StepParams& p, uint64_t w0, bo
 #pragma unroll
       for (int i = 0; i < W; i++) lo[j][i] = hi[j][i] = ~0u;
   }
-}
-
-// per-WG statistics record: 4 tagged granules (tag 12 bits at [52, 64))
-//   g0 = dec:26 | v1:26 << 26      g1 = pend:26 | draws:26 << 26
-//   g2 = (largest accepted V1 offset + 1, 0 = none):33   g3 = smallest undecided offset (2^33-1 = none):33
-constexpr int kPersistStatGranules = 4;
-constexpr unsigned long long kOff33 = (1ull << 33) - 1;
-__device__ __forceinline__ unsigned long long pstat_tag(uint32_t seq) {
-  return (unsigned long long)(0x800u | (seq & 0x7FFu)) << 52;
-}
-
-// WG 0 of a persistent launch: fold the G per-WG records, advance the engine
-// state, write the step result (TOTAL = threads per WG).
-template <int TOTAL>
-__device__ __forceinline__ void persist_fold(const StepParams& p, Record* rec, uint32_t G, int tid, int lane,
-                                             int wave) {
-  unsigned long long v[7] = {0, 0, 0, 0, 0, ~0ull, 0};  // dec v1 pend draws max(id+1) min(id) fault
-  const unsigned long long tag = pstat_tag(p.seq);
-  constexpr unsigned long long kTagMask = ~0ull << 52, kMask26 = (1ull << 26) - 1;
-  for (uint32_t wg = tid; wg < G; wg += TOTAL) {
-    unsigned long long* gp = p.stats + (uint64_t)wg * kPersistStatGranules;
-    unsigned long long gv[4];
-#pragma unroll
-    for (int k2 = 0; k2 < 4; k2++) gv[k2] = atomic_load_agent(gp + k2);
-    uint32_t spins = 0;
-    for (;;) {
-      bool ready = true;
-#pragma unroll
-      for (int k2 = 0; k2 < 4; k2++) ready &= (gv[k2] & kTagMask) == tag;
-      if (ready) break;
-      if (++spins > kSpinLimit) { v[6] = 2; break; }
-      __builtin_amdgcn_s_sleep(2);
-#pragma unroll
-      for (int k2 = 0; k2 < 4; k2++)
-        if ((gv[k2] & kTagMask) != tag) gv[k2] = atomic_load_agent(gp + k2);
-    }
-    v[0] += gv[0] & kMask26;
-    v[1] += (gv[0] >> 26) & kMask26;
-    v[2] += gv[1] & kMask26;
-    v[3] += (gv[1] >> 26) & kMask26;
-    const unsigned long long mx = gv[2] & kOff33, mn = gv[3] & kOff33;
-    if (mx && p.slot_base + mx > v[4]) v[4] = p.slot_base + mx;
-    if (mn != kOff33 && p.slot_base + mn < v[5]) v[5] = p.slot_base + mn;
-  }
-  block_reduce_totals<TOTAL>(v, lane, wave);
-  if (tid != 0) return;
-  const unsigned long long err = atomicAdd(&rec->error.v, 0ull) | v[6];
-  DevState st = *p.state;
-  DevResult r;
-  r.n_slots = p.n_slots;
-  r.n_decided = v[0];
-  r.n_v1 = v[1];
-  r.n_pending_r1 = v[2];
-  r.n_draws = v[3];
-  const unsigned long long end = p.slot_base + p.n_slots;
-  const unsigned long long fu = v[5] < end ? v[5] : end;
-  unsigned long long lc = st.last_committed;  // commit_phase: monotonic max, state.rs:77-99
-  if (v[4] && v[4] - 1 > lc) lc = v[4] - 1;
-  unsigned long long wm = st.commit_watermark;
-  if (p.slot_base <= wm && wm < fu) wm = fu;
-  r.last_committed_max = lc;
-  r.first_undecided = fu;
-  r.rng_next = st.rng_next + r.n_draws;
-  r.commit_watermark = wm;
-  r.flags = err;
-  st.rng_next = r.rng_next;
-  st.last_committed = lc;
-  st.commit_watermark = wm;
-  st.steps += 1;
-  *p.state = st;
-  *p.result = r;
-  if (p.result_user) *p.result_user = r;
 }
 
 // Plane loads without a branch: a thread past the window loads word 0 instead
@@ -1039,7 +905,27 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_step_kernel(StepParams p) {
   unsigned long long kr = k_first - k_base;  // SHARD: local draw number of this thread's first VQ slot
 #pragma unroll
   for (int i = 0; i < W; i++) {
-    if constexpr (SHARD) {
+    if constexpr (DEF != 0) {
+      const uint32_t sel = own_lo[i] & r1vq[i];  // VQ slots whose draw gave V1
+      dlo[i] = (dalo[i] & ~sel) | (dblo[i] & sel);
+      dhi[i] = (dahi[i] & ~sel) | (dbhi[i] & sel);
+      if constexpr (SHARD) {  // draw records: both decisions are at hand already
+        uint32_t m = r1vq[i];
+        const uint32_t gtm = m ? s_cls[2 * i][tid] : 0u, ltm = m ? s_cls[2 * i + 1][tid] : 0u;
+        while (m) {  // indexed by local draw number (ascending slot order)
+          const int b = __builtin_ctz(m);
+          m &= m - 1;
+          const uint32_t own = (own_lo[i] >> b) & 1u;
+          const uint32_t d_v0 = ((dalo[i] >> b) & 1u) | (((dahi[i] >> b) & 1u) << 1);
+          const uint32_t d_v1 = ((dblo[i] >> b) & 1u) | (((dbhi[i] >> b) & 1u) << 1);
+          const uint32_t cls = ((gtm >> b) & 1u) ? kRecGt : (((ltm >> b) & 1u) ? kRecLt : 0u);
+          const uint32_t info = cls | (d_v0 << 2) | (d_v1 << 4) | (own << 6);
+          const uint32_t off = (uint32_t)(32u * (w0 + i) + b);
+          if (kr < p.vq_cap) p.vq_rec[kr] = ((unsigned long long)info << 32) | off;
+          kr++;
+        }
+      }
+    } else if constexpr (SHARD) {
       uint32_t alo = 0, ahi = 0;
       if (r1vq[i]) {  // the decision under the other own vote, for the draw records
 #pragma unroll
@@ -1075,10 +961,6 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_step_kernel(StepParams p) {
         if (kr < p.vq_cap) p.vq_rec[kr] = ((unsigned long long)info << 32) | off;
         kr++;
       }
-    } else if constexpr (DEF != 0) {
-      const uint32_t sel = own_lo[i] & r1vq[i];  // VQ slots whose draw gave V1
-      dlo[i] = (dalo[i] & ~sel) | (dblo[i] & sel);
-      dhi[i] = (dahi[i] & ~sel) | (dbhi[i] & sel);
     } else {
 #pragma unroll
       for (int j = 0; j < N; j++)
@@ -1130,526 +1012,6 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_step_kernel(StepParams p) {
   const TileStats ts = thread_stats<W>(st_dec, st_v1, pend, st_vm, vq_count, w0, tw0, p);
   finish_tile<SHARD ? kFinShard : kFinRef, BLOCK, W, (OCC > 4 ? 2 : 8)>(p, rec, ts, tile, tid, lane, wave);
   stamp(p, tile, 4, tid);
-}
-
-// ============================================================================
-// Persistent software-pipelined REF step (large rg_phase_step_async launches).
-// G workgroups, all resident (the host sizes G from the occupancy query); WG g
-// owns tiles g, g + G, g + 2G, ... A tile's round-1 tally and both-outcome
-// round-2 decisions (r2_decision_ab) run as soon as its planes land, which leaves
-// 7 words of state per thread word (V1/VQ/pending masks, decision A and B); the
-// planes of the WG's NEXT tile are then in flight while wave 0 looks back for the
-// current tile's VQ prefix, so the look-back's round trip (which queues behind
-// the CU's own plane loads) overlaps HBM traffic instead of holding an idle tile.
-// Per iteration:
-//   issue the next tile's R1 + R2 loads | wave 0: look back (one wide poll over the
-//   512 predecessors: this iteration's tiles published aggregates one step earlier,
-//   the previous iteration's tiles are inclusive) | tally + decisions of the next
-//   tile | barrier | wave 0 publishes the next tile's aggregate | ChaCha12 blocks,
-//   draws, own votes and the 8 output planes of the current tile.
-// Forward progress: a tile's look-back needs only aggregates published before the
-// previous barrier of every WG and inclusives of the previous iteration; every WG
-// is resident; the spin is bounded (Record.error -> RG_ESTATE). Statistics
-// accumulate per WG in registers and WG 0 folds the G per-WG records.
-// ============================================================================
-template <int W>
-struct PipeTile {  // one tile's round-1 state between its tally and its stores
-  uint32_t v1[W], vq[W], pd[W];
-  uint32_t cnt, incl;
-};
-
-// Round 1 of one tile (engine.rs:495-505) word after word: V1 / VQ / pending masks,
-// the VQ slots' (c1 > c0), (c1 < c0) masks into LDS, the VQ count and its wave scan.
-template <int N, int W, int BLOCK>
-__device__ __forceinline__ void pipe_tally(const StepParams& p, uint64_t w0, const uint32_t (&r1lo)[N][W],
-                                           const uint32_t (&r1hi)[N][W], uint32_t (*cls)[BLOCK], int tid, int lane,
-                                           PipeTile<W>& t) {
-  constexpr int B = ctr_bits(N);
-  uint32_t seq0 = 0, cnt = 0;
-#pragma unroll
-  for (int i = 0; i < W; i++) {
-    const uint32_t vm = valid_mask(w0 + i, p.n_words, p.n_slots);
-    Ctr<B> c0, c1, cp;
-    ctr_zero(c0); ctr_zero(c1); ctr_zero(cp);
-    c0.b[0] = c1.b[0] = cp.b[0] = seq0;  // word i+1 after word i (no 4-word ILP: registers)
-#pragma unroll
-    for (int j = 0; j < N; j++) {
-      const uint32_t lo = r1lo[j][i], hi = r1hi[j][i];
-      ctr_add(c0, ~lo & ~hi);
-      ctr_add(c1, lo & ~hi);
-      ctr_add(cp, ~(lo & hi));
-    }
-    const uint32_t g0 = ctr_ge(c0, p.q), g1 = ctr_ge(c1, p.q), gp = ctr_ge(cp, p.q);
-    t.v1[i] = ~g0 & g1 & vm;
-    t.vq[i] = ~g0 & ~g1 & gp & vm;
-    t.pd[i] = ~((g0 & vm) | t.v1[i] | t.vq[i]) & vm;
-    uint32_t gt, lt;
-    ctr_cmp(c1, c0, gt, lt);
-    cls[2 * i][tid] = gt & t.vq[i];
-    cls[2 * i + 1][tid] = lt & t.vq[i];
-    cnt += __builtin_popcount(t.vq[i]);
-    asm volatile("" : "+v"(seq0), "+v"(t.v1[i]), "+v"(t.vq[i]), "+v"(t.pd[i]));
-  }
-  t.cnt = cnt;
-  t.incl = wave_incl_scan32(cnt, lane);
-}
-
-// Both-outcome round-2 decisions of one tile into LDS (4 words per thread word).
-template <int N, int W, int BLOCK>
-__device__ __forceinline__ void pipe_decide(const StepParams& p, const uint32_t (&r2lo)[N][W],
-                                            const uint32_t (&r2hi)[N][W], const PipeTile<W>& t,
-                                            uint32_t (*dec)[BLOCK], int tid) {
-#pragma unroll
-  for (int i = 0; i < W; i++) {
-    uint32_t alo, ahi, blo, bhi;
-    r2_decision_ab<N, W>(r2lo, r2hi, i, p.q, p.self_lane, t.v1[i], t.vq[i], t.pd[i], alo, ahi, blo, bhi);
-    dec[4 * i][tid] = alo;
-    dec[4 * i + 1][tid] = ahi;
-    dec[4 * i + 2][tid] = blo;
-    dec[4 * i + 3][tid] = bhi;
-  }
-}
-
-template <int BLOCK>
-__device__ __forceinline__ uint32_t pipe_tile_total(const uint32_t* sw_lds, int lane) {
-  constexpr int WAVES = BLOCK / 64;
-  const uint32_t sw = lane < WAVES ? sw_lds[lane] : 0u;
-  uint32_t t = 0;
-#pragma unroll
-  for (int w = 0; w < WAVES; w++) t += __builtin_amdgcn_readlane(sw, w);
-  return t;
-}
-
-template <int N, int W, int BLOCK, int OCC = 4>
-__global__ __launch_bounds__(BLOCK, OCC) void ref_pipe_kernel(StepParams p) {
-  constexpr int WAVES = BLOCK / 64;
-  constexpr uint64_t kTW = (uint64_t)BLOCK * W;
-  constexpr int kRows = 128;                   // ChaCha12 blocks (1024 draws) staged per pass
-  __shared__ uint32_t s_wave[2][WAVES];        // per-wave inclusive VQ counts, by tile parity
-  __shared__ uint32_t s_excl;                  // the current tile's exclusive VQ prefix
-  __shared__ uint32_t s_cls[2][2 * W][BLOCK];  // (c1 > c0), (c1 < c0) of the VQ slots, by tile parity
-  __shared__ uint32_t s_dec[4 * W][BLOCK];     // the current tile's decisions for own V0 / own V1
-  __shared__ uint32_t s_blk[kRows][17];
-  Record* rec = p.rec + (p.seq & 1u);
-  const int tid0 = threadIdx.x, lane0 = tid0 & 63, wave = tid0 >> 6;
-  const int tid = tid0, lane = lane0;
-  const uint32_t G = gridDim.x, g = blockIdx.x;
-  const uint32_t nt = (p.n_tiles - g + G - 1) / G;  // this WG's tiles (>= 1: the host keeps G <= n_tiles)
-  if (g == 0 && tid == 0) atomic_store_agent(&p.rec[(p.seq + 1) & 1u].error.v, 0ull);
-  const unsigned long long k_base = p.state->rng_next;
-  const uint32_t tw0 = (uint32_t)tid * W;
-  uint32_t a_cnt0 = 0, a_cnt1 = 0;                 // dec | v1 << 16, pend | draws << 16 (per thread <= 2^16)
-  uint32_t a_max1 = 0, a_min = 0xFFFFFFFFu;        // launch-relative slot offsets (n_slots < 2^32)
-
-  PipeTile<W> cur;
-  {  // prologue: tile g
-    uint32_t r1lo[N][W], r1hi[N][W], r2lo[N][W], r2hi[N][W];
-    const uint64_t w0 = (uint64_t)g * kTW + tw0;
-    load_planes_any<N, W>(p, w0, 0, r1lo, r1hi);
-    load_planes_any<N, W>(p, w0, 2 * N, r2lo, r2hi);
-    pipe_tally<N, W, BLOCK>(p, w0, r1lo, r1hi, s_cls[0], tid, lane, cur);
-    if (lane == 63) s_wave[0][wave] = cur.incl;
-    pipe_decide<N, W, BLOCK>(p, r2lo, r2hi, cur, s_dec, tid);
-  }
-  lds_barrier();
-  uint32_t cur_total = pipe_tile_total<BLOCK>(s_wave[0], lane);
-  if (wave == 0 && lane == 0 && !(p.diag & 1u))
-    atomic_store_agent(p.lookback + g, ((unsigned long long)(p.seq << 1) << 32) | cur_total);
-
-  for (uint32_t j = 0; j < nt; j++) {
-    // Loop-variant copies of the thread index and the key: otherwise LICM hoists the
-    // LDS / shuffle addresses and the key-only part of ChaCha's first round out of
-    // the loop and keeps ~40 of them live across it (spills at 128 VGPRs).
-    int tid = tid0, lane = lane0;
-    asm volatile("" : "+v"(tid), "+v"(lane));
-    Key key = p.key;
-#pragma unroll
-    for (int z = 0; z < 8; z++) asm volatile("" : "+s"(key.k[z]));
-    const uint32_t tw0 = (uint32_t)tid * W;
-    const uint32_t tile = g + j * G;
-    const uint64_t w0 = (uint64_t)tile * kTW + tw0;
-    const uint64_t nw0 = w0 + (uint64_t)G * kTW;
-    const bool more = j + 1 < nt;
-    // ---- the next tile's planes in flight (unconditional: past the end they read word 0)
-    uint32_t r1lo[N][W], r1hi[N][W], r2lo[N][W], r2hi[N][W];
-    load_planes_any<N, W>(p, nw0, 0, r1lo, r1hi);
-    // ---- look-back for the current tile (its aggregate is published already)
-    if (wave == 0) {
-      uint32_t e = 0;
-      if (!(p.diag & 1u))
-        e = lookback_pipe(p.lookback, tile, p.seq, cur_total, lane, &rec->error.v);
-      if (lane == 0) s_excl = e;
-    }
-    // ---- round 1 of the next tile; then its R2 planes (in flight across the draws
-    // and stores of the current tile; the R1 registers are free by then)
-    PipeTile<W> nxt;
-    pipe_tally<N, W, BLOCK>(p, nw0, r1lo, r1hi, s_cls[(j + 1) & 1], tid, lane, nxt);
-    load_planes_any<N, W>(p, nw0, 2 * N, r2lo, r2hi);
-    if (lane == 63) s_wave[(j + 1) & 1][wave] = more ? nxt.incl : 0u;
-    lds_barrier();  // s_excl of the current tile, s_wave of the next
-    const uint32_t nxt_total = pipe_tile_total<BLOCK>(s_wave[(j + 1) & 1], lane);
-    if (more && wave == 0 && lane == 0 && !(p.diag & 1u))
-      atomic_store_agent(p.lookback + tile + G, ((unsigned long long)(p.seq << 1) << 32) | nxt_total);
-
-    // ---- own round-2 votes of the current tile (engine.rs:523-537, 567-611)
-    uint32_t wave_off = 0;
-    {
-      const uint32_t sw = lane < WAVES ? s_wave[j & 1][lane] : 0u;
-      const int wv = __builtin_amdgcn_readfirstlane(wave);
-#pragma unroll
-      for (int w = 0; w < WAVES; w++) wave_off += (w < wv) ? __builtin_amdgcn_readlane(sw, w) : 0u;
-    }
-    const unsigned long long k_tile = k_base + s_excl;
-    unsigned long long k = k_tile + wave_off + cur.incl - cur.cnt;
-    uint32_t own_lo[W], mq[W];
-#pragma unroll
-    for (int i = 0; i < W; i++) {
-      own_lo[i] = cur.v1[i];
-      mq[i] = cur.vq[i];
-    }
-    if (cur_total) {
-      const unsigned long long b_first = k_tile >> 3, b_last = (k_tile + cur_total - 1) >> 3;
-      for (unsigned long long cb = b_first; cb <= b_last; cb += kRows) {
-        if (tid < kRows && cb + tid <= b_last) {
-          uint32_t x[16];
-          chacha_block<12>(key, cb + tid, 0, x);
-#pragma unroll
-          for (int z = 0; z < 16; z++) s_blk[tid][z] = x[z];
-        }
-        lds_barrier();
-        const unsigned long long k_lim = (cb + kRows) << 3;
-#pragma unroll
-        for (int i = 0; i < W; i++) {
-          if (!mq[i] || k >= k_lim) continue;
-          const uint32_t gtm = s_cls[j & 1][2 * i][tid], ltm = s_cls[j & 1][2 * i + 1][tid];
-          while (mq[i] && k < k_lim) {
-            const int b = __builtin_ctz(mq[i]);
-            mq[i] &= mq[i] - 1;
-            const uint32_t row = (uint32_t)((k >> 3) - cb), ws = (uint32_t)(k & 7u) * 2u;
-            const unsigned long long u =
-                (unsigned long long)s_blk[row][ws] | ((unsigned long long)s_blk[row][ws + 1] << 32);
-            const bool gt = (gtm >> b) & 1u, lt = (ltm >> b) & 1u;
-            const bool v1 = gt ? (u < kP90) : (lt ? (u >= kP90) : (u < kP80));
-            own_lo[i] |= (uint32_t)v1 << b;
-            k++;
-          }
-        }
-        lds_barrier();
-      }
-    }
-    // ---- decision with the own vote (engine.rs:540-542, 613-628), stores, statistics
-    uint32_t dlo[W], dhi[W];
-    const uint32_t toff = (uint32_t)(32u * (uint64_t)tile * kTW) + 32u * tw0;  // launch-relative slot offset
-#pragma unroll
-    for (int i = 0; i < W; i++) {
-      const uint32_t sel = own_lo[i] & cur.vq[i];
-      dlo[i] = (s_dec[4 * i][tid] & ~sel) | (s_dec[4 * i + 2][tid] & sel);
-      dhi[i] = (s_dec[4 * i + 1][tid] & ~sel) | (s_dec[4 * i + 3][tid] & sel);
-      const uint32_t vm = valid_mask(w0 + i, p.n_words, p.n_slots);
-      dlo[i] &= vm;
-      dhi[i] &= vm;
-      const uint32_t d1 = dlo[i] & ~dhi[i], dc = ~dhi[i] & vm;
-      a_cnt0 += __builtin_popcount(dc) | (__builtin_popcount(d1) << 16);
-      a_cnt1 += __builtin_popcount(cur.pd[i]);
-      const uint32_t v1l = d1 & phase_limit_mask(p.slot_base, w0 + i, p.max_phase);
-      if (v1l) {
-        const uint32_t m1 = toff + 32u * i + (31u - __builtin_clz(v1l)) + 1u;
-        a_max1 = m1 > a_max1 ? m1 : a_max1;
-      }
-      const uint32_t und = ~dc & vm;
-      if (und) {
-        const uint32_t mn = toff + 32u * i + __builtin_ctz(und);
-        a_min = mn < a_min ? mn : a_min;
-      }
-    }
-    a_cnt1 += cur.cnt << 16;
-    if (w0 < p.n_words) {  // plane by plane (include/rabia_gpu.h output planes)
-      uint32_t* ob = p.out + p.lout.base(w0);
-      const uint64_t ps = p.lout.pstride;
-      uint32_t v[W];
-#pragma unroll
-      for (int i = 0; i < W; i++) v[i] = cur.v1[i] | cur.pd[i];
-      store_words_nt<W>(ob, v);
-#pragma unroll
-      for (int i = 0; i < W; i++) v[i] = cur.vq[i] | cur.pd[i];
-      store_words_nt<W>(ob + ps, v);
-#pragma unroll
-      for (int i = 0; i < W; i++) v[i] = own_lo[i] | cur.pd[i];
-      store_words_nt<W>(ob + 2 * ps, v);
-      store_words_nt<W>(ob + 3 * ps, cur.pd);
-      store_words_nt<W>(ob + 4 * ps, dlo);
-      store_words_nt<W>(ob + 5 * ps, dhi);
-#pragma unroll
-      for (int i = 0; i < W; i++) v[i] = ~dhi[i] & valid_mask(w0 + i, p.n_words, p.n_slots);
-      store_words_nt<W>(ob + 6 * ps, v);  // set_decision: committed iff not VQuestion
-#pragma unroll
-      for (int i = 0; i < W; i++) v[i] = dlo[i] & ~dhi[i];
-      store_words_nt<W>(ob + 7 * ps, v);  // V1: apply_batch + commit_phase
-    }
-    lds_barrier();  // every thread read the current tile's s_dec
-    pipe_decide<N, W, BLOCK>(p, r2lo, r2hi, nxt, s_dec, tid);  // the next tile's, from its R2 planes
-    cur = nxt;
-    cur_total = nxt_total;
-  }
-
-  // ---- per-WG record (persist_fold), folded by WG 0
-  if (p.diag & 2u) return;
-  {
-    __shared__ unsigned long long red[WAVES][4];
-    const unsigned long long c0 = a_cnt0, c1 = a_cnt1;
-    const unsigned long long s0 = wave_sum64((c0 & 0xFFFFu) | ((c0 >> 16) << 26));
-    const unsigned long long s1 = wave_sum64((c1 & 0xFFFFu) | ((c1 >> 16) << 26));
-    const unsigned long long mx = wave_max64(a_max1);
-    const unsigned long long mn = wave_min64(a_min == 0xFFFFFFFFu ? kOff33 : (unsigned long long)a_min);
-    if (lane == 0) { red[wave][0] = s0; red[wave][1] = s1; red[wave][2] = mx; red[wave][3] = mn; }
-    lds_barrier();
-    if (tid == 0) {
-      unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = kOff33;
-#pragma unroll 1
-      for (int w = 0; w < WAVES; w++) {
-        t0 += red[w][0]; t1 += red[w][1];
-        t2 = red[w][2] > t2 ? red[w][2] : t2;
-        t3 = red[w][3] < t3 ? red[w][3] : t3;
-      }
-      const unsigned long long tag = pstat_tag(p.seq);
-      unsigned long long* gr = p.stats + (uint64_t)g * kPersistStatGranules;
-      atomic_store_agent(gr + 0, tag | t0);
-      atomic_store_agent(gr + 1, tag | t1);
-      atomic_store_agent(gr + 2, tag | t2);
-      atomic_store_agent(gr + 3, tag | t3);
-    }
-  }
-  if (g != 0) return;
-  persist_fold<BLOCK>(p, rec, G, tid, lane, wave);
-}
-
-// ============================================================================
-// Paired REF step (large rg_phase_step_async launches): each workgroup owns two
-// consecutive tiles A = 2b, B = 2b + 1 of the look-back chain. A is tallied and its
-// both-outcome decisions parked in LDS; then B's planes are loaded while wave 0
-// looks back for A, so A's wait for its predecessors overlaps B's HBM traffic, and
-// B needs no look-back of its own (its prefix is A's inclusive value). Half as many
-// look-backs as tiles, each hidden behind a tile's loads.
-// ============================================================================
-struct SubAcc {  // per-thread statistics over a workgroup's tiles
-  uint32_t cnt0 = 0, cnt1 = 0;                   // dec | v1 << 16, pend | draws << 16
-  uint32_t max1 = 0, min = 0xFFFFFFFFu;          // launch-relative slot offsets (+1 for max)
-};
-
-// Draws, own votes, decisions, stores and statistics of one tile whose exclusive VQ
-// prefix is known. Decisions for own V0 / V1 come from LDS (dec != nullptr) or from
-// the register arrays.
-template <int N, int W, int BLOCK>
-__device__ __forceinline__ void ref_finish_sub(const StepParams& p, const Key& key, uint64_t w0, uint32_t toff,
-                                               int tid, const PipeTile<W>& t, unsigned long long k_tile,
-                                               uint32_t wave_off, uint32_t total, uint32_t (*cls)[BLOCK],
-                                               uint32_t (*blk)[17], uint32_t (*dec)[BLOCK],
-                                               const uint32_t (&alo)[W], const uint32_t (&ahi)[W],
-                                               const uint32_t (&blo)[W], const uint32_t (&bhi)[W], SubAcc& acc) {
-  constexpr int kRows = 128;
-  unsigned long long k = k_tile + wave_off + t.incl - t.cnt;
-  uint32_t own_lo[W], mq[W];
-#pragma unroll
-  for (int i = 0; i < W; i++) {
-    own_lo[i] = t.v1[i];
-    mq[i] = t.vq[i];
-  }
-  if (total) {  // ChaCha12 blocks of the tile's draw range, staged in LDS (engine.rs:567-611)
-    const unsigned long long b_first = k_tile >> 3, b_last = (k_tile + total - 1) >> 3;
-    for (unsigned long long cb = b_first; cb <= b_last; cb += kRows) {
-      if (tid < kRows && cb + tid <= b_last) {
-        uint32_t x[16];
-        chacha_block<12>(key, cb + tid, 0, x);
-#pragma unroll
-        for (int z = 0; z < 16; z++) blk[tid][z] = x[z];
-      }
-      lds_barrier();
-      const unsigned long long k_lim = (cb + kRows) << 3;
-#pragma unroll
-      for (int i = 0; i < W; i++) {
-        if (!mq[i] || k >= k_lim) continue;
-        const uint32_t gtm = cls[2 * i][tid], ltm = cls[2 * i + 1][tid];
-        while (mq[i] && k < k_lim) {
-          const int b = __builtin_ctz(mq[i]);
-          mq[i] &= mq[i] - 1;
-          const uint32_t row = (uint32_t)((k >> 3) - cb), ws = (uint32_t)(k & 7u) * 2u;
-          const unsigned long long u = (unsigned long long)blk[row][ws] | ((unsigned long long)blk[row][ws + 1] << 32);
-          const bool gt = (gtm >> b) & 1u, lt = (ltm >> b) & 1u;
-          const bool v1 = gt ? (u < kP90) : (lt ? (u >= kP90) : (u < kP80));
-          own_lo[i] |= (uint32_t)v1 << b;
-          k++;
-        }
-      }
-      lds_barrier();
-    }
-  }
-  // the own vote joins round2_votes (engine.rs:540-542); decision (613-628)
-  uint32_t dlo[W], dhi[W];
-#pragma unroll
-  for (int i = 0; i < W; i++) {
-    const uint32_t sel = own_lo[i] & t.vq[i];
-    const uint32_t al = dec ? dec[4 * i][tid] : alo[i], ah = dec ? dec[4 * i + 1][tid] : ahi[i];
-    const uint32_t bl = dec ? dec[4 * i + 2][tid] : blo[i], bh = dec ? dec[4 * i + 3][tid] : bhi[i];
-    const uint32_t vm = valid_mask(w0 + i, p.n_words, p.n_slots);
-    dlo[i] = ((al & ~sel) | (bl & sel)) & vm;
-    dhi[i] = ((ah & ~sel) | (bh & sel)) & vm;
-    const uint32_t d1 = dlo[i] & ~dhi[i], dc = ~dhi[i] & vm;
-    acc.cnt0 += __builtin_popcount(dc) | (__builtin_popcount(d1) << 16);
-    acc.cnt1 += __builtin_popcount(t.pd[i]);
-    const uint32_t v1l = d1 & phase_limit_mask(p.slot_base, w0 + i, p.max_phase);
-    if (v1l) {
-      const uint32_t m1 = toff + 32u * i + (31u - __builtin_clz(v1l)) + 1u;
-      acc.max1 = m1 > acc.max1 ? m1 : acc.max1;
-    }
-    const uint32_t und = ~dc & vm;
-    if (und) {
-      const uint32_t mn = toff + 32u * i + __builtin_ctz(und);
-      acc.min = mn < acc.min ? mn : acc.min;
-    }
-  }
-  acc.cnt1 += t.cnt << 16;
-  if (w0 < p.n_words) {  // plane by plane (include/rabia_gpu.h output planes)
-    uint32_t* ob = p.out + p.lout.base(w0);
-    const uint64_t ps = p.lout.pstride;
-    uint32_t v[W];
-#pragma unroll
-    for (int i = 0; i < W; i++) v[i] = t.v1[i] | t.pd[i];
-    store_words_nt<W>(ob, v);
-#pragma unroll
-    for (int i = 0; i < W; i++) v[i] = t.vq[i] | t.pd[i];
-    store_words_nt<W>(ob + ps, v);
-#pragma unroll
-    for (int i = 0; i < W; i++) v[i] = own_lo[i] | t.pd[i];
-    store_words_nt<W>(ob + 2 * ps, v);
-    store_words_nt<W>(ob + 3 * ps, t.pd);
-    store_words_nt<W>(ob + 4 * ps, dlo);
-    store_words_nt<W>(ob + 5 * ps, dhi);
-#pragma unroll
-    for (int i = 0; i < W; i++) v[i] = ~dhi[i] & valid_mask(w0 + i, p.n_words, p.n_slots);
-    store_words_nt<W>(ob + 6 * ps, v);  // set_decision: committed iff not VQuestion
-#pragma unroll
-    for (int i = 0; i < W; i++) v[i] = dlo[i] & ~dhi[i];
-    store_words_nt<W>(ob + 7 * ps, v);  // V1: apply_batch + commit_phase
-  }
-}
-
-// Per-WG statistics record (persist_fold's format) from the threads' SubAcc.
-template <int BLOCK>
-__device__ __forceinline__ void publish_wg_record(const StepParams& p, uint32_t g, const SubAcc& acc, int tid,
-                                                  int lane, int wave) {
-  constexpr int WAVES = BLOCK / 64;
-  __shared__ unsigned long long red[WAVES][4];
-  const unsigned long long c0 = acc.cnt0, c1 = acc.cnt1;
-  const unsigned long long s0 = wave_sum64((c0 & 0xFFFFu) | ((c0 >> 16) << 26));
-  const unsigned long long s1 = wave_sum64((c1 & 0xFFFFu) | ((c1 >> 16) << 26));
-  const unsigned long long mx = wave_max64(acc.max1);
-  const unsigned long long mn = wave_min64(acc.min == 0xFFFFFFFFu ? kOff33 : (unsigned long long)acc.min);
-  if (lane == 0) { red[wave][0] = s0; red[wave][1] = s1; red[wave][2] = mx; red[wave][3] = mn; }
-  lds_barrier();
-  if (tid == 0) {
-    unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = kOff33;
-#pragma unroll 1
-    for (int w = 0; w < WAVES; w++) {
-      t0 += red[w][0]; t1 += red[w][1];
-      t2 = red[w][2] > t2 ? red[w][2] : t2;
-      t3 = red[w][3] < t3 ? red[w][3] : t3;
-    }
-    const unsigned long long tag = pstat_tag(p.seq);
-    unsigned long long* gr = p.stats + (uint64_t)g * kPersistStatGranules;
-    atomic_store_agent(gr + 0, tag | t0);
-    atomic_store_agent(gr + 1, tag | t1);
-    atomic_store_agent(gr + 2, tag | t2);
-    atomic_store_agent(gr + 3, tag | t3);
-  }
-}
-
-template <int N, int W, int BLOCK>
-__global__ __launch_bounds__(BLOCK, 4) void ref_pair_kernel(StepParams p) {
-  constexpr int WAVES = BLOCK / 64;
-  constexpr uint64_t kTW = (uint64_t)BLOCK * W;
-  __shared__ uint32_t s_wave[2][WAVES];
-  __shared__ uint32_t s_excl;
-  __shared__ uint32_t s_cls[2][2 * W][BLOCK];
-  __shared__ uint32_t s_dec[4 * W][BLOCK];     // A's decisions for own V0 / own V1
-  __shared__ uint32_t s_blk[128][17];
-  __shared__ uint32_t s_arrive;                // waves done with B's tally
-  Record* rec = p.rec + (p.seq & 1u);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t g = blockIdx.x, G = gridDim.x;
-  if (tid == 0) s_arrive = 0;  // (ordered before any arrival by the barrier after A's tally)
-  const uint32_t ta = 2 * g, tb = ta + 1;      // p.n_tiles = look-back tiles (2 per WG)
-  if (g == G - 1 && tid == 0) atomic_store_agent(&p.rec[(p.seq + 1) & 1u].error.v, 0ull);
-  const uint32_t tw0 = (uint32_t)tid * W;
-  const uint64_t wa = (uint64_t)ta * kTW + tw0, wb = wa + kTW;
-  const uint32_t toff_a = (uint32_t)(32u * (uint64_t)ta * kTW) + 32u * tw0, toff_b = toff_a + (uint32_t)(32u * kTW);
-  uint32_t r1lo[N][W], r1hi[N][W], r2lo[N][W], r2hi[N][W];
-  uint32_t z0[W], z1[W], z2[W], z3[W];         // (unused register decisions of tile A)
-  PipeTile<W> A, Bt;
-  SubAcc acc;
-
-  // ---- tile A: round 1, aggregate, both-outcome decisions into LDS
-  load_planes_any<N, W>(p, wa, 0, r1lo, r1hi);
-  pipe_tally<N, W, BLOCK>(p, wa, r1lo, r1hi, s_cls[0], tid, lane, A);
-  load_planes_any<N, W>(p, wa, 2 * N, r2lo, r2hi);
-  if (lane == 63) s_wave[0][wave] = A.incl;
-  lds_barrier();
-  const uint32_t tot_a = pipe_tile_total<BLOCK>(s_wave[0], lane);
-  if (wave == 0 && lane == 0 && ta > 0 && !(p.diag & 1u))
-    atomic_store_agent(p.lookback + ta, ((unsigned long long)(p.seq << 1) << 32) | tot_a);
-  pipe_decide<N, W, BLOCK>(p, r2lo, r2hi, A, s_dec, tid);
-  // ---- tile B's round 1; its aggregate goes out as soon as every wave has tallied
-  // (the next workgroup's A looks back through it), without a workgroup barrier:
-  // the last wave to arrive on an LDS counter publishes it
-  load_planes_any<N, W>(p, wb, 0, r1lo, r1hi);
-  pipe_tally<N, W, BLOCK>(p, wb, r1lo, r1hi, s_cls[1], tid, lane, Bt);
-  load_planes_any<N, W>(p, wb, 2 * N, r2lo, r2hi);
-  if (lane == 63) {
-    s_wave[1][wave] = Bt.incl;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (atomicAdd(&s_arrive, 1u) == WAVES - 1 && tb < p.n_tiles && !(p.diag & 1u)) {
-      uint32_t t = 0;
-#pragma unroll
-      for (int w = 0; w < WAVES; w++) t += __hip_atomic_load(&s_wave[1][w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      atomic_store_agent(p.lookback + tb, ((unsigned long long)(p.seq << 1) << 32) | t);
-    }
-  }
-  // ---- A's prefix while B's R2 planes are in flight
-  if (wave == 0) {
-    uint32_t e = 0;
-    if (!(p.diag & 1u)) e = lookback_pipe(p.lookback, ta, p.seq, tot_a, lane, &rec->error.v);
-    if (lane == 0) s_excl = e;
-  }
-  lds_barrier();  // A's prefix, B's wave counts
-  const uint32_t tot_b = pipe_tile_total<BLOCK>(s_wave[1], lane);
-  const uint32_t excl_a = s_excl;
-  if (wave == 0 && lane == 0 && tb < p.n_tiles && !(p.diag & 1u))  // B's inclusive: no look-back of its own
-    atomic_store_agent(p.lookback + tb,
-                       ((unsigned long long)((p.seq << 1) | 1u) << 32) | (excl_a + tot_a + tot_b));
-  const unsigned long long k_a = p.state->rng_next + excl_a;
-  uint32_t off_a = 0, off_b = 0;
-  {
-    const uint32_t sa = lane < WAVES ? s_wave[0][lane] : 0u, sb = lane < WAVES ? s_wave[1][lane] : 0u;
-    const int wv = __builtin_amdgcn_readfirstlane(wave);
-#pragma unroll
-    for (int w = 0; w < WAVES; w++) {
-      off_a += (w < wv) ? __builtin_amdgcn_readlane(sa, w) : 0u;
-      off_b += (w < wv) ? __builtin_amdgcn_readlane(sb, w) : 0u;
-    }
-  }
-  ref_finish_sub<N, W, BLOCK>(p, p.key, wa, toff_a, tid, A, k_a, off_a, tot_a, s_cls[0], s_blk, s_dec, z0, z1, z2,
-                              z3, acc);
-  // ---- tile B: decisions in registers (its R2 planes landed meanwhile), then the same
-  uint32_t blo_a[W], bhi_a[W], blo_b[W], bhi_b[W];
-#pragma unroll
-  for (int i = 0; i < W; i++)
-    r2_decision_ab<N, W>(r2lo, r2hi, i, p.q, p.self_lane, Bt.v1[i], Bt.vq[i], Bt.pd[i], blo_a[i], bhi_a[i],
-                         blo_b[i], bhi_b[i]);
-  ref_finish_sub<N, W, BLOCK>(p, p.key, wb, toff_b, tid, Bt, k_a + tot_a, off_b, tot_b, s_cls[1], s_blk, nullptr,
-                              blo_a, bhi_a, blo_b, bhi_b, acc);
-  if (p.diag & 2u) return;
-  publish_wg_record<BLOCK>(p, g, acc, tid, lane, wave);
-  if (g != G - 1) return;
-  persist_fold<BLOCK>(p, rec, G, tid, lane, wave);
 }
 
 // ============================================================================

@@ -10,9 +10,9 @@ namespace {
 template <int N>
 void launch_n(int block, int words, uint32_t grid, hipStream_t s, const StepParams& p) {
   constexpr int WM = N <= 5 ? 4 : (N <= 10 ? 2 : 1);
-  if (block == 512) hipLaunchKernelGGL((ref_step_kernel<N, WM, 512, true>), dim3(grid), dim3(512), 0, s, p);
-  else if (block == 256) hipLaunchKernelGGL((ref_step_kernel<N, WM, 256, true>), dim3(grid), dim3(256), 0, s, p);
-  else hipLaunchKernelGGL((ref_step_kernel<N, 1, 128, true>), dim3(grid), dim3(128), 0, s, p);
+  if (block == 512) hipLaunchKernelGGL((ref_step_kernel<N, WM, 512, true, 1>), dim3(grid), dim3(512), 0, s, p);
+  else if (block == 256) hipLaunchKernelGGL((ref_step_kernel<N, WM, 256, true, 1>), dim3(grid), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL((ref_step_kernel<N, 1, 128, true, 1>), dim3(grid), dim3(128), 0, s, p);
   (void)words;
 }
 using Launch = void (*)(int, int, uint32_t, hipStream_t, const StepParams&);
