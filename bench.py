@@ -51,6 +51,27 @@ def bytes_per_slot_ref(n: int) -> float:
     return (4 * n + 8) / 8.0
 
 
+def c3_roofline(r, bytes_slot):
+    """C3 is VALU-issue bound (per phase 2n keyed scheduler hashes per slot + the coin),
+    not HBM bound. achieved = VALU wave-instructions per launch (per-slot count from the
+    SQ_INSTS_VALU pass committed in profiles/r02_pmc_c3.json, tools/pmc_c3.sh) / the live
+    kernel time; peak = 256 CUs x 4 SIMDs x 1/2 wave-instruction per cycle at the 2.4 GHz
+    peak engine clock (MI355X_MICROARCH.md). The HBM fraction is kept beside it."""
+    kern_s = r["kern_ms"] / 1000.0
+    hbm = r["S"] * bytes_slot / kern_s / 1e9
+    out = {"bound": "valu", "achieved": None, "peak": 512 * 2.4, "unit": "G VALU wave-instr/s", "frac": None,
+           "traffic": None, "kernel_avg_us": r["kern_ms"] * 1000.0, "hbm_gbs": hbm, "hbm_frac": hbm / HBM_PEAK_GBS}
+    path = os.path.join(ROOT, "profiles", "r02_pmc_c3.json")
+    if os.path.exists(path):
+        pmc = json.load(open(path))
+        achieved = pmc["valu_wave_instr_per_slot"] * r["S"] / kern_s / 1e9
+        out.update(achieved=achieved, frac=achieved / out["peak"],
+                   counter_issue_util=pmc["valu_issue_util"],
+                   note="counter_issue_util = SQ_INSTS_VALU / (512 x GRBM_GUI_ACTIVE/8 cycles): the same "
+                        "ratio at the clock the chip actually ran (DVFS)")
+    return out
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -466,11 +487,7 @@ def main():
                            "replicas": 5, "slots_per_step": r["total"], "slots_per_gpu": r["S"],
                            "mean_phases": r["mean_phases"], "max_phases": r["max_phases"],
                            "parallelism": f"slot-shard x{world}, stats + decided bitmaps all-gathered"},
-                "roofline": {"bound": "valu", "achieved": r["S"] * bytes_slot / (r["kern_ms"] / 1000.0) / 1e9,
-                             "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                             "frac": r["S"] * bytes_slot / (r["kern_ms"] / 1000.0) / 1e9 / HBM_PEAK_GBS,
-                             "traffic": None, "kernel_avg_us": r["kern_ms"] * 1000.0,
-                             "note": "VALU-bound (scheduler hashes + coin), HBM fraction shown for reference"},
+                "roofline": c3_roofline(r, bytes_slot),
                 "cpu_baseline": None, "sweep_1m_us": None,
             }
             print(json.dumps(line), flush=True)
