@@ -75,13 +75,16 @@ struct KvEntry {        // one table slot (the hash lives in its own array for p
 static_assert(sizeof(KvEntry) == 32, "entry layout is part of rg_kv_dump");
 
 struct KvOp {           // decoded command
-  uint64_t key_off;     // offset into the batch's data bytes
-  uint64_t val_off;
+  uint64_t key_off;     // offset into the batch's data bytes (a SET's value follows at
+                        // key_off + key_len + 8, after its u64 length: kv_val_off)
+  uint64_t hash;        // full key hash (kInvalidKey: not applied); one gather gives both
   uint32_t key_len;
   uint32_t val_len;
   uint32_t kind;        // 0 Set 1 Get 2 Delete 3 Exists
   uint32_t status;      // kPending or a final result code
 };
+
+__device__ __forceinline__ uint64_t kv_val_off(const KvOp& op) { return op.key_off + op.key_len + 8; }
 
 struct KvCounters {
   unsigned long long live, version, total_ops, occupied, heap_top;
@@ -188,13 +191,12 @@ __device__ __forceinline__ void bytes_copy(uint8_t* dst, const uint8_t* src, uin
 __global__ __launch_bounds__(kBlock) void kv_decode_kernel(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ off, uint64_t n, const uint8_t* __restrict__ mask,
     uint64_t max_value, uint64_t hmask, uint64_t bmask, uint32_t invalid_bucket, KvOp* __restrict__ ops,
-    uint32_t* __restrict__ sort_key,
-    uint64_t* __restrict__ full_hash, uint32_t* __restrict__ sort_idx, uint8_t* __restrict__ results,
+    uint32_t* __restrict__ sort_key, uint32_t* __restrict__ sort_idx, uint8_t* __restrict__ results,
     unsigned long long* __restrict__ set_part) {
   const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long sets = 0, set_bytes = 0;  // worst-case growth of the batch (the refusal check)
   if (c < n) {
-  KvOp op{0, 0, 0, 0, 0, kPending};
+  KvOp op{0, kInvalidKey, 0, 0, 0, kPending};
   uint64_t key = kInvalidKey;
   if (mask && !mask[c]) {
     op.status = RG_KV_NOT_APPLIED;
@@ -221,7 +223,6 @@ __global__ __launch_bounds__(kBlock) void kv_decode_kernel(
           op.kind = kind;
           op.key_off = b + 12;
           op.key_len = (uint32_t)(klen > 0xFFFFFFFFull ? 0xFFFFFFFFull : klen);
-          op.val_off = b + pos + 8;
           op.val_len = (uint32_t)(vlen > 0xFFFFFFFFull ? 0xFFFFFFFFull : vlen);
           if (klen == 0) op.status = RG_KV_E_KEY_EMPTY;                 // store.rs:464-466
           else if (klen > kMaxKeyLen) op.status = RG_KV_E_KEY_LONG;     // store.rs:467-469
@@ -234,9 +235,9 @@ __global__ __launch_bounds__(kBlock) void kv_decode_kernel(
       }
     }
   }
+  op.hash = key;
   ops[c] = op;
   sort_key[c] = key == kInvalidKey ? invalid_bucket : (uint32_t)hash_bucket(key, bmask);
-  full_hash[c] = key;
   sort_idx[c] = (uint32_t)c;
   if (op.status != kPending) results[c] = (uint8_t)op.status;
   if (op.status == kPending && op.kind == 0) {
@@ -318,7 +319,6 @@ struct BatchView {
   const uint8_t* data;
   const KvOp* ops;
   const uint32_t* skey;   // sorted hash buckets
-  const uint64_t* hfull;  // full key hash per command index
   const uint32_t* sidx;   // command index per sorted position
   uint64_t n;
   uint8_t* results;
@@ -390,7 +390,7 @@ __device__ uint64_t plan_key(const BatchView& b, const KeyOutcome& o, int64_t sl
   uint32_t vlen = 0;
   if (value) {
     const KvOp v = b.ops[o.last_set];
-    vsrc = v.val_off;
+    vsrc = kv_val_off(v);
     vlen = v.val_len;
   }
   // in place when the final value's class fits the slot's current allocation
@@ -487,7 +487,7 @@ __global__ __launch_bounds__(kBlock) void kv_plan_kernel(BatchView b, StoreView 
         if (cont) {
           const uint32_t cp = b.sidx[i - 1];
           const KvOp pp = b.ops[cp];
-          const bool eq = b.hfull[c] == b.hfull[cp] && same_key(b, op, pp);
+          const bool eq = op.hash == pp.hash && same_key(b, op, pp);
           inf |= kInfCont | (eq ? kInfSame : 0u);
         }
       }
@@ -514,7 +514,7 @@ __global__ __launch_bounds__(kBlock) void kv_plan_kernel(BatchView b, StoreView 
     if (single) {  // one key, every command in LDS
       const uint32_t c0 = s_c[l0];
       const KvOp lead = b.ops[c0];
-      const uint64_t hl = b.hfull[c0];
+      const uint64_t hl = lead.hash;
       KvEntry e{};
       const int64_t slot = table_find(st.hashes, st.ent, st.heap, st.mask, hl, b.data + lead.key_off,
                                       lead.key_len, &e);
@@ -540,7 +540,7 @@ __global__ __launch_bounds__(kBlock) void kv_plan_kernel(BatchView b, StoreView 
         keys++;
         const uint32_t c0 = b.sidx[first];
         const KvOp lead = b.ops[c0];
-        const uint64_t hl = b.hfull[c0];
+        const uint64_t hl = lead.hash;
         KvEntry e{};
         const int64_t slot = table_find(st.hashes, st.ent, st.heap, st.mask, hl, b.data + lead.key_off,
                                         lead.key_len, &e);
@@ -549,7 +549,7 @@ __global__ __launch_bounds__(kBlock) void kv_plan_kernel(BatchView b, StoreView 
           if (b.done[q]) continue;
           const uint32_t c = b.sidx[q];
           const KvOp op = b.ops[c];
-          if (q != first && !(b.hfull[c] == hl && same_key(b, op, lead))) continue;
+          if (q != first && !(op.hash == hl && same_key(b, op, lead))) continue;
           b.done[q] = 1;
           b.results[c] = key_step(o, op.kind, c, st.notify);
         }
@@ -730,7 +730,7 @@ __global__ void kv_refuse_kernel(const KvOp* ops, uint64_t n, const KvCounters* 
 }
 
 // ---- 6 ordered replay (StoreFull reachable) -------------------------------------
-__global__ void kv_ordered_kernel(const uint8_t* data, const KvOp* ops, const uint64_t* okey, uint64_t n,
+__global__ void kv_ordered_kernel(const uint8_t* data, const KvOp* ops, uint64_t n,
                                   uint8_t* results, StoreView st) {
   if (threadIdx.x != 0 || st.ctr->mode != 1) return;
   KvCounters* k = st.ctr;
@@ -739,7 +739,7 @@ __global__ void kv_ordered_kernel(const uint8_t* data, const KvOp* ops, const ui
     const KvOp op = ops[c];
     if (op.status != kPending) continue;
     const uint8_t* kp = data + op.key_off;
-    const uint64_t h = okey[c];
+    const uint64_t h = op.hash;
     KvEntry e{};
     int64_t s = table_find(st.hashes, st.ent, st.heap, st.mask, h, kp, op.key_len, &e);
     const bool is_live = s >= 0 && e.version > 0;
@@ -769,7 +769,7 @@ __global__ void kv_ordered_kernel(const uint8_t* data, const KvOp* ops, const ui
         st.ent[s].val_off = top;
         top += val_class(op.val_len);
       }
-      bytes_copy(st.heap + voff, data + op.val_off, op.val_len);
+      bytes_copy(st.heap + voff, data + kv_val_off(op), op.val_len);
       st.ent[s].val_len = op.val_len;
       st.ent[s].version = is_live ? e.version + 1 : 1;
       if (!is_live) live++;
@@ -875,7 +875,7 @@ struct rg_kv {
   // per-batch scratch
   uint64_t cap_cmds = 0;
   KvOp* ops = nullptr;
-  uint64_t *hfull = nullptr, *need = nullptr, *block_base = nullptr;
+  uint64_t *need = nullptr, *block_base = nullptr;
   uint32_t *key_a = nullptr, *key_b = nullptr, *idx_a = nullptr, *idx_b = nullptr;
   KeyRec* recs = nullptr;
   uint8_t* done = nullptr;
@@ -907,12 +907,12 @@ StoreView view(rg_kv* kv) {
 }
 
 void free_scratch(rg_kv* kv) {
-  (void)hipFree(kv->ops); (void)hipFree(kv->key_a); (void)hipFree(kv->key_b); (void)hipFree(kv->hfull);
+  (void)hipFree(kv->ops); (void)hipFree(kv->key_a); (void)hipFree(kv->key_b);
   (void)hipFree(kv->need); (void)hipFree(kv->block_base); (void)hipFree(kv->idx_a);
   (void)hipFree(kv->idx_b); (void)hipFree(kv->done); (void)hipFree(kv->part); (void)hipFree(kv->tmp);
   (void)hipFree(kv->set_part); (void)hipFree(kv->recs);
   kv->set_part = nullptr; kv->recs = nullptr;
-  kv->ops = nullptr; kv->hfull = kv->need = kv->block_base = nullptr;
+  kv->ops = nullptr; kv->need = kv->block_base = nullptr;
   kv->key_a = kv->key_b = kv->idx_a = kv->idx_b = nullptr; kv->done = nullptr; kv->part = nullptr; kv->tmp = nullptr;
   kv->cap_cmds = 0; kv->tmp_bytes = 0;
 }
@@ -928,7 +928,6 @@ int ensure_scratch(rg_kv* kv, uint64_t n) {
   KV_HIP(kv, hipMalloc(&kv->key_a, cap * 4));
   KV_HIP(kv, hipMalloc(&kv->key_b, cap * 4));
   KV_HIP(kv, hipMalloc(&kv->recs, cap * sizeof(KeyRec)));
-  KV_HIP(kv, hipMalloc(&kv->hfull, cap * 8));
   KV_HIP(kv, hipMalloc(&kv->need, cap * 8));
   KV_HIP(kv, hipMalloc(&kv->block_base, (cap / kWalkBlockSpan + 1) * 8));
   KV_HIP(kv, hipMalloc(&kv->idx_a, cap * 4));
@@ -939,7 +938,7 @@ int ensure_scratch(rg_kv* kv, uint64_t n) {
   size_t t1 = 0, t2 = 0;
   KV_HIP(kv, hipcub::DeviceRadixSort::SortPairs(nullptr, t1, kv->key_a, kv->key_b, kv->idx_a, kv->idx_b,
                                                   (int)cap, 0, 32, kv->stream));
-  KV_HIP(kv, hipcub::DeviceScan::ExclusiveSum(nullptr, t2, kv->need, kv->hfull, (int)cap, kv->stream));
+  KV_HIP(kv, hipcub::DeviceScan::ExclusiveSum(nullptr, t2, kv->need, kv->need, (int)cap, kv->stream));
   kv->tmp_bytes = t1 > t2 ? t1 : t2;
   KV_HIP(kv, hipMalloc(&kv->tmp, kv->tmp_bytes));
   kv->cap_cmds = cap;
@@ -1051,14 +1050,14 @@ int rg_kv_apply_async(rg_kv* kv, const uint8_t* data_dev, const uint64_t* cmd_of
   hipLaunchKernelGGL(kv_decode_kernel, dim3(blocks), dim3(kBlock), 0, s, data_dev, cmd_off_dev, n_cmds,
                      apply_mask_dev, kv->cfg.max_value_size,
                      kv->cfg.hash_bits && kv->cfg.hash_bits < 64 ? (1ull << kv->cfg.hash_bits) - 1 : ~0ull,
-                     (uint64_t)invalid_bucket - 1, invalid_bucket, kv->ops, kv->key_a, kv->hfull, kv->idx_a,
+                     (uint64_t)invalid_bucket - 1, invalid_bucket, kv->ops, kv->key_a, kv->idx_a,
                      results_dev, kv->set_part);
   KV_HIP(kv, hipGetLastError());
   size_t tb = kv->tmp_bytes;
   KV_HIP(kv, hipcub::DeviceRadixSort::SortPairs(kv->tmp, tb, kv->key_a, kv->key_b, kv->idx_a, kv->idx_b,
                                                   (int)n_cmds, 0, sbits, s));
   KV_HIP(kv, hipMemsetAsync(kv->done, 0, n_cmds, s));
-  BatchView b{data_dev, kv->ops, kv->key_b, kv->hfull, kv->idx_b, n_cmds, results_dev, kv->done, kv->need,
+  BatchView b{data_dev, kv->ops, kv->key_b, kv->idx_b, n_cmds, results_dev, kv->done, kv->need,
               kv->block_base, kv->recs, invalid_bucket, kv->part};
   const StoreView st = view(kv);
   const uint32_t walk_blocks = (uint32_t)((n_cmds + kWalkBlockSpan - 1) / kWalkBlockSpan);
@@ -1067,7 +1066,7 @@ int rg_kv_apply_async(rg_kv* kv, const uint8_t* data_dev, const uint64_t* cmd_of
   hipLaunchKernelGGL(kv_decide_kernel, dim3(1), dim3(kFoldBlock), 0, s, st, kv->part, walk_blocks, kv->set_part,
                      blocks, kv->block_base);
   hipLaunchKernelGGL(kv_commit_kernel, dim3(walk_blocks), dim3(kBlock), 0, s, b, st);
-  hipLaunchKernelGGL(kv_ordered_kernel, dim3(1), dim3(64), 0, s, data_dev, kv->ops, kv->hfull, n_cmds,
+  hipLaunchKernelGGL(kv_ordered_kernel, dim3(1), dim3(64), 0, s, data_dev, kv->ops, n_cmds,
                      results_dev, st);
   hipLaunchKernelGGL(kv_finish_kernel, dim3(1), dim3(kFoldBlock), 0, s, kv->ctr, kv->part, walk_blocks);
   hipLaunchKernelGGL(kv_refuse_kernel, dim3(blocks), dim3(kBlock), 0, s, kv->ops, n_cmds, kv->ctr, results_dev);
