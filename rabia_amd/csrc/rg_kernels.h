@@ -1782,6 +1782,27 @@ __device__ __forceinline__ uint64_t cluster_key(uint64_t seed, uint32_t phase, u
                           0x9E6C63D0676A9A99ull);
 }
 
+// The receiver's heard set from its (phase, round, replica) key (cluster_key, which
+// does not depend on the slot: the lane-compacted kernel keeps a table of them).
+template <int N>
+__device__ __forceinline__ uint32_t heard_mask_k(uint64_t ckey, uint64_t slot, int r, uint32_t q) {
+  const uint64_t h = mix64(ckey + slot);
+  uint32_t avail = ((1u << N) - 1u) & ~(1u << r);
+  uint32_t mask = 1u << r;
+#pragma unroll
+  for (uint32_t i = 0; i + 1 < (uint32_t)N; i++) {
+    if (i + 1 >= q) break;
+    const uint32_t span = N - 1 - i;
+    const uint32_t k = (uint32_t)((h >> (6 * i)) & 63u) % span;
+    uint32_t a = avail;
+    for (uint32_t t = 0; t < k; t++) a &= a - 1;
+    const uint32_t pick = a & (~a + 1u);
+    mask |= pick;
+    avail &= ~pick;
+  }
+  return mask;
+}
+
 template <int N>
 __device__ __forceinline__ uint32_t heard_mask(uint64_t dseed, uint64_t slot, uint32_t phase, uint32_t round,
                                                int r, uint32_t q) {
@@ -1927,11 +1948,17 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
                                                               unsigned long long* partials, const uint32_t* coin_tab,
                                                               uint32_t coin_phases, uint64_t chunk) {
   constexpr uint32_t kAll = (1u << N) - 1u;
+  constexpr uint32_t kKeyPhases = 32;  // cluster_key table: phases 1..32 (later phases compute theirs)
   __shared__ unsigned long long s_next;
+  __shared__ uint64_t s_ck[kKeyPhases][2][N];
   const uint64_t n_words = (n_slots + 31) / 32;
   const uint64_t c0 = (uint64_t)blockIdx.x * chunk;
   const uint64_t c1 = c0 + chunk < n_slots ? c0 + chunk : n_slots;
   if (threadIdx.x == 0) s_next = c0;
+  for (uint32_t e = threadIdx.x; e < kKeyPhases * 2 * N; e += blockDim.x) {
+    const uint32_t ph = e / (2 * N), rd = (e / N) % 2, rr = e % N;
+    s_ck[ph][rd][rr] = cluster_key(dseed, ph + 1, rd + 1, (int)rr);
+  }
   __syncthreads();
   const int lane = threadIdx.x & 63;
   unsigned long long acc[kClusterStats] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1965,9 +1992,11 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
     if (!active) continue;
     // ---- one phase of every replica of slot s (same rules as wmvc_cluster_kernel)
     uint32_t v1 = 0, vq = 0;
+    const bool tab = p <= kKeyPhases;
 #pragma unroll
     for (int r = 0; r < N; r++) {
-      const uint32_t h = heard_mask<N>(dseed, id, p, 1, r, q);
+      const uint64_t ck = tab ? s_ck[p - 1][0][r] : cluster_key(dseed, p, 1, r);
+      const uint32_t h = heard_mask_k<N>(ck, id, r, q);
       const uint32_t c1r = __builtin_popcount(h & st), c0r = __builtin_popcount(h & ~st);
       if (c1r >= q) v1 |= 1u << r;
       else if (c0r < q) vq |= 1u << r;
@@ -1976,7 +2005,8 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
     int coin = -1;
 #pragma unroll
     for (int r = 0; r < N; r++) {
-      const uint32_t h = heard_mask<N>(dseed, id, p, 2, r, q);
+      const uint64_t ck = tab ? s_ck[p - 1][1][r] : cluster_key(dseed, p, 2, r);
+      const uint32_t h = heard_mask_k<N>(ck, id, r, q);
       const uint32_t c1r = __builtin_popcount(h & v1), cq = __builtin_popcount(h & vq);
       const uint32_t c0r = q - c1r - cq;
       int nv = c0r >= fp1 ? 0 : (c1r >= fp1 ? 1 : -1);
