@@ -325,8 +325,20 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, bitmaps):
             comp.wait_event(e_done[t - a.sets])
         if evs is not None:
             evs[0].record(comp)
-        ev.phase_step_shard_async(votes.data_ptr(), out.data_ptr(), S, stride, base + start, rec.data_ptr(), cap,
-                                  rows[t].data_ptr(), stream=comp.cuda_stream)
+        if a.backend == "gloo" and world > 1:
+            # Rehearsal: the ranks share one GPU, and two look-back launches running at
+            # once on one GPU can wait on each other across kernels (each holds CUs its
+            # partner's predecessors need: the bounded spin then flags a fault). Real
+            # runs have one GPU per rank. So the ranks' step kernels take turns here.
+            for r in range(world):
+                if r == rank:
+                    ev.phase_step_shard_async(votes.data_ptr(), out.data_ptr(), S, stride, base + start,
+                                              rec.data_ptr(), cap, rows[t].data_ptr(), stream=comp.cuda_stream)
+                    comp.synchronize()
+                dist.barrier()
+        else:
+            ev.phase_step_shard_async(votes.data_ptr(), out.data_ptr(), S, stride, base + start, rec.data_ptr(), cap,
+                                      rows[t].data_ptr(), stream=comp.cuda_stream)
         if evs is not None:
             evs[1].record(comp)
         e_main[t].record(comp)
@@ -362,8 +374,12 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, bitmaps):
     total_ms = t_begin.elapsed_time(t_end)
     kern_ms = float(np.mean([b.elapsed_time(e) for b, e in evs]))
     res = result.cpu().numpy().view(np.uint64)
-    if int(res[:, 9].max()) != 0 or int(fixed.cpu().numpy().view(np.uint64)[:, 9].max()) != 0:
-        raise RuntimeError("device-side fault flagged in a step result (look-back timeout or record overflow)")
+    fx = fixed.cpu().numpy().view(np.uint64)
+    if int(res[:, 9].max()) != 0 or int(fx[:, 9].max()) != 0:
+        raise RuntimeError("device-side fault flagged in a step result (1/2 look-back/fold timeout, 4 stale record "
+                           f"ring, 8 draw-record overflow): result flags {sorted(set(res[:, 9].tolist()))}, shard "
+                           f"flags {sorted(set(fx[:, 9].tolist()))}, rows flags "
+                           f"{sorted(set(rows.cpu().numpy().view(np.uint64)[:, 9].tolist()))}")
     timed = res[a.warmup:]
     assert (timed[:, 0] == window_slots).all(), "a timed window did not complete"
     decided = int(timed[:, 1].sum())  # global (every shard), identical on every rank

@@ -137,7 +137,10 @@ int rg_get_state(rg_ctx* ctx, rg_engine_state* st);
 /* Phase step over one slot window [slot_base, slot_base + n_slots).
  * `phase` is the WMVC phase number (>= 1; ignored in REF). `max_phase` is
  * EngineState.current_phase for commit_phase's ordering check (state.rs:70-75);
- * 0 disables it. Calls on one context must be stream-ordered.
+ * 0 disables it. Calls on one context must be stream-ordered, and so must REF
+ * steps of different contexts on one device: two look-back launches running at
+ * once on one GPU can hold the CUs each other's earlier tiles need (the bounded
+ * spin then reports RG_ESTATE).
  *  _async: device pointers, enqueued on `stream`; result_dev may be NULL
  *          (then fetch it with rg_last_result).
  *  plain : host pointers; copies in, runs, copies out, synchronises. */
