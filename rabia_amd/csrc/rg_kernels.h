@@ -352,6 +352,8 @@ __device__ __forceinline__ uint32_t lookback_exclusive_wide(unsigned long long* 
   return excl;
 }
 
+constexpr int kLBWide = 8;  // granules per lane in a first-generation tile's poll
+
 // ---- per-tile statistics -> granules; the last tile reduces them ------------
 // Per tile, two 8-B granules written with agent-scope stores by one lane:
 //   g0 = tag:13 | n_decided:17 | n_v1:17 | n_pending_r1:17
@@ -831,8 +833,21 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_step_kernel(StepParams p) {
                                      : lookback_exclusive_wide<4>(p.lookback, tile, p.seq, tile_total, lane,
                                                                   &rec->error.v, RG_LB_WIDE);
 #else
-    const uint32_t e = (p.diag & 1u) ? 0u
-                                     : lookback_exclusive(p.lookback, tile, p.seq, tile_total, lane, &rec->error.v);
+    // The launch's first tiles all start together, and tile t needs the aggregates of
+    // all t predecessors: with 64 granules per poll the inclusive frontier crosses the
+    // first generation in t/64 round trips while the later tiles hold their CUs.
+    // In launches of at most 1024 tiles (a single 2^20 window: 14.1 -> 13.2 us) those
+    // tiles poll kLBWide x 64 predecessors at once; large launches and steady-state
+    // tiles keep the one-granule-per-lane poll (wider polls measured slower there).
+    uint32_t e = 0;
+    if (!(p.diag & 1u)) {
+      if (DEF != 0 && tile < 64u * kLBWide && p.n_tiles <= 1024u && !(p.diag & 16u)) {
+        const int kf = (int)((tile + 63u) / 64u);
+        e = lookback_exclusive_wide<kLBWide>(p.lookback, tile, p.seq, tile_total, lane, &rec->error.v, kf, kLBWide, 1);
+      } else {
+        e = lookback_exclusive(p.lookback, tile, p.seq, tile_total, lane, &rec->error.v);
+      }
+    }
 #endif
     if (lane == 0) s_excl = e;
   }

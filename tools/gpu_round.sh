@@ -17,5 +17,5 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_$TAG -o bench --
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch_$TAG -o pmc --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 10 --warmup 2 > $OUT/pmc_fetch_$TAG.log 2>&1 || { echo "pmc fetch failed"; tail -30 $OUT/pmc_fetch_$TAG.log; exit 1; }
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write_$TAG -o pmc --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 10 --warmup 2 > $OUT/pmc_write_$TAG.log 2>&1 || { echo "pmc write failed"; tail -30 $OUT/pmc_write_$TAG.log; exit 1; }
 cd $R
-python3 tools/pmc_traffic.py $OUT/pmc_fetch_$TAG $OUT/pmc_write_$TAG 5 268435456 $OUT/pmc_c2.json || echo "pmc parse failed"
+python3 tools/pmc_traffic.py $OUT/pmc_fetch_$TAG $OUT/pmc_write_$TAG 5 1073741824 $OUT/pmc_c2.json || echo "pmc parse failed"
 cat $OUT/prof_$TAG/bench_kernel_stats.csv | head -5
