@@ -468,6 +468,10 @@ __global__ __launch_bounds__(kBlock) void kv_plan_kernel(BatchView b, StoreView 
   unsigned long long acc[kPCount] = {0, 0, 0, 0, 0, 0, 0};
   const uint64_t bbase = (uint64_t)blockIdx.x * kWalkBlockSpan;
   const uint32_t wl = (uint32_t)wave * kWalkSpan;
+  if (b.skey[bbase] == b.invalid_bucket) {  // the sorted tail of commands not applied: nothing to plan
+    if (threadIdx.x < kPCount) b.part[(uint64_t)blockIdx.x * kPCount + threadIdx.x] = 0;
+    return;
+  }
   // phase A: per position, command index, kind, continues / same key as previous
   uint32_t nh = 0;
 #pragma unroll
@@ -570,6 +574,7 @@ __global__ __launch_bounds__(kBlock) void kv_commit_kernel(BatchView b, StoreVie
   __shared__ uint16_t s_heads[kBlock / 64][kWalkSpan];
   __shared__ unsigned long long s_wsum[kBlock / 64];
   if (st.ctr->mode != 0) return;  // uniform over the grid
+  if (b.skey[(uint64_t)blockIdx.x * kWalkBlockSpan] == b.invalid_bucket) return;  // no heads in the tail
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t wbase = (uint64_t)blockIdx.x * kWalkBlockSpan + (uint64_t)wave * kWalkSpan;
   const uint32_t nh = collect_heads(b, wbase, lane, true, s_heads[wave]);
@@ -593,17 +598,20 @@ __global__ __launch_bounds__(kBlock) void kv_commit_kernel(BatchView b, StoreVie
     for (uint64_t k = i; k < b.n && k < i + kMaxRunKeys; k++) {
       const KeyRec r = b.recs[k];
       int64_t s = r.slot;
-      if (r.flags & kRecNew) {
+      if (r.flags & kRecNew) {  // a new key always ends live with a value: the whole entry at once
         s = table_claim(st.hashes, st.mask, r.hash);
-        if (s < 0 || heap_pos + r.key_len > st.heap_cap) {
+        const uint64_t koff = heap_pos, voff = heap_pos + r.key_len;
+        heap_pos += r.key_len + val_class(r.val_len);
+        if (s < 0 || heap_pos > st.heap_cap) {
           atomicOr(&st.ctr->flags, s < 0 ? kFaultTable : kFaultHeap);
-          s = -1;
         } else {
-          bytes_copy(st.heap + heap_pos, b.data + r.key_src, r.key_len);
-          st.ent[s].key_off = heap_pos;
-          st.ent[s].key_len = r.key_len;
+          bytes_copy(st.heap + koff, b.data + r.key_src, r.key_len);
+          bytes_copy(st.heap + voff, b.data + r.val_src, r.val_len);
+          const KvEntry e{koff, voff, r.ver1, r.key_len, r.val_len};
+          st.ent[s] = e;
         }
-        heap_pos += r.key_len;
+        if (r.flags & kRecLast) break;
+        continue;
       }
       if (s >= 0 && (r.flags & kRecValue)) {
         uint64_t dst = r.val_dst;
