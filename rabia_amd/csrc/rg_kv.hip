@@ -187,6 +187,62 @@ __device__ __forceinline__ void bytes_copy(uint8_t* dst, const uint8_t* src, uin
   for (; i < n; i++) dst[i] = src[i];
 }
 
+// ---- decode fast path ----------------------------------------------------------
+// A byte range [0, u) at q (u <= 8 * W, u > 0, q - 8 readable when u < 8) held as W
+// words: word j starts at s_j = min(8j, u - 8), so every load stays inside the
+// command and all of them issue at once (one round trip instead of one per loop
+// iteration of utf8_valid / key_hash). Bytes of word j at offsets o hold range
+// bytes s_j + o.
+template <int W>
+struct Span {
+  uint64_t w[W];
+  int32_t s[W];
+  int nw;
+};
+template <int W>
+__device__ __forceinline__ void span_load(Span<W>& sp, const uint8_t* q, uint32_t u) {
+  sp.nw = (int)((u + 7) >> 3);
+#pragma unroll
+  for (int j = 0; j < W; j++) {
+    const int32_t sj = min((int32_t)(8 * j), (int32_t)u - 8);
+    sp.s[j] = sj;
+    sp.w[j] = j < sp.nw ? ld_u64(q + sj) : 0;
+  }
+}
+// mask of the bytes of word j that hold range bytes [lo, hi)
+__device__ __forceinline__ uint64_t byte_mask(int32_t sj, int32_t lo, int32_t hi) {
+  const int32_t a = max(lo - sj, 0), b = min(hi - sj, 8);
+  if (b <= a) return 0;
+  const uint64_t top = b == 8 ? ~0ull : ((1ull << (8 * b)) - 1ull);
+  return top & ~((1ull << (8 * a)) - 1ull);
+}
+// all range bytes [0, n) are ASCII (n <= u)
+template <int W>
+__device__ __forceinline__ bool span_ascii(const Span<W>& sp, uint32_t n) {
+  uint64_t acc = 0;
+#pragma unroll
+  for (int j = 0; j < W; j++)
+    if (j < sp.nw) acc |= sp.w[j] & byte_mask(sp.s[j], 0, (int32_t)n);
+  return (acc & 0x8080808080808080ull) == 0;
+}
+// key_hash over range bytes [0, n) (n == u), byte order as key_hash's
+template <int W>
+__device__ __forceinline__ uint64_t span_key_hash(const Span<W>& sp, uint32_t n, uint64_t hmask) {
+  uint64_t h = 0xcbf29ce484222325ull;
+#pragma unroll
+  for (int b = 0; b < 8 * W; b++) {
+    if (b < (int)n) {
+      const int j = b >> 3;
+      h = (h ^ ((sp.w[j] >> (8 * (b - sp.s[j]))) & 0xFFu)) * 0x100000001b3ull;
+    }
+  }
+  h = fmix64(h ^ n) & hmask;
+  if (h == kEmpty) h = 1;
+  if (h == kInvalidKey) h = kInvalidKey - 1;
+  return h;
+}
+constexpr uint32_t kFastKey = 16, kFastVal = 64;  // decode fast path: key <= 16 B, value region <= 64 B
+
 // ---- 1 decode ----------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void kv_decode_kernel(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ off, uint64_t n, const uint8_t* __restrict__ mask,
@@ -205,7 +261,42 @@ __global__ __launch_bounds__(kBlock) void kv_decode_kernel(
     const uint64_t len = e > b ? e - b : 0;
     const uint8_t* p = data + b;
     op.status = RG_KV_E_DECODE;
-    if (len >= 12) {
+    const uint32_t kind0 = len >= 12 ? ld_u32(p) : 0xFFFFFFFFu;
+    const uint64_t klen0 = len >= 12 ? ld_u64(p + 4) : ~0ull;
+    // fast path (short ASCII key, SET value region <= 64 B): the key words, the value
+    // length and the value region's words are loaded together
+    const uint64_t urest = kind0 == 0 && klen0 <= len - 12 && len - 12 - klen0 >= 8 ? len - 20 - klen0 : ~0ull;
+    const bool fast = kind0 <= 3 && klen0 >= 1 && klen0 <= kFastKey && klen0 <= len - 12 &&
+                      (kind0 != 0 || urest <= kFastVal);
+    bool done = false;
+    if (fast) {
+      const uint32_t kl = (uint32_t)klen0;
+      Span<2> ks;
+      span_load(ks, p + 12, kl);
+      uint64_t vlen = 0;
+      bool vok = true;
+      if (kind0 == 0) {
+        const uint32_t u = (uint32_t)urest;
+        vlen = ld_u64(p + 12 + kl);
+        Span<8> vs;
+        if (u) span_load(vs, p + 20 + kl, u);
+        if (vlen > u) vok = false;               // decode error (slow path reports it)
+        else if (vlen && !span_ascii(vs, (uint32_t)vlen)) vok = false;
+      }
+      if (vok && span_ascii(ks, kl)) {
+        op.kind = kind0;
+        op.key_off = b + 12;
+        op.key_len = kl;
+        op.val_len = (uint32_t)vlen;
+        if (kind0 == 0 && vlen > max_value) op.status = RG_KV_E_VALUE_LARGE;  // store.rs:473-477
+        else {
+          op.status = kPending;
+          key = span_key_hash(ks, kl, hmask);
+        }
+        done = true;
+      }
+    }
+    if (!done && len >= 12) {
       const uint32_t kind = ld_u32(p);
       const uint64_t klen = ld_u64(p + 4);
       if (kind <= 3 && klen <= len - 12) {
@@ -377,8 +468,10 @@ __device__ __forceinline__ uint8_t key_step(KeyOutcome& o, uint32_t kind, uint32
 
 // Folds a replayed key into the block partials and its commit record; returns the
 // heap bytes the commit will take for it (new key bytes + a new value allocation).
-__device__ uint64_t plan_key(const BatchView& b, const KeyOutcome& o, int64_t slot, const KvEntry& e,
-                             const KvOp& lead, uint64_t hl, unsigned long long (&acc)[kPCount], KeyRec& r) {
+// (vsrc, vlen: the final value's bytes, from the SET the replay recorded in last_set.)
+__device__ uint64_t plan_key(const KeyOutcome& o, int64_t slot, const KvEntry& e, uint64_t key_off,
+                             uint32_t key_len, uint64_t vsrc, uint32_t vlen, uint64_t hl,
+                             unsigned long long (&acc)[kPCount], KeyRec& r) {
   acc[kPOps] += o.n_ops;
   acc[kPVersion] += o.n_version;
   acc[kPLiveDelta] += (unsigned long long)((int64_t)o.live1 - (int64_t)o.live0);
@@ -386,27 +479,24 @@ __device__ uint64_t plan_key(const BatchView& b, const KeyOutcome& o, int64_t sl
   const bool new_slot = slot < 0 && o.live1;
   acc[kPNewSlots] += new_slot;
   const bool value = o.live1 && o.wrote_value;
-  uint64_t vsrc = 0;
-  uint32_t vlen = 0;
-  if (value) {
-    const KvOp v = b.ops[o.last_set];
-    vsrc = kv_val_off(v);
-    vlen = v.val_len;
+  if (!value) {
+    vsrc = 0;
+    vlen = 0;
   }
   // in place when the final value's class fits the slot's current allocation
   const bool in_place = value && slot >= 0 && val_class(vlen) <= val_class(e.val_len);
   r.slot = slot;
   r.ver1 = o.live1 ? o.ver1 : 0;
   r.hash = hl;
-  r.key_src = lead.key_off;
+  r.key_src = key_off;
   r.val_src = vsrc;
   r.val_dst = e.val_off;
-  r.key_len = lead.key_len;
+  r.key_len = key_len;
   r.val_len = vlen;
   r.flags = (new_slot ? kRecNew : 0u) | (value ? kRecValue : 0u) | (in_place ? kRecInPlace : 0u) |
             ((slot >= 0 || new_slot) && (o.any_set || o.live0 != o.live1) ? kRecVersion : 0u);
   r.pad = 0;
-  return (new_slot ? lead.key_len : 0) + (value && !in_place ? val_class(vlen) : 0);
+  return (new_slot ? key_len : 0) + (value && !in_place ? val_class(vlen) : 0);
 }
 
 __device__ __forceinline__ void block_add_partials(unsigned long long (&v)[kPCount],
@@ -460,10 +550,23 @@ __device__ __forceinline__ uint32_t collect_heads(const BatchView& b, uint64_t w
 
 enum : uint8_t { kInfCont = 4, kInfSame = 8 };  // bits 0-1: kind
 
+// LDS written by this wave's lanes, then read by other lanes of the same wave.
+__device__ __forceinline__ void lds_wave_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
 __global__ __launch_bounds__(kBlock) void kv_plan_kernel(BatchView b, StoreView st) {
   __shared__ uint32_t s_c[kWalkBlockSpan];
   __shared__ uint8_t s_inf[kWalkBlockSpan];
   __shared__ uint16_t s_heads[kBlock / 64][kWalkSpan];
+  // each position's decoded command fields, gathered once (phase A) and read by the
+  // same-key compare of the next position, the run head's lookup and the final
+  // value's source: no second gather of a KvOp on the single-key path
+  __shared__ uint64_t s_hash[kWalkBlockSpan];
+  __shared__ uint64_t s_koff[kWalkBlockSpan];
+  __shared__ uint32_t s_klen[kWalkBlockSpan];
+  __shared__ uint32_t s_vlen[kWalkBlockSpan];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   unsigned long long acc[kPCount] = {0, 0, 0, 0, 0, 0, 0};
   const uint64_t bbase = (uint64_t)blockIdx.x * kWalkBlockSpan;
@@ -472,32 +575,56 @@ __global__ __launch_bounds__(kBlock) void kv_plan_kernel(BatchView b, StoreView 
     if (threadIdx.x < kPCount) b.part[(uint64_t)blockIdx.x * kPCount + threadIdx.x] = 0;
     return;
   }
-  // phase A: per position, command index, kind, continues / same key as previous
+  // phase A1: per position, command index, kind, continues the previous bucket, and
+  // the command's fields into LDS (all gathers of the wave in flight at once)
+#pragma unroll
+  for (int k = 0; k < kWalkPerLane; k++) {
+    const uint32_t l = wl + 64 * k + lane;
+    const uint64_t i = bbase + l;
+    uint32_t c = 0, inf = 0;
+    if (i < b.n) {
+      const uint32_t h = b.skey[i];
+      if (h != b.invalid_bucket) {
+        c = b.sidx[i];
+        const KvOp op = b.ops[c];
+        inf = (op.kind & 3u) | (i > 0 && b.skey[i - 1] == h ? kInfCont : 0u);
+        s_hash[l] = op.hash;
+        s_koff[l] = op.key_off;
+        s_klen[l] = op.key_len;
+        s_vlen[l] = op.val_len;
+      }
+    }
+    s_c[l] = c;
+    s_inf[l] = (uint8_t)inf;
+  }
+  lds_wave_sync();
+  // phase A2: same key as the previous position (key bytes decide); run heads
+  // compacted per wave. The previous position is in this wave's LDS except for the
+  // wave's first one.
   uint32_t nh = 0;
 #pragma unroll
   for (int k = 0; k < kWalkPerLane; k++) {
     const uint32_t l = wl + 64 * k + lane;
     const uint64_t i = bbase + l;
-    bool head = false;
-    uint32_t c = 0, inf = 0;
-    if (i < b.n) {
-      const uint32_t h = b.skey[i];
-      if (h != b.invalid_bucket) {
-        const bool cont = i > 0 && b.skey[i - 1] == h;
-        head = !cont;
-        c = b.sidx[i];
-        const KvOp op = b.ops[c];
-        inf = op.kind & 3u;
-        if (cont) {
-          const uint32_t cp = b.sidx[i - 1];
-          const KvOp pp = b.ops[cp];
-          const bool eq = op.hash == pp.hash && same_key(b, op, pp);
-          inf |= kInfCont | (eq ? kInfSame : 0u);
-        }
+    uint32_t inf = s_inf[l];
+    const bool head = i < b.n && b.skey[i] != b.invalid_bucket && !(inf & kInfCont);
+    if (inf & kInfCont) {
+      uint64_t ph, pko;
+      uint32_t pkl;
+      if (l > wl) {
+        ph = s_hash[l - 1];
+        pko = s_koff[l - 1];
+        pkl = s_klen[l - 1];
+      } else {
+        const KvOp pp = b.ops[b.sidx[i - 1]];
+        ph = pp.hash;
+        pko = pp.key_off;
+        pkl = pp.key_len;
       }
+      const uint32_t kl = s_klen[l];
+      const bool eq = s_hash[l] == ph && kl == pkl && bytes_eq(b.data + s_koff[l], b.data + pko, kl);
+      if (eq) s_inf[l] = (uint8_t)(inf | kInfSame);
     }
-    s_c[l] = c;
-    s_inf[l] = (uint8_t)inf;
     const unsigned long long m = __ballot(head);
     if (head) s_heads[wave][nh + __builtin_popcountll(m & ((1ull << lane) - 1ull))] = (uint16_t)(64 * k + lane);
     nh += (uint32_t)__builtin_popcountll(m);
@@ -516,19 +643,16 @@ __global__ __launch_bounds__(kBlock) void kv_plan_kernel(BatchView b, StoreView 
     if (l == (uint32_t)kWalkBlockSpan && bbase + l < b.n && b.skey[bbase + l] == b.skey[i]) single = false;
     uint64_t need = 0;
     if (single) {  // one key, every command in LDS
-      const uint32_t c0 = s_c[l0];
-      const KvOp lead = b.ops[c0];
-      const uint64_t hl = lead.hash;
+      const uint64_t hl = s_hash[l0], koff = s_koff[l0];
+      const uint32_t klen = s_klen[l0];
       KvEntry e{};
-      const int64_t slot = table_find(st.hashes, st.ent, st.heap, st.mask, hl, b.data + lead.key_off,
-                                      lead.key_len, &e);
+      const int64_t slot = table_find(st.hashes, st.ent, st.heap, st.mask, hl, b.data + koff, klen, &e);
       KeyOutcome o = key_start(slot, e);
-      for (uint32_t q = l0; q < l; q++) {
-        const uint32_t c = s_c[q];
-        b.results[c] = key_step(o, s_inf[q] & 3u, c, st.notify);
-      }
+      for (uint32_t q = l0; q < l; q++)  // last_set records the LDS position here
+        b.results[s_c[q]] = key_step(o, s_inf[q] & 3u, q, st.notify);
+      const uint32_t ls = o.last_set;
       KeyRec r;
-      need = plan_key(b, o, slot, e, lead, hl, acc, r);
+      need = plan_key(o, slot, e, koff, klen, s_koff[ls] + s_klen[ls] + 8, s_vlen[ls], hl, acc, r);
       r.flags |= kRecLast;
       b.recs[i] = r;
     } else {       // general: split the bucket run into keys by their bytes
@@ -557,7 +681,14 @@ __global__ __launch_bounds__(kBlock) void kv_plan_kernel(BatchView b, StoreView 
           b.done[q] = 1;
           b.results[c] = key_step(o, op.kind, c, st.notify);
         }
-        need += plan_key(b, o, slot, e, lead, hl, acc, r);
+        uint64_t vsrc = 0;
+        uint32_t vlen = 0;
+        if (o.wrote_value) {
+          const KvOp v = b.ops[o.last_set];
+          vsrc = kv_val_off(v);
+          vlen = v.val_len;
+        }
+        need += plan_key(o, slot, e, lead.key_off, lead.key_len, vsrc, vlen, hl, acc, r);
       }
       if (keys) {
         r.flags |= kRecLast;

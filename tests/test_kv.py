@@ -456,3 +456,53 @@ def test_gpu_narrow_buckets_mix_hashes(bucket_bits):
         _check_state(dev, ref)
         # 3 / 6 bits: ~60 / ~8 keys per run -> ordered replay; 10 bits: ~1 key per run
         assert (dev.stats()["ordered_batches"] > 0) == (bucket_bits <= 6)
+
+
+def decode_edge_blobs(rng: random.Random):
+    """Commands at the edges of the decode fast path (key <= 16 B, SET value region
+    <= 64 B, ASCII, all loads in one round trip) and just outside it: every key
+    length 1..17, every value length 0..66, trailing bytes after a value (non-ASCII
+    and invalid UTF-8 ones included: not part of the value), value lengths that
+    claim more bytes than the command holds, non-ASCII valid UTF-8 and invalid
+    UTF-8 at the first and last byte of short keys and values."""
+    out = []
+    for kl in range(1, 18):
+        key = (f"k{kl:02d}" + "abcdefghijklmnop")[:kl].encode()
+        out.append(R.encode_op(R.SET, key, b"v" * (kl % 5)))
+        out.append(R.encode_op(R.GET, key))
+        out.append(R.encode_op(R.EXISTS, key) + b"\xff\xfe")
+    for vl in range(0, 67):
+        key = f"val{vl % 7}".encode()
+        out.append(R.encode_op(R.SET, key, bytes(rng.choice(b"0123456789abcdef") for _ in range(vl))))
+    for tail in (b"x", b"\xff", b"\xc3", b"trailing bytes!!", b"\x80" * 30):
+        out.append(R.encode_op(R.SET, b"tail", b"abc") + tail)
+        out.append(R.encode_op(R.SET, b"t" * 16, b"q" * 40) + tail)
+    good = R.encode_op(R.SET, b"claim", b"12345678")
+    for extra in (1, 8, 100):   # value length field larger than the bytes that follow
+        out.append(good[:12 + 5] + (8 + extra).to_bytes(8, "little") + good[12 + 5 + 8:])
+    out.append(good[:12 + 5] + (2).to_bytes(8, "little") + good[12 + 5 + 8:])  # shorter: rest trails
+    for bad in (b"\xff", b"\xc3\x28", b"\xed\xa0\x80"):
+        out.append(R.encode_op(R.SET, bad + b"key", b"v"))
+        out.append(R.encode_op(R.SET, b"key" + bad, b"v"))
+        out.append(R.encode_op(R.SET, b"key", bad + b"value"))
+        out.append(R.encode_op(R.SET, b"key", b"value" + bad))
+    for s in ("é", "ключ", "€uro", "a€", "日本語のキー"):
+        out.append(R.encode_op(R.SET, s.encode(), s.encode() * 3))
+        out.append(R.encode_op(R.GET, s.encode()))
+    out.append(R.encode_op(R.GET, b""))
+    out.append(b"\x00\x00\x00\x00" + (3).to_bytes(8, "little") + b"ab")  # key cut short
+    rng.shuffle(out)
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [0, 1])
+def test_gpu_decode_fast_path_edges(seed):
+    rng = random.Random(seed)
+    with _store(max_value_size=60) as dev:
+        ref = R.KVStoreRef(max_value_size=60)
+        for _ in range(2):
+            blobs = decode_edge_blobs(rng)
+            got = [int(x) for x in dev.apply_commands(blobs)]
+            assert got == ref.apply_commands(blobs)
+        _check_state(dev, ref)

@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--slots-log2", type=int, default=22)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--key-space-log2", type=int, default=20)
+    ap.add_argument("--bucket-bits", type=int, default=0, help="sort bucket width (0: the library's choice)")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the C restatement baseline")
     a = ap.parse_args()
     n, S = 7, 1 << a.slots_log2
     stream = torch.cuda.Stream()
@@ -59,7 +61,7 @@ def main():
     cmd_off2 = torch.empty(S + 1, dtype=torch.int64, device="cuda")
     res2 = torch.empty(S, dtype=torch.uint8, device="cuda")
     for rep in range(a.reps + 1):
-        with DeviceKVStore(KVStoreConfig(max_keys=4 * ks)) as kv:
+        with DeviceKVStore(KVStoreConfig(max_keys=4 * ks, bucket_bits=a.bucket_bits)) as kv:
             kv.trace_async(rep, S, ks, cmd_data.data_ptr(), cmd_data.numel(), cmd_off.data_ptr(), sp)
             stream.synchronize()
             evs = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
@@ -95,6 +97,10 @@ def main():
     # CPU baseline: the sequential C restatement (oracle/kvstore_ref.c, one thread; the
     # KVStore is one HashMap behind one lock, store.rs) applying the same commands with
     # the same mask, median of 3; its results must equal the device's
+    if a.no_cpu:
+        print(json.dumps({"bucket_bits": a.bucket_bits, "stage_us_median": med,
+                          "apply_warm_us_median": float(np.median(warm)), "store": st}))
+        return
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
     data = cmd_data.cpu().numpy()
