@@ -1000,6 +1000,26 @@ __global__ void kv_trace_fill_kernel(uint64_t seed, uint64_t n, uint64_t key_spa
   }
 }
 
+// Stable (bucket, index) sort. RG_KV_SORT_BITS (experiment builds): rocprim onesweep
+// with that many bits per pass and RG_KV_SORT_BLOCK x RG_KV_SORT_IPT tiles instead of
+// hipCUB's tuned default (8 bits per pass).
+#ifndef RG_KV_SORT_BITS
+#define RG_KV_SORT_BITS 0
+#endif
+hipError_t kv_sort(void* tmp, size_t& tb, uint32_t* ka, uint32_t* kb, uint32_t* ia, uint32_t* ib, int n,
+                   int bits, hipStream_t s) {
+#if RG_KV_SORT_BITS
+  using cfg = rocprim::radix_sort_config<
+      rocprim::default_config, rocprim::default_config,
+      rocprim::radix_sort_onesweep_config<rocprim::kernel_config<RG_KV_SORT_BLOCK, RG_KV_SORT_IPT>,
+                                          rocprim::kernel_config<RG_KV_SORT_BLOCK, RG_KV_SORT_IPT>, RG_KV_SORT_BITS,
+                                          rocprim::block_radix_rank_algorithm::RG_KV_SORT_RANK>>;
+  return rocprim::radix_sort_pairs<cfg>(tmp, tb, ka, kb, ia, ib, n, 0u, (unsigned)bits, s);
+#else
+  return hipcub::DeviceRadixSort::SortPairs(tmp, tb, ka, kb, ia, ib, n, 0, bits, s);
+#endif
+}
+
 }  // namespace
 
 // ============================================================================
@@ -1075,8 +1095,7 @@ int ensure_scratch(rg_kv* kv, uint64_t n) {
   KV_HIP(kv, hipMalloc(&kv->part, blocks * kPCount * 8));
   KV_HIP(kv, hipMalloc(&kv->set_part, blocks * 2 * 8));
   size_t t1 = 0, t2 = 0;
-  KV_HIP(kv, hipcub::DeviceRadixSort::SortPairs(nullptr, t1, kv->key_a, kv->key_b, kv->idx_a, kv->idx_b,
-                                                  (int)cap, 0, 32, kv->stream));
+  KV_HIP(kv, kv_sort(nullptr, t1, kv->key_a, kv->key_b, kv->idx_a, kv->idx_b, (int)cap, 32, kv->stream));
   KV_HIP(kv, hipcub::DeviceScan::ExclusiveSum(nullptr, t2, kv->need, kv->need, (int)cap, kv->stream));
   kv->tmp_bytes = t1 > t2 ? t1 : t2;
   KV_HIP(kv, hipMalloc(&kv->tmp, kv->tmp_bytes));
@@ -1193,8 +1212,7 @@ int rg_kv_apply_async(rg_kv* kv, const uint8_t* data_dev, const uint64_t* cmd_of
                      results_dev, kv->set_part);
   KV_HIP(kv, hipGetLastError());
   size_t tb = kv->tmp_bytes;
-  KV_HIP(kv, hipcub::DeviceRadixSort::SortPairs(kv->tmp, tb, kv->key_a, kv->key_b, kv->idx_a, kv->idx_b,
-                                                  (int)n_cmds, 0, sbits, s));
+  KV_HIP(kv, kv_sort(kv->tmp, tb, kv->key_a, kv->key_b, kv->idx_a, kv->idx_b, (int)n_cmds, sbits, s));
   KV_HIP(kv, hipMemsetAsync(kv->done, 0, n_cmds, s));
   BatchView b{data_dev, kv->ops, kv->key_b, kv->idx_b, n_cmds, results_dev, kv->done, kv->need,
               kv->block_base, kv->recs, invalid_bucket, kv->part};
