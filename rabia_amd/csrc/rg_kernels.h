@@ -827,6 +827,24 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_step_kernel(StepParams p) {
     }
   }
   stamp(p, tile, 1, tid);
+#ifdef RG_EARLY_STORES  // build-time experiment: the round-1-only planes (0, 1, 3) stored before the wait
+  // (1: every wave before the look-back; 2: wave 0 after its look-back, the others before)
+  auto early_stores = [&]() {
+    if (active) {
+      uint32_t* ob = p.out + p.lout.base(w0);
+      const uint64_t ps = p.lout.pstride;
+      uint32_t v[W];
+#pragma unroll
+      for (int i = 0; i < W; i++) v[i] = r1v1[i] | pend[i];
+      store_words_nt<W>(ob, v);
+#pragma unroll
+      for (int i = 0; i < W; i++) v[i] = r1vq[i] | pend[i];
+      store_words_nt<W>(ob + ps, v);
+      store_words_nt<W>(ob + 3 * ps, pend);
+    }
+  };
+  if (DEF != 0 && (RG_EARLY_STORES == 1 || wave != 0)) early_stores();
+#endif
   if (wave == 0) {
 #ifdef RG_LB_WIDE  // build-time experiment: K-wide polls (tools/ab_variants.sh)
     const uint32_t e = (p.diag & 1u) ? 0u
@@ -850,6 +868,9 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_step_kernel(StepParams p) {
     }
 #endif
     if (lane == 0) s_excl = e;
+#ifdef RG_EARLY_STORES
+    if (DEF != 0 && RG_EARLY_STORES == 2) early_stores();
+#endif
   }
   // DEF: both-outcome decisions while wave 0 looks back; the R2 registers die here,
   // before the ChaCha12 blocks need theirs
@@ -999,16 +1020,23 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_step_kernel(StepParams p) {
     uint32_t* ob = p.out + p.lout.base(w0);
     const uint64_t ps = p.lout.pstride;
     uint32_t v[W];
+#ifdef RG_EARLY_STORES
+    constexpr bool late = DEF == 0;
+#else
+    constexpr bool late = true;
+#endif
+    if (late) {
 #pragma unroll
-    for (int i = 0; i < W; i++) v[i] = r1v1[i] | pend[i];
-    store_words_nt<W>(ob, v);
+      for (int i = 0; i < W; i++) v[i] = r1v1[i] | pend[i];
+      store_words_nt<W>(ob, v);
 #pragma unroll
-    for (int i = 0; i < W; i++) v[i] = r1vq[i] | pend[i];
-    store_words_nt<W>(ob + ps, v);
+      for (int i = 0; i < W; i++) v[i] = r1vq[i] | pend[i];
+      store_words_nt<W>(ob + ps, v);
+    }
 #pragma unroll
     for (int i = 0; i < W; i++) v[i] = own_lo[i] | pend[i];
     store_words_nt<W>(ob + 2 * ps, v);
-    store_words_nt<W>(ob + 3 * ps, pend);
+    if (late) store_words_nt<W>(ob + 3 * ps, pend);
     store_words_nt<W>(ob + 4 * ps, dlo);
     store_words_nt<W>(ob + 5 * ps, dhi);
     store_words_nt<W>(ob + 6 * ps, st_dec);
