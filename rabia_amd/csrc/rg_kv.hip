@@ -241,6 +241,35 @@ __device__ __forceinline__ uint64_t span_key_hash(const Span<W>& sp, uint32_t n,
   if (h == kInvalidKey) h = kInvalidKey - 1;
   return h;
 }
+template <int W>
+__device__ __forceinline__ void span_store(uint8_t* dst, const Span<W>& sp) {
+#pragma unroll
+  for (int j = 0; j < W; j++)
+    if (j < sp.nw) *(u64_unaligned*)(dst + sp.s[j]) = sp.w[j];  // overlapping words carry equal bytes
+}
+// Copy of n bytes with every load issued before the first store (the byte pointers
+// may alias as far as the compiler knows, so a load-store loop is one round trip per
+// word); n in [8, 64], else the word loop.
+__device__ __forceinline__ void copy_fast(uint8_t* dst, const uint8_t* src, uint32_t n) {
+  if (n >= 8 && n <= 64) {
+    Span<8> sp;
+    span_load(sp, src, n);
+    span_store(dst, sp);
+  } else {
+    bytes_copy(dst, src, n);
+  }
+}
+// Byte equality of two n-byte strings, n in [8, 16] with all four words in flight at
+// once (bytes_eq's early-exit loop is one round trip per word), else bytes_eq.
+__device__ __forceinline__ bool eq_fast(const uint8_t* a, const uint8_t* b, uint32_t n) {
+  if (n >= 8 && n <= 16) {
+    Span<2> x, y;
+    span_load(x, a, n);
+    span_load(y, b, n);
+    return x.w[0] == y.w[0] && x.w[1] == y.w[1];  // equal offsets on both sides; word 1 is 0 when absent
+  }
+  return bytes_eq(a, b, n);
+}
 constexpr uint32_t kFastKey = 16, kFastVal = 64;  // decode fast path: key <= 16 B, value region <= 64 B
 
 // ---- 1 decode ----------------------------------------------------------------
@@ -372,7 +401,7 @@ __device__ int64_t table_find(const uint64_t* hashes, const KvEntry* ent, const 
       const unsigned long long lens = __hip_atomic_load(ep + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       e.key_len = (uint32_t)lens;
       e.val_len = (uint32_t)(lens >> 32);
-      if (e.key_len == klen && bytes_eq(heap + e.key_off, key, klen)) {
+      if (e.key_len == klen && eq_fast(heap + e.key_off, key, klen)) {
         *out = e;
         return (int64_t)s;
       }
@@ -622,7 +651,7 @@ __global__ __launch_bounds__(kBlock) void kv_plan_kernel(BatchView b, StoreView 
         pkl = pp.key_len;
       }
       const uint32_t kl = s_klen[l];
-      const bool eq = s_hash[l] == ph && kl == pkl && bytes_eq(b.data + s_koff[l], b.data + pko, kl);
+      const bool eq = s_hash[l] == ph && kl == pkl && eq_fast(b.data + s_koff[l], b.data + pko, kl);
       if (eq) s_inf[l] = (uint8_t)(inf | kInfSame);
     }
     const unsigned long long m = __ballot(head);
@@ -736,8 +765,17 @@ __global__ __launch_bounds__(kBlock) void kv_commit_kernel(BatchView b, StoreVie
         if (s < 0 || heap_pos > st.heap_cap) {
           atomicOr(&st.ctr->flags, s < 0 ? kFaultTable : kFaultHeap);
         } else {
-          bytes_copy(st.heap + koff, b.data + r.key_src, r.key_len);
-          bytes_copy(st.heap + voff, b.data + r.val_src, r.val_len);
+          if (r.key_len >= 8 && r.key_len <= 16 && r.val_len >= 8 && r.val_len <= 64) {
+            Span<2> ks;  // key and value words all in flight before the stores
+            Span<8> vs;
+            span_load(ks, b.data + r.key_src, r.key_len);
+            span_load(vs, b.data + r.val_src, r.val_len);
+            span_store(st.heap + koff, ks);
+            span_store(st.heap + voff, vs);
+          } else {
+            bytes_copy(st.heap + koff, b.data + r.key_src, r.key_len);
+            bytes_copy(st.heap + voff, b.data + r.val_src, r.val_len);
+          }
           const KvEntry e{koff, voff, r.ver1, r.key_len, r.val_len};
           st.ent[s] = e;
         }
@@ -753,7 +791,7 @@ __global__ __launch_bounds__(kBlock) void kv_commit_kernel(BatchView b, StoreVie
         if (dst + r.val_len > st.heap_cap) {
           atomicOr(&st.ctr->flags, kFaultHeap);
         } else {
-          bytes_copy(st.heap + dst, b.data + r.val_src, r.val_len);
+          copy_fast(st.heap + dst, b.data + r.val_src, r.val_len);
           st.ent[s].val_off = dst;
           st.ent[s].val_len = r.val_len;
         }
