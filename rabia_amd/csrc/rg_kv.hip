@@ -277,7 +277,7 @@ __global__ __launch_bounds__(kBlock) void kv_decode_kernel(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ off, uint64_t n, const uint8_t* __restrict__ mask,
     uint64_t max_value, uint64_t hmask, uint64_t bmask, uint32_t invalid_bucket, KvOp* __restrict__ ops,
     uint32_t* __restrict__ sort_key, uint32_t* __restrict__ sort_idx, uint8_t* __restrict__ results,
-    unsigned long long* __restrict__ set_part) {
+    unsigned long long* __restrict__ set_part, uint8_t* __restrict__ done) {
   const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long sets = 0, set_bytes = 0;  // worst-case growth of the batch (the refusal check)
   if (c < n) {
@@ -359,6 +359,7 @@ __global__ __launch_bounds__(kBlock) void kv_decode_kernel(
   ops[c] = op;
   sort_key[c] = key == kInvalidKey ? invalid_bucket : (uint32_t)hash_bucket(key, bmask);
   sort_idx[c] = (uint32_t)c;
+  done[c] = 0;  // the plan's per-sorted-position marks (multi-key runs), cleared here: no memset launch
   if (op.status != kPending) results[c] = (uint8_t)op.status;
   if (op.status == kPending && op.kind == 0) {
     sets = 1;
@@ -1247,11 +1248,10 @@ int rg_kv_apply_async(rg_kv* kv, const uint8_t* data_dev, const uint64_t* cmd_of
                      apply_mask_dev, kv->cfg.max_value_size,
                      kv->cfg.hash_bits && kv->cfg.hash_bits < 64 ? (1ull << kv->cfg.hash_bits) - 1 : ~0ull,
                      (uint64_t)invalid_bucket - 1, invalid_bucket, kv->ops, kv->key_a, kv->idx_a,
-                     results_dev, kv->set_part);
+                     results_dev, kv->set_part, kv->done);
   KV_HIP(kv, hipGetLastError());
   size_t tb = kv->tmp_bytes;
   KV_HIP(kv, kv_sort(kv->tmp, tb, kv->key_a, kv->key_b, kv->idx_a, kv->idx_b, (int)n_cmds, sbits, s));
-  KV_HIP(kv, hipMemsetAsync(kv->done, 0, n_cmds, s));
   BatchView b{data_dev, kv->ops, kv->key_b, kv->idx_b, n_cmds, results_dev, kv->done, kv->need,
               kv->block_base, kv->recs, invalid_bucket, kv->part};
   const StoreView st = view(kv);
