@@ -18,6 +18,7 @@
 //   6 ordered   otherwise ONE thread replays the batch in total order (exact,
 //               slow; counted in rg_kv_stats.ordered_batches)
 //   7 finish    folds the per-block counter deltas into the store counters
+//               (6, 7 and the refusal results are one launch, kv_close_kernel)
 // Key equality is byte equality (hash runs are split by comparing key bytes).
 // Deleted keys keep their table slot (version 0 = not live) so probe chains stay
 // intact; a later SET of the same key reuses it with a fresh ValueEntry (version 1).
@@ -901,16 +902,9 @@ __global__ __launch_bounds__(kFoldBlock) void kv_decide_kernel(StoreView st, con
 }
 
 // Refused batch (mode 2): every command still pending gets RG_KV_E_CAPACITY.
-__global__ void kv_refuse_kernel(const KvOp* ops, uint64_t n, const KvCounters* k, uint8_t* results) {
-  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= n || k->mode != 2) return;
-  if (ops[c].status == kPending) results[c] = RG_KV_E_CAPACITY;
-}
 
 // ---- 6 ordered replay (StoreFull reachable) -------------------------------------
-__global__ void kv_ordered_kernel(const uint8_t* data, const KvOp* ops, uint64_t n,
-                                  uint8_t* results, StoreView st) {
-  if (threadIdx.x != 0 || st.ctr->mode != 1) return;
+__device__ void kv_ordered(const uint8_t* data, const KvOp* ops, uint64_t n, uint8_t* results, StoreView st) {
   KvCounters* k = st.ctr;
   unsigned long long live = k->live, ver = k->version, tops = k->total_ops, occ = k->occupied, top = k->heap_top;
   for (uint64_t c = 0; c < n; c++) {
@@ -971,9 +965,24 @@ __global__ void kv_ordered_kernel(const uint8_t* data, const KvOp* ops, uint64_t
 }
 
 // ---- 7 finish (keyed path counters) ----------------------------------------------
-__global__ __launch_bounds__(kFoldBlock) void kv_finish_kernel(KvCounters* k, const unsigned long long* part,
-                                                               uint32_t blocks) {
-  if (k->mode != 0) return;
+// One launch closes the batch by its path (mode is uniform): 0 folds the keyed
+// path's counter deltas; 1 runs the ordered replay (one thread); 2 (refused) gives
+// every pending command RG_KV_E_CAPACITY (a block-stride loop: refusals are rare).
+__global__ __launch_bounds__(kFoldBlock) void kv_close_kernel(const uint8_t* data, const KvOp* ops, uint64_t n,
+                                                              uint8_t* results, StoreView st,
+                                                              const unsigned long long* part, uint32_t blocks) {
+  KvCounters* k = st.ctr;
+  const unsigned long long mode = k->mode;
+  if (mode == 1) {
+    if (threadIdx.x == 0) kv_ordered(data, ops, n, results, st);
+    return;
+  }
+  if (mode == 2) {
+    for (uint64_t c = threadIdx.x; c < n; c += blockDim.x)
+      if (ops[c].status == kPending) results[c] = RG_KV_E_CAPACITY;
+    return;
+  }
+  if (mode != 0) return;
   unsigned long long v[3] = {0, 0, 0};
   fold_block<kPLiveDelta, kPVersion, kPOps>(v, part, blocks, kPCount);
   if (threadIdx.x != 0) return;
@@ -1261,10 +1270,8 @@ int rg_kv_apply_async(rg_kv* kv, const uint8_t* data_dev, const uint64_t* cmd_of
   hipLaunchKernelGGL(kv_decide_kernel, dim3(1), dim3(kFoldBlock), 0, s, st, kv->part, walk_blocks, kv->set_part,
                      blocks, kv->block_base);
   hipLaunchKernelGGL(kv_commit_kernel, dim3(walk_blocks), dim3(kBlock), 0, s, b, st);
-  hipLaunchKernelGGL(kv_ordered_kernel, dim3(1), dim3(64), 0, s, data_dev, kv->ops, n_cmds,
-                     results_dev, st);
-  hipLaunchKernelGGL(kv_finish_kernel, dim3(1), dim3(kFoldBlock), 0, s, kv->ctr, kv->part, walk_blocks);
-  hipLaunchKernelGGL(kv_refuse_kernel, dim3(blocks), dim3(kBlock), 0, s, kv->ops, n_cmds, kv->ctr, results_dev);
+  hipLaunchKernelGGL(kv_close_kernel, dim3(1), dim3(kFoldBlock), 0, s, data_dev, kv->ops, n_cmds, results_dev, st,
+                     kv->part, walk_blocks);
   KV_HIP(kv, hipGetLastError());
   return 0;
 }
