@@ -52,6 +52,7 @@ struct rg_ctx {
   unsigned long long* cluster_part = nullptr;  // [blocks][kClusterStats]
   unsigned long long* cluster_stats = nullptr;  // [kClusterStats]
   unsigned long long* fix_acc = nullptr;        // sharded REF fix-up accumulator [4]
+  uint32_t n_cu = 256;                          // compute units (persistent lag-kernel grid)
   std::string err;
 };
 
@@ -77,6 +78,9 @@ int hip_fail(rg_ctx* ctx, hipError_t e, const char* what) {
   } while (0)
 
 constexpr int wmax_for(int n) { return n <= 5 ? 4 : (n <= 10 ? 2 : 1); }
+// persistent lag kernel: 512-thread workgroups, two per CU, lag_words(n) words per thread
+constexpr int kLagBlock = 512;
+constexpr int lag_words(int n) { return n <= 5 ? 2 : 1; }
 
 // Tile shapes: {threads, words per thread}. Big tiles keep the per-launch count
 // of tiles and look-back hand-offs low on large windows; small tiles fill
@@ -127,6 +131,10 @@ struct Disp {
     else if (c == kCfgMid) hipLaunchKernelGGL((ref_step_kernel<N, WM, 256, false, 1>), dim3(grid), dim3(256), 0, s, p);
     else hipLaunchKernelGGL((ref_step_kernel<N, 1, 128, false, 1>), dim3(grid), dim3(128), 0, s, p);
   }
+  // persistent lag kernel (large launches): grid = resident workgroups, tiles by ticket
+  static void ref_lag(uint32_t grid, hipStream_t s, const StepParams& p) {
+    hipLaunchKernelGGL((ref_lag_kernel<N, lag_words(N), kLagBlock, false>), dim3(grid), dim3(kLagBlock), 0, s, p);
+  }
   static void wmvc(int c, uint32_t grid, hipStream_t s, const StepParams& p) {
     if (c == kCfgBig) hipLaunchKernelGGL((wmvc_step_kernel<N, WM, 512>), dim3(grid), dim3(512), 0, s, p);
     else if (c == kCfgMid) hipLaunchKernelGGL((wmvc_step_kernel<N, WM, 256>), dim3(grid), dim3(256), 0, s, p);
@@ -166,6 +174,8 @@ using DigestLaunch = void (*)(uint32_t, hipStream_t, const uint64_t*, uint64_t, 
    &Disp<12>::fn, &Disp<13>::fn, &Disp<14>::fn, &Disp<15>::fn, &Disp<16>::fn}
 
 const StepLaunch kRefLaunch[17] = RG_TABLE(ref);
+using LagLaunch = void (*)(uint32_t, hipStream_t, const StepParams&);
+const LagLaunch kRefLagLaunch[17] = RG_TABLE(ref_lag);
 const StepLaunch kWmvcLaunch[17] = RG_TABLE(wmvc);
 const DigestLaunch kDigestLaunch[17] = RG_TABLE(digest);
 const ClusterLaunch kClusterLaunch[17] = RG_TABLE(cluster);
@@ -280,6 +290,7 @@ int rg_create(rg_ctx** out, const rg_config* cfg) {
   rg_ctx* ctx = new (std::nothrow) rg_ctx();
   if (!ctx) return fail(nullptr, RG_ENOMEM, "rg_create: host allocation failed");
   ctx->cfg = *cfg;
+  ctx->n_cu = prop.multiProcessorCount > 0 ? (uint32_t)prop.multiProcessorCount : 256u;
   ctx->cfg.quorum = q;
   ctx->cfg.decide_threshold = fp1;
   ctx->q = q;
@@ -399,9 +410,20 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
   const uint32_t dforce = (ctx->diag >> 16) & 7u;  // diagnostics: A/B shapes (REF, n = 5)
   if (dforce && (dforce > 2 || n != 5 || wmvc || shard)) return fail(ctx, RG_EINVAL, "rg_debug_set: bad shape");
   int cfg = dforce ? kCfgLegacyBig + (int)dforce - 1 : force ? (int)force - 1 : pick_cfg(n, n_words);
-  uint64_t tile_words = (uint64_t)cfg_block(cfg) * cfg_words(cfg, n);
+  // Large REF launches run the persistent lag kernel (512 x lag_words tiles, taken by
+  // ticket): two resident workgroups per CU. diag bit 20 keeps the tiled kernel
+  // (A/B), bit 21 forces the lag kernel at any size.
+  const bool lag_ok = !wmvc && cfg == kCfgBig && !dforce && !force && !(ctx->diag & 0x7u);
+  // (its buffer offsets are 31-bit: every plane of a tile within 2 GiB of the tile base)
+  const bool lag_fits = (uint64_t)(4 * n + 1) * lin.pstride * 4 + 4096 < (1ull << 31) &&
+                        (uint64_t)kOutPlanes * lout.pstride * 4 + 4096 < (1ull << 31);
+  const bool lag = lag_fits && ((ctx->diag & 0x200000u) ? !wmvc : (lag_ok && !(ctx->diag & 0x100000u)));
+  uint64_t tile_words = lag ? (uint64_t)kLagBlock * lag_words(n) : (uint64_t)cfg_block(cfg) * cfg_words(cfg, n);
   uint64_t n_tiles = (n_words + tile_words - 1) / tile_words;
-  const uint64_t gran_tiles = n_tiles;
+  const uint32_t grid_force = (ctx->diag >> 24) & 0xFFu;  // diagnostics: lag-kernel grid (tests: many tiles per WG)
+  const uint64_t lag_grid_max = grid_force ? grid_force : 2ull * ctx->n_cu;
+  const uint32_t lag_grid = (uint32_t)(n_tiles < lag_grid_max ? n_tiles : lag_grid_max);
+  const uint64_t gran_tiles = lag ? (n_tiles > 3ull * lag_grid ? n_tiles : 3ull * lag_grid) : n_tiles;
   if (int rc = ensure_tiles(ctx, gran_tiles, false)) return rc;
   // Statistics granules carry 12 bits of seq and look-back granules 31: start a
   // fresh epoch on zeroed granules whenever either wraps.
@@ -448,7 +470,8 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
     p.dbg = ctx->dbg;
   }
   hipStream_t s = pick_stream(ctx, stream);
-  if (shard) launch_ref_shard(n, cfg_block(cfg), cfg_words(cfg, n), (uint32_t)n_tiles, s, p);
+  if (shard) launch_ref_shard(n, lag ? 0 : cfg_block(cfg), cfg_words(cfg, n), lag ? lag_grid : (uint32_t)n_tiles, s, p);
+  else if (lag) kRefLagLaunch[n](lag_grid, s, p);
   else (wmvc ? kWmvcLaunch : kRefLaunch)[n](cfg, (uint32_t)n_tiles, s, p);
   RG_HIP(ctx, hipGetLastError());
   return RG_OK;

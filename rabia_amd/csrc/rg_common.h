@@ -103,6 +103,8 @@ struct alignas(128) Line {
 // (e+1)&1 for the next launch, so no host memset sits between steps.
 struct Record {
   Line error;      // device protocol fault bits
+  Line ticket;     // lag kernel: next tile ticket (dynamic tile order)
+  Line done;       // lag kernel: workgroups that published their statistics
 };
 
 struct DevState {

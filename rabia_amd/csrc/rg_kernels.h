@@ -456,6 +456,9 @@ __device__ __forceinline__ void block_reduce_totals(unsigned long long (&v)[7], 
   for (int k = 0; k < 7; k++) v[k] = r[k];
 }
 
+template <int FIN>
+__device__ __forceinline__ void step_commit(const StepParams& p, Record* rec, const unsigned long long (&v)[7]);
+
 // Publish this tile's statistics; the tile with the last index folds every
 // tile's granules, advances the device engine state and writes the step result.
 template <int FIN, int BLOCK, int W, int kBatch = 8>  // kBatch: tiles per thread with loads in flight together
@@ -517,8 +520,17 @@ __device__ __forceinline__ void finish_tile(const StepParams& p, Record* rec, Ti
   block_reduce_totals<BLOCK>(v, lane, wave);
   stamp(p, tile, 5, tid);
   if (tid != 0) return;
+  step_commit<FIN>(p, rec, v);
+}
+
+// The launch's totals (dec v1 pend draws max(id+1) min(id) fault) -> step result and
+// engine state. Run by ONE thread after every tile's statistics are in. Each flavour
+// writes only the DevState fields it owns: the sharded step may run on one stream
+// while the fix-up and commit of an earlier window (rng_next, last_committed,
+// commit_watermark, steps) run on another.
+template <int FIN>
+__device__ __forceinline__ void step_commit(const StepParams& p, Record* rec, const unsigned long long (&v)[7]) {
   const unsigned long long err = atomicAdd(&rec->error.v, 0ull) | v[6];
-  DevState s = *p.state;
   DevResult r;
   r.n_slots = p.n_slots;
   r.n_decided = v[0];
@@ -534,15 +546,15 @@ __device__ __forceinline__ void finish_tile(const StepParams& p, Record* rec, Ti
     // rg_shard_commit (state.rs:65-103 over the whole window).
     r.last_committed_max = v[4] ? v[4] - 1 : 0;
     r.first_undecided = fu;
-    r.rng_next = s.shard_draws + r.n_draws;
+    r.rng_next = p.state->shard_draws + r.n_draws;
     r.commit_watermark = 0;
     r.flags = err;
-    s.shard_draws = r.rng_next;
-    *p.state = s;
+    p.state->shard_draws = r.rng_next;
     *p.result = r;
     if (p.result_user) *p.result_user = r;
     return;
   }
+  DevState s = *p.state;
   unsigned long long lc = s.last_committed;          // commit_phase: monotonic max,
   if (v[4] && v[4] - 1 > lc) lc = v[4] - 1;          // state.rs:77-99
   unsigned long long wm = s.commit_watermark;
@@ -552,11 +564,10 @@ __device__ __forceinline__ void finish_tile(const StepParams& p, Record* rec, Ti
   r.rng_next = FIN == kFinRef ? s.rng_next + r.n_draws : s.rng_next;
   r.commit_watermark = wm;
   r.flags = err;
-  s.rng_next = r.rng_next;
-  s.last_committed = lc;
-  s.commit_watermark = wm;
-  s.steps += 1;
-  *p.state = s;
+  p.state->rng_next = r.rng_next;
+  p.state->last_committed = lc;
+  p.state->commit_watermark = wm;
+  p.state->steps = s.steps + 1;
   *p.result = r;
   if (p.result_user) *p.result_user = r;
 }
@@ -574,6 +585,8 @@ __device__ __forceinline__ bool tile_prologue(const StepParams& p, Record* rec, 
   if (tid == 0 && tile == p.n_tiles - 1) {
     Record* nxt = p.rec + ((p.seq + 1) & 1u);
     atomic_store_agent(&nxt->error.v, 0ull);
+    atomic_store_agent(&nxt->ticket.v, 0ull);
+    atomic_store_agent(&nxt->done.v, 0ull);
   }
   return true;
 }
@@ -1055,6 +1068,639 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_step_kernel(StepParams p) {
   const TileStats ts = thread_stats<W>(st_dec, st_v1, pend, st_vm, vq_count, w0, tw0, p);
   finish_tile<SHARD ? kFinShard : kFinRef, BLOCK, W, (OCC > 4 ? 2 : 8)>(p, rec, ts, tile, tid, lane, wave);
   stamp(p, tile, 4, tid);
+}
+
+// ============================================================================
+// Persistent REF step with dynamic tile tickets and a one-tile lag (large launches).
+//
+// The tiled kernel above makes every tile wait for its VQ prefix between its plane
+// loads and its stores; under full streaming load a look-back poll is a 3-4 us
+// round trip through the CU's own memory queue (MI355X_MICROARCH.md handoff-1to1),
+// during which the tile's 8 waves hold half the CU and move nothing. Here a
+// workgroup never waits for its own tile: it publishes the tile's aggregate, parks
+// what the draws still need in LDS, and takes its next tile; the parked tile is
+// finished (draws, decisions, stores) one iteration later, while the next tile's
+// round-2 planes are in flight. By then every predecessor published its aggregate
+// long ago, so the look-back almost never spins.
+//
+// Tile order is a ticket from one counter per launch (Record.ticket), not
+// blockIdx: a tile index is only ever held by a running workgroup and a workgroup
+// only waits for lower tickets, whose holders never wait on it (the lowest
+// unfinished ticket always progresses). Forward progress therefore needs no
+// dispatch-order assumption, and two such launches sharing a GPU cannot wait on
+// each other (the tiled kernel's cross-kernel cycle).
+//
+// Look-back of the parked tile p: the workgroup knows the inclusive prefix of its
+// own previous tile pp (< p), so the scan ends at pp at the latest; any newer
+// inclusive granule ends it earlier. kLagPoll x 64 granules per poll, issued at the
+// top of the iteration (ahead of the round-1 loads) and resolved after the tally.
+// Statistics accumulate per thread over all of a workgroup's tiles; each
+// workgroup publishes one record and the last to arrive (Record.done) folds them.
+// ============================================================================
+constexpr int kLagPoll = 4;
+constexpr int kLagStatGranules = 6;  // dec v1 pend draws max_off1 min_off, {tag:13 | value:51}
+
+// Poll granules at distances d = 64k + lane below `pos` (index pos - d); indices at
+// or below pp are never read (their value is synthetic: pp is inclusive).
+__device__ __forceinline__ void lag_poll(const unsigned long long* status, int32_t pos, int32_t pp, int lane,
+                                         unsigned long long (&g)[kLagPoll]) {
+#pragma unroll
+  for (int k = 0; k < kLagPoll; k++) {
+    const int32_t idx = pos - lane - 64 * k;
+    // branchless: an index at or below pp reads granule 0 and the value is ignored
+    g[k] = atomic_load_agent(const_cast<unsigned long long*>(status) + (idx > pp ? idx : 0));
+  }
+}
+
+// One pass of the look-back of tile p over a poll g at `pos` (wave 0, all lanes):
+// adds the values up to the newest inclusive granule to excl and returns true when
+// that granule was in the poll (the prefix is complete); false with blocked = some
+// needed granule is not published yet (poll again at the same pos), or blocked =
+// false: everything was an aggregate (continue below pos - 64 * kLagPoll).
+__device__ __forceinline__ bool lag_eval(const unsigned long long (&g)[kLagPoll], int32_t pos, int32_t pp,
+                                         uint32_t incl_pp, uint32_t seq, int lane, uint32_t& excl,
+                                         bool& blocked) {
+  int first = 64 * kLagPoll;
+  bool blk = false;
+  uint32_t v = 0;
+#pragma unroll
+  for (int k = 0; k < kLagPoll; k++) {
+    const int32_t idx = pos - lane - 64 * k;
+    const uint32_t tag = (uint32_t)(g[k] >> 32);
+    const bool synth = idx <= pp;
+    const bool ready = synth || (tag >> 1) == seq;
+    const bool incl = synth || (ready && (tag & 1u));
+    const unsigned long long im = __ballot(incl), nr = __ballot(!ready);
+    const bool open = first == 64 * kLagPoll && !blk;  // wave-uniform
+    const int f = im ? __builtin_ctzll(im) : 64;
+    const unsigned long long need = f >= 63 ? ~0ull : ((2ull << f) - 1ull);
+    if (open && (nr & need)) blk = true;
+    if (open && !(nr & need)) {
+      if (lane <= f) v += idx == pp ? incl_pp : (synth ? 0u : (uint32_t)g[k]);
+      if (f < 64) first = 64 * k + f;
+    }
+  }
+  blocked = blk;
+  if (blk) return false;
+  excl += wave_sum32(v);
+  return first < 64 * kLagPoll;
+}
+
+// The rest of a look-back that lag_eval left open (pos/excl as it left them).
+__device__ __forceinline__ uint32_t lag_finish(const unsigned long long* status, int32_t pos, int32_t pp,
+                                               uint32_t incl_pp, uint32_t seq, int lane, uint32_t excl,
+                                               bool blocked, unsigned long long* err) {
+  uint32_t spins = 0;
+  for (;;) {
+    if (blocked) {
+      if (++spins > (1u << 22)) {  // ~seconds: a protocol fault, not a wait
+        if (lane == 0) {
+          atomicOr(err, 1ull);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        return excl;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    } else {
+      pos -= 64 * kLagPoll;
+    }
+    unsigned long long g[kLagPoll];
+    lag_poll(status, pos, pp, lane, g);
+    if (lag_eval(g, pos, pp, incl_pp, seq, lane, excl, blocked)) return excl;
+  }
+}
+
+// W consecutive words of one thread in LDS (one ds_read/write_b128 at W = 4)
+template <int W>
+__device__ __forceinline__ void lds_ld(const uint32_t* s, uint32_t (&v)[W]) {
+  if constexpr (W == 4) {
+    const u32x4 x = *reinterpret_cast<const u32x4*>(s);
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+  } else if constexpr (W == 2) {
+    const u32x2 x = *reinterpret_cast<const u32x2*>(s);
+    v[0] = x.x; v[1] = x.y;
+  } else {
+    v[0] = s[0];
+  }
+}
+template <int W>
+__device__ __forceinline__ void lds_st(uint32_t* s, const uint32_t (&v)[W]) {
+  if constexpr (W == 4) {
+    u32x4 x;
+    x.x = v[0]; x.y = v[1]; x.z = v[2]; x.w = v[3];
+    *reinterpret_cast<u32x4*>(s) = x;
+  } else if constexpr (W == 2) {
+    u32x2 x;
+    x.x = v[0]; x.y = v[1];
+    *reinterpret_cast<u32x2*>(s) = x;
+  } else {
+    s[0] = v[0];
+  }
+}
+
+// Plane access of the lag kernel through buffer resources: the tile's uniform base in
+// SGPRs, the thread's offset in ONE VGPR for every plane, the plane offset in an SGPR
+// (a global load needs a 64-bit VGPR address per plane: 20 of them in flight at n = 5).
+// A tile of kTW words starts on a layout-tile boundary (both powers of two), so
+// Layout::base(tile_start + x) = base(tile_start) + base(x).
+// num_records = 2^31: an offset of kOffNone (a lane past the window) is out of range,
+// so its store is dropped by the buffer unit instead of being branched around (a
+// conditional store between a load and its use makes the compiler's waitcnt merge
+// wait for everything). The host keeps every real offset below 2^31.
+constexpr uint32_t kOffNone = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const uint32_t* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(base), (short)0, (int)kOffNone, 0x00020000);
+}
+constexpr int kAuxNT = 2;  // non-temporal (read or written once)
+
+template <int W>
+__device__ __forceinline__ void buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, uint32_t (&v)[W]) {
+  if constexpr (W == 4) {
+    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, kAuxNT);
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+  } else if constexpr (W == 2) {
+    const u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, kAuxNT);
+    v[0] = x.x; v[1] = x.y;
+  } else {
+    v[0] = __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, kAuxNT);
+  }
+}
+template <int W>
+__device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, const uint32_t (&v)[W]) {
+  if constexpr (W == 4) {
+    u32x4 x;
+    x.x = v[0]; x.y = v[1]; x.z = v[2]; x.w = v[3];
+    __builtin_amdgcn_raw_buffer_store_b128(x, r, voff, soff, kAuxNT);
+  } else if constexpr (W == 2) {
+    u32x2 x;
+    x.x = v[0]; x.y = v[1];
+    __builtin_amdgcn_raw_buffer_store_b64(x, r, voff, soff, kAuxNT);
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b32(v[0], r, voff, soff, kAuxNT);
+  }
+}
+// 2N vote planes starting at plane `first` (lo, hi per replica lane)
+template <int N, int W>
+__device__ __forceinline__ void buf_ld_planes(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t pbytes, int first,
+                                              uint32_t (&lo)[N][W], uint32_t (&hi)[N][W]) {
+#pragma unroll
+  for (int j = 0; j < N; j++) {
+    buf_ld<W>(r, voff, (uint32_t)(first + 2 * j) * pbytes, lo[j]);
+    buf_ld<W>(r, voff, (uint32_t)(first + 2 * j + 1) * pbytes, hi[j]);
+  }
+}
+
+// Parked per-thread state of a tile, s_park[buffer][field][tid][word]; two buffers
+// (by iteration parity): the tile being tallied writes one while the parked tile's
+// finish reads the other, so no tile state waits in registers across the finish.
+//   0 plane-0 value (V1 | pending; plane 2 = this | the VQ slots whose draw gave V1)
+//   1 pending (round 1 without quorum)
+//   2 e0 = VQ & !(c1 < c0), 3 e1 = VQ & !(c1 > c0)   (VQ = e0 | e1; gt = e0 & !e1, lt = e1 & !e0)
+//   4-5 decision (lo, hi) if the own round-2 vote is V0, 6-7 if it is V1
+constexpr int kParkFields = 8;
+
+// Next tile ticket. The address is made divergent-looking so that LLVM's atomic
+// optimizer leaves the returning atomic alone: its wave-aggregated form reads the
+// result back at once (s_waitcnt vmcnt(0)), i.e. waits for every store in flight.
+// 32-bit (the low word of Record.ticket): a 64-bit result register pair whose high
+// half is dead gets reused while the atomic is in flight, which forces a wait.
+__device__ __forceinline__ uint32_t take_ticket(Record* rec) {
+  const uint32_t zero = __builtin_amdgcn_mbcnt_lo(0u, 0u);  // 0, divergent to the compiler
+  return atomicAdd(reinterpret_cast<unsigned int*>(&rec->ticket.v) + zero, 1u);
+}
+
+template <int N, int W, int BLOCK, bool SHARD>
+__global__ __launch_bounds__(BLOCK, 2 * BLOCK / 256) void ref_lag_kernel(StepParams p) {
+  constexpr int B = ctr_bits(N);
+  constexpr int WAVES = BLOCK / 64;
+  constexpr int kRows = BLOCK < 128 ? BLOCK : 128;
+  constexpr uint32_t kTW = (uint32_t)BLOCK * W;  // words per tile
+  __shared__ __attribute__((aligned(16))) uint32_t s_park[2][kParkFields][BLOCK][W];
+  __shared__ uint32_t s_blk[kRows][17];  // ChaCha12 blocks of the parked tile's draws (+1 word: no conflicts)
+  __shared__ uint32_t s_wave[WAVES];
+  __shared__ unsigned long long s_lb[WAVES];  // per-wave look-back result: sum | inclusive << 32 | blocked << 33
+  __shared__ uint32_t s_bcast[4];        // [0] next ticket, [1] parked tile's prefix (continued look-back)
+  Record* rec = p.rec + (p.seq & 1u);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t tag_agg = p.seq << 1, tag_inc = tag_agg | 1u;
+  const unsigned long long k_base = SHARD ? p.state->shard_draws : p.state->rng_next;  // StdRng position
+
+  // this thread's byte offsets inside a tile's planes; plane strides in bytes
+  const uint32_t in_lane = (uint32_t)p.lin.base((uint64_t)tid * W) * 4u;
+  const uint32_t out_lane = (uint32_t)p.lout.base((uint64_t)tid * W) * 4u;
+  const uint32_t in_pb = (uint32_t)p.lin.pstride * 4u, out_pb = (uint32_t)p.lout.pstride * 4u;
+  auto in_rsrc = [&](uint32_t t) { return plane_rsrc(p.votes + p.lin.base((uint64_t)t * kTW)); };
+  auto out_rsrc = [&](uint32_t t) { return plane_rsrc(p.out + p.lout.base((uint64_t)t * kTW)); };
+  auto active = [&](uint32_t t) { return (uint64_t)t * kTW + (uint64_t)tid * W < p.n_words; };
+  // a thread past the window loads its tile's first word (valid; its masks are 0)
+  // and its stores go out of range (dropped)
+  auto in_off = [&](uint32_t t) { return active(t) ? in_lane : 0u; };
+  auto out_off = [&](uint32_t t) { return active(t) ? out_lane : kOffNone; };
+
+  // tickets: c = the tile being tallied (its round-1 planes were loaded during the
+  // previous iteration); the ticket after it is requested one iteration ahead
+  uint32_t nt = 0;
+  if (tid == 0) s_bcast[0] = take_ticket(rec);
+  lds_barrier();
+  uint32_t c = s_bcast[0];
+  if (tid == 0) nt = take_ticket(rec);
+  uint32_t r1lo[N][W], r1hi[N][W];
+  unsigned long long lbg;  // the look-back poll of the tile parked next (issued before its successor's loads)
+
+  int32_t prev_tile = -1;   // this workgroup's last finished tile and its inclusive prefix
+  uint32_t prev_incl = 0;
+  int32_t park_tile = -1;   // the parked tile, its VQ total and this thread's offset in it
+  uint32_t park_total = 0, park_thr = 0;
+  uint32_t pk = 0;          // park buffer of the tile being tallied (the parked tile: pk ^ 1)
+  uint32_t a_dec = 0, a_v1 = 0, a_pend = 0, a_draws = 0, a_max1 = 0, a_min = ~0u;  // launch-relative offsets
+
+  // ---- look-back of the parked tile p: every wave polls 64 predecessor granules
+  // (wave w: distances 64w .. 64w + 63 below p; one load per lane, so every wave
+  // issues the same memory operations) with the round-1 planes' wait, evaluates them
+  // after the tally, and the waves' results combine after the scan barrier.
+  auto lb_poll = [&]() -> unsigned long long {
+    const int32_t idx = park_tile - 1 - (64 * wave + lane);
+    return atomic_load_agent(p.lookback + (idx > prev_tile ? idx : 0));
+  };
+  auto lb_eval = [&](unsigned long long g) {
+    const int32_t idx = park_tile - 1 - (64 * wave + lane);
+    const uint32_t tag = (uint32_t)(g >> 32);
+    const bool synth = idx <= prev_tile;  // prev_tile is inclusive (this WG computed it)
+    const bool ready = synth || (tag >> 1) == p.seq;
+    const bool incl = synth || (ready && (tag & 1u));
+    const unsigned long long im = __ballot(incl), nr = __ballot(!ready);
+    const int f = im ? __builtin_ctzll(im) : 64;
+    const unsigned long long need = f >= 63 ? ~0ull : ((2ull << f) - 1ull);
+    const uint32_t val = idx == prev_tile ? prev_incl : (synth ? 0u : (uint32_t)g);
+    const uint32_t sum = wave_sum32(lane <= f ? val : 0u);
+    if (lane == 0)
+      s_lb[wave] = (unsigned long long)sum | ((unsigned long long)(f < 64) << 32) |
+                   ((unsigned long long)((nr & need) != 0) << 33);
+  };
+  // after the barrier (uniform): true and the prefix when the polls reached an inclusive
+  auto lb_combine = [&](uint32_t& excl) -> bool {
+    excl = 0;
+#pragma unroll
+    for (int w = 0; w < WAVES; w++) {
+      const unsigned long long x = s_lb[w];
+      if (x >> 33) return false;  // a granule it needs is not published yet
+      excl += (uint32_t)x;
+      if ((x >> 32) & 1u) return true;
+    }
+    return false;  // every polled granule was an aggregate: continue further back
+  };
+
+  // Draws of the parked tile: own round-2 votes of its VQ slots (bits set = V1).
+  auto draw_parked = [&](uint32_t (&own)[W]) {
+    uint32_t(&pp)[kParkFields][BLOCK][W] = s_park[pk ^ 1u];
+    uint32_t excl;
+    if (!lb_combine(excl)) {  // uniform: the rare continued look-back (wave 0, 256 granules per poll)
+      if (wave == 0) {
+        const uint32_t e = lag_finish(p.lookback, park_tile - 1 + 64 * kLagPoll, prev_tile, prev_incl, p.seq, lane,
+                                      0u, false, &rec->error.v);
+        if (lane == 0) s_bcast[1] = e;
+      }
+      lds_barrier();
+      excl = s_bcast[1];
+    }
+    if (tid == 0)
+      atomic_store_agent(p.lookback + park_tile, ((unsigned long long)tag_inc << 32) | (excl + park_total));
+    prev_tile = park_tile;
+    prev_incl = excl + park_total;
+    const unsigned long long k_tile = k_base + excl;
+    // VQ slots whose draw gave V1 (engine.rs:523-537, 567-611)
+#pragma unroll
+    for (int i = 0; i < W; i++) own[i] = 0;
+    if (park_total) {
+      uint32_t mq[W];
+      {
+        uint32_t e0[W], e1[W];
+        lds_ld<W>(pp[2][tid], e0);
+        lds_ld<W>(pp[3][tid], e1);
+#pragma unroll
+        for (int i = 0; i < W; i++) mq[i] = e0[i] | e1[i];
+      }
+      unsigned long long k = k_tile + park_thr;
+      const unsigned long long b_first = k_tile >> 3, b_last = (k_tile + park_total - 1) >> 3;
+      for (unsigned long long cb = b_first; cb <= b_last; cb += kRows) {
+        if (tid < kRows && cb + tid <= b_last) {
+          uint32_t x[16];
+          chacha_block<12>(p.key, cb + tid, 0, x);
+#pragma unroll
+          for (int j = 0; j < 16; j++) s_blk[tid][j] = x[j];
+        }
+        lds_barrier();
+        const unsigned long long k_lim = (cb + kRows) << 3;
+#pragma unroll
+        for (int i = 0; i < W; i++) {
+          if (!mq[i] || k >= k_lim) continue;
+          const uint32_t e0 = pp[2][tid][i], e1 = pp[3][tid][i];
+          while (mq[i] && k < k_lim) {
+            const int b = __builtin_ctz(mq[i]);
+            mq[i] &= mq[i] - 1;
+            const uint32_t row = (uint32_t)((k >> 3) - cb), ws = (uint32_t)(k & 7u) * 2u;
+            const unsigned long long u =
+                (unsigned long long)s_blk[row][ws] | ((unsigned long long)s_blk[row][ws + 1] << 32);
+            const bool x0 = (e0 >> b) & 1u, x1 = (e1 >> b) & 1u;  // gt: 1/0, lt: 0/1, tie: 1/1
+            const bool v1 = (x0 && !x1) ? (u < kP90) : ((x1 && !x0) ? (u >= kP90) : (u < kP80));
+            own[i] |= (uint32_t)v1 << b;
+            k++;
+          }
+        }
+        lds_barrier();
+      }
+    }
+    if constexpr (SHARD) {  // draw records, indexed by local draw number (ascending slot order)
+      const uint32_t pw0 = (uint32_t)park_tile * kTW + (uint32_t)tid * W;
+      uint32_t e0[W], e1[W], alo[W], ahi[W], blo[W], bhi[W];
+      lds_ld<W>(pp[2][tid], e0);
+      lds_ld<W>(pp[3][tid], e1);
+      lds_ld<W>(pp[4][tid], alo);
+      lds_ld<W>(pp[5][tid], ahi);
+      lds_ld<W>(pp[6][tid], blo);
+      lds_ld<W>(pp[7][tid], bhi);
+      unsigned long long kr = excl + park_thr;
+#pragma unroll
+      for (int i = 0; i < W; i++) {
+        uint32_t m = e0[i] | e1[i];
+        while (m) {
+          const int b = __builtin_ctz(m);
+          m &= m - 1;
+          const uint32_t x0 = (e0[i] >> b) & 1u, x1 = (e1[i] >> b) & 1u;
+          const uint32_t cls = (x0 && !x1) ? kRecGt : ((x1 && !x0) ? kRecLt : 0u);
+          const uint32_t d_v0 = ((alo[i] >> b) & 1u) | (((ahi[i] >> b) & 1u) << 1);
+          const uint32_t d_v1 = ((blo[i] >> b) & 1u) | (((bhi[i] >> b) & 1u) << 1);
+          const uint32_t info = cls | (d_v0 << 2) | (d_v1 << 4) | (((own[i] >> b) & 1u) << 6);
+          if (kr < p.vq_cap) p.vq_rec[kr] = ((unsigned long long)info << 32) | (32u * (pw0 + i) + b);
+          kr++;
+        }
+      }
+    }
+  };
+
+  // Decisions, stores and statistics of the parked tile (after draw_parked). Every
+  // lane stores (a lane past the window out of range): no branch between the plane
+  // loads in flight and their use.
+  // Without a parked tile (a workgroup's first iteration) it issues the same stores
+  // out of range and counts nothing: every path into the next tally then has the
+  // same memory operations in flight behind the round-1 loads.
+  auto store_parked = [&](const uint32_t (&own)[W], bool have_park) {
+    uint32_t(&pp)[kParkFields][BLOCK][W] = s_park[pk ^ 1u];
+    const uint32_t pt = have_park ? (uint32_t)park_tile : 0u;
+    const uint32_t pw0 = pt * kTW + (uint32_t)tid * W;
+    const __amdgpu_buffer_rsrc_t orr = out_rsrc(pt);
+    const uint32_t oo = have_park ? out_off(pt) : kOffNone;
+    {  // plane 2: own round-2 vote lo
+      uint32_t v[W];
+      lds_ld<W>(pp[0][tid], v);
+#pragma unroll
+      for (int i = 0; i < W; i++) v[i] |= own[i];
+      buf_st<W>(orr, oo, 2 * out_pb, v);
+    }
+    uint32_t dlo[W], dhi[W];  // own vote joins round2_votes (engine.rs:540-542); decision (613-628)
+    {
+      uint32_t alo[W], ahi[W], blo[W], bhi[W];
+      lds_ld<W>(pp[4][tid], alo);
+      lds_ld<W>(pp[5][tid], ahi);
+      lds_ld<W>(pp[6][tid], blo);
+      lds_ld<W>(pp[7][tid], bhi);
+#pragma unroll
+      for (int i = 0; i < W; i++) {
+        dlo[i] = (alo[i] & ~own[i]) | (blo[i] & own[i]);
+        dhi[i] = (ahi[i] & ~own[i]) | (bhi[i] & own[i]);
+      }
+    }
+    buf_st<W>(orr, oo, 4 * out_pb, dlo);
+    buf_st<W>(orr, oo, 5 * out_pb, dhi);
+    uint32_t keep[W];  // SHARD: VQ slots are counted by the fix-up
+#pragma unroll
+    for (int i = 0; i < W; i++) keep[i] = have_park ? ~0u : 0u;
+    if constexpr (SHARD) {
+      uint32_t e0[W], e1[W];
+      lds_ld<W>(pp[2][tid], e0);
+      lds_ld<W>(pp[3][tid], e1);
+#pragma unroll
+      for (int i = 0; i < W; i++) keep[i] &= ~(e0[i] | e1[i]);
+    }
+    const uint32_t toff = 32u * pw0;  // launch-relative slot offset of this thread's first word
+#pragma unroll
+    for (int i = 0; i < W; i++) {
+      const uint32_t vm = valid_mask(pw0 + i, p.n_words, p.n_slots);
+      const uint32_t pdec = ~dhi[i] & vm;    // committed iff not VQuestion
+      const uint32_t pv1 = dlo[i] & ~dhi[i];  // V1: apply_batch + commit_phase
+      dlo[i] = pdec;
+      dhi[i] = pv1;
+      const uint32_t cd = pdec & keep[i], c1 = pv1 & keep[i];
+      a_dec += __builtin_popcount(cd);
+      a_v1 += __builtin_popcount(c1);
+      const uint32_t m1 = c1 & phase_limit_mask(p.slot_base, pw0 + i, p.max_phase);
+      const uint32_t o1 = m1 ? toff + 32u * i + (31u - __builtin_clz(m1)) + 1u : 0u;
+      a_max1 = o1 > a_max1 ? o1 : a_max1;
+      const uint32_t und = ~pdec & vm & keep[i];
+      const uint32_t o0 = und ? toff + 32u * i + __builtin_ctz(und) : ~0u;
+      a_min = o0 < a_min ? o0 : a_min;
+    }
+    buf_st<W>(orr, oo, 6 * out_pb, dlo);
+    buf_st<W>(orr, oo, 7 * out_pb, dhi);
+  };
+
+  // The vector memory counter retires in issue order, so an iteration issues, in this
+  // order: [tally's stores] [round 2 of tile c] [the parked tile's stores] [the
+  // look-back poll of tile c] [round 1 of the next tile]. The next tally waits for the
+  // round-1 planes, and the poll (older) has landed by then. The operations issued do
+  // not depend on whether a tile is parked (the poll and stores without one are
+  // harmless), so the compiler's waits count exactly on every path.
+  {
+    lbg = lb_poll();
+    const bool any = c < p.n_tiles;
+    buf_ld_planes<N, W>(in_rsrc(any ? c : 0u), any ? in_off(c) : 0u, in_pb, 0, r1lo, r1hi);
+  }
+  while (c < p.n_tiles) {
+    const bool have_park = park_tile >= 0;
+    uint32_t(&pc)[kParkFields][BLOCK][W] = s_park[pk];
+    // (1) round 1 of tile c: count_votes + |votes| >= quorum fallback (engine.rs:495-505);
+    //     the round-1-only output planes (final already) and the tile's state to LDS
+    const uint32_t w0 = c * kTW + (uint32_t)tid * W;
+    uint32_t vq_count = 0;
+    {
+      uint32_t v1[W], vq[W], pd[W], e0[W], e1[W];
+      uint32_t seq0 = 0;  // a zero the compiler cannot see through: the words tally one after another
+#pragma unroll
+      for (int i = 0; i < W; i++) {
+        const uint32_t vm = valid_mask(w0 + i, p.n_words, p.n_slots);
+        Ctr<B> c0, c1, cp;
+        ctr_zero(c0); ctr_zero(c1); ctr_zero(cp);
+        c0.b[0] = c1.b[0] = cp.b[0] = seq0;
+#pragma unroll
+        for (int j = 0; j < N; j++) {
+          const uint32_t lo = r1lo[j][i], hi = r1hi[j][i];
+          ctr_add(c0, ~lo & ~hi);
+          ctr_add(c1, lo & ~hi);
+          ctr_add(cp, ~(lo & hi));
+        }
+        const uint32_t g0 = ctr_ge(c0, p.q), g1 = ctr_ge(c1, p.q), gp = ctr_ge(cp, p.q);
+        const uint32_t x0 = g0 & vm;
+        v1[i] = ~g0 & g1 & vm;
+        vq[i] = ~g0 & ~g1 & gp & vm;  // cq >= q implies present >= q
+        pd[i] = ~(x0 | v1[i] | vq[i]) & vm;
+        uint32_t gt, lt;
+        ctr_cmp(c1, c0, gt, lt);
+        e0[i] = vq[i] & ~lt;
+        e1[i] = vq[i] & ~gt;
+        vq_count += __builtin_popcount(vq[i]);
+        a_pend += __builtin_popcount(pd[i]);
+        asm volatile("" : "+v"(seq0), "+v"(v1[i]), "+v"(vq[i]), "+v"(pd[i]));
+      }
+      uint32_t x[W];
+#pragma unroll
+      for (int i = 0; i < W; i++) x[i] = v1[i] | pd[i];
+      lds_st<W>(pc[0][tid], x);
+      lds_st<W>(pc[1][tid], pd);
+      lds_st<W>(pc[2][tid], e0);
+      lds_st<W>(pc[3][tid], e1);
+      const __amdgpu_buffer_rsrc_t orr = out_rsrc(c);
+      const uint32_t oo = out_off(c);
+      buf_st<W>(orr, oo, 0, x);
+#pragma unroll
+      for (int i = 0; i < W; i++) x[i] = vq[i] | pd[i];
+      buf_st<W>(orr, oo, out_pb, x);
+      buf_st<W>(orr, oo, 3 * out_pb, pd);
+    }
+    lb_eval(lbg);
+    // (2) VQ prefix inside the tile; publish the tile's aggregate; the next ticket
+    const uint32_t incl = wave_incl_scan32(vq_count, lane);
+    if (lane == 63) s_wave[wave] = incl;
+    if (tid == 0) s_bcast[0] = nt;
+    lds_barrier();
+    uint32_t wave_off = 0, total = 0;
+    {
+      const uint32_t sw = lane < WAVES ? s_wave[lane] : 0u;
+      const int wv = __builtin_amdgcn_readfirstlane(wave);
+#pragma unroll
+      for (int w = 0; w < WAVES; w++) {
+        const uint32_t x = __builtin_amdgcn_readlane(sw, w);
+        wave_off += (w < wv) ? x : 0u;
+        total += x;
+      }
+    }
+    const uint32_t nx = s_bcast[0];
+    if (tid == 0) {
+      atomic_store_agent(p.lookback + c, ((unsigned long long)(c == 0 ? tag_inc : tag_agg) << 32) | total);
+      if (nx < p.n_tiles) nt = take_ticket(rec);
+    }
+    // (3) round 2 of tile c in flight behind the parked tile's draws and stores; then
+    //     round 1 of the next tile. The vector memory counter retires in issue order:
+    //     the stores go before the next tile's loads, so the next tally's wait covers
+    //     them and the look-back poll issued after it waits for nothing else.
+    uint32_t r2lo[N][W], r2hi[N][W];
+    buf_ld_planes<N, W>(in_rsrc(c), in_off(c), in_pb, 2 * N, r2lo, r2hi);
+    uint32_t own[W] = {};
+    if (have_park) draw_parked(own);
+    store_parked(own, have_park);
+    const int32_t prev_park = park_tile;
+    park_tile = (int32_t)c;  // the look-back poll of tile c (prev_tile: the tile just finished)
+    lbg = lb_poll();
+    park_tile = prev_park;
+    {  // unconditional: past the last tile every lane reads tile c's first word
+      const bool more = nx < p.n_tiles;
+      buf_ld_planes<N, W>(in_rsrc(more ? nx : c), more ? in_off(nx) : 0u, in_pb, 0, r1lo, r1hi);
+    }
+    // (4) round-2 decisions of tile c for both own votes (engine.rs:540-542, 613-628)
+    {
+      uint32_t x[W], pd[W], e0[W], e1[W];
+      lds_ld<W>(pc[0][tid], x);
+      lds_ld<W>(pc[1][tid], pd);
+      lds_ld<W>(pc[2][tid], e0);
+      lds_ld<W>(pc[3][tid], e1);
+      uint32_t alo[W], ahi[W], blo[W], bhi[W];
+#pragma unroll
+      for (int i = 0; i < W; i++) {
+        r2_decision_ab<N, W>(r2lo, r2hi, i, p.q, p.self_lane, x[i] & ~pd[i], e0[i] | e1[i], pd[i], alo[i], ahi[i],
+                             blo[i], bhi[i]);
+        const uint32_t vm = valid_mask(w0 + i, p.n_words, p.n_slots);
+        alo[i] &= vm; ahi[i] &= vm; blo[i] &= vm; bhi[i] &= vm;
+      }
+      lds_st<W>(pc[4][tid], alo);
+      lds_st<W>(pc[5][tid], ahi);
+      lds_st<W>(pc[6][tid], blo);
+      lds_st<W>(pc[7][tid], bhi);
+    }
+    a_draws += vq_count;
+    park_tile = (int32_t)c;
+    park_total = total;
+    park_thr = wave_off + incl - vq_count;
+    pk ^= 1u;
+    c = nx;
+  }
+  if (park_tile >= 0) {  // the last parked tile (its poll went out in the last iteration)
+    lb_eval(lbg);
+    lds_barrier();
+    uint32_t own[W];
+    draw_parked(own);
+    store_parked(own, true);
+  }
+
+  // ---- per-workgroup record; the last workgroup to arrive folds them all
+  {
+    __shared__ unsigned long long red[WAVES][4];
+    __shared__ uint32_t s_last;
+    const unsigned long long s0 = wave_sum64((unsigned long long)a_dec | ((unsigned long long)a_v1 << 32));
+    const unsigned long long s1 = wave_sum64((unsigned long long)a_pend | ((unsigned long long)a_draws << 32));
+    const uint32_t mx = wave_max32(a_max1), mn = wave_min32(a_min);
+    if (lane == 0) { red[wave][0] = s0; red[wave][1] = s1; red[wave][2] = mx; red[wave][3] = mn; }
+    lds_barrier();
+    if (tid == 0) {
+      unsigned long long t[kLagStatGranules] = {0, 0, 0, 0, 0, 0xFFFFFFFFull};
+#pragma unroll 1
+      for (int w = 0; w < WAVES; w++) {
+        t[0] += red[w][0] & 0xFFFFFFFFull; t[1] += red[w][0] >> 32;
+        t[2] += red[w][1] & 0xFFFFFFFFull; t[3] += red[w][1] >> 32;
+        t[4] = red[w][2] > t[4] ? red[w][2] : t[4];
+        t[5] = red[w][3] < t[5] ? red[w][3] : t[5];
+      }
+      const unsigned long long tag = stat_tag(p.seq);
+      unsigned long long* gr = p.stats + (uint64_t)blockIdx.x * kLagStatGranules;
+#pragma unroll
+      for (int k = 0; k < kLagStatGranules; k++) atomic_store_agent(gr + k, tag | t[k]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned long long arrived = atomicAdd(&rec->done.v, 1ull);
+      s_last = arrived == gridDim.x - 1 ? 1u : 0u;
+    }
+    lds_barrier();
+    if (!s_last) return;
+  }
+  unsigned long long v[7] = {0, 0, 0, 0, 0, ~0ull, 0};  // dec v1 pend draws max(id+1) min(id) fault
+  constexpr unsigned long long kTagMask = ~0ull << 51;
+  const unsigned long long tag = stat_tag(p.seq);
+  for (uint32_t g = tid; g < gridDim.x; g += BLOCK) {
+    const unsigned long long* gr = p.stats + (uint64_t)g * kLagStatGranules;
+    unsigned long long x[kLagStatGranules];
+#pragma unroll
+    for (int k = 0; k < kLagStatGranules; k++) x[k] = atomic_load_agent(const_cast<unsigned long long*>(gr) + k);
+    uint32_t spins = 0;
+    for (;;) {  // visible already (arrival counter): a guard, not a wait
+      bool ok = true;
+#pragma unroll
+      for (int k = 0; k < kLagStatGranules; k++) ok &= (x[k] & kTagMask) == tag;
+      if (ok) break;
+      if (++spins > kSpinLimit) { v[6] = 2; break; }
+      __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+      for (int k = 0; k < kLagStatGranules; k++) x[k] = atomic_load_agent(const_cast<unsigned long long*>(gr) + k);
+    }
+#pragma unroll
+    for (int k = 0; k < kLagStatGranules; k++) x[k] &= ~kTagMask;
+    v[0] += x[0]; v[1] += x[1]; v[2] += x[2]; v[3] += x[3];
+    if (x[4] && p.slot_base + x[4] > v[4]) v[4] = p.slot_base + x[4];
+    if (x[5] != 0xFFFFFFFFull && p.slot_base + x[5] < v[5]) v[5] = p.slot_base + x[5];
+  }
+  block_reduce_totals<BLOCK>(v, lane, wave);
+  if (tid != 0) return;
+  Record* nxt = p.rec + ((p.seq + 1) & 1u);  // the next launch's record (the previous launch completed)
+  atomic_store_agent(&nxt->error.v, 0ull);
+  atomic_store_agent(&nxt->ticket.v, 0ull);
+  atomic_store_agent(&nxt->done.v, 0ull);
+  step_commit<SHARD ? kFinShard : kFinRef>(p, rec, v);
 }
 
 // ============================================================================

@@ -10,7 +10,8 @@ namespace {
 template <int N>
 void launch_n(int block, int words, uint32_t grid, hipStream_t s, const StepParams& p) {
   constexpr int WM = N <= 5 ? 4 : (N <= 10 ? 2 : 1);
-  if (block == 512) hipLaunchKernelGGL((ref_step_kernel<N, WM, 512, true, 1>), dim3(grid), dim3(512), 0, s, p);
+  if (block == 0) hipLaunchKernelGGL((ref_lag_kernel<N, (N <= 5 ? 2 : 1), 512, true>), dim3(grid), dim3(512), 0, s, p);
+  else if (block == 512) hipLaunchKernelGGL((ref_step_kernel<N, WM, 512, true, 1>), dim3(grid), dim3(512), 0, s, p);
   else if (block == 256) hipLaunchKernelGGL((ref_step_kernel<N, WM, 256, true, 1>), dim3(grid), dim3(256), 0, s, p);
   else hipLaunchKernelGGL((ref_step_kernel<N, 1, 128, true, 1>), dim3(grid), dim3(128), 0, s, p);
   (void)words;
@@ -21,7 +22,8 @@ const Launch kTable[17] = {nullptr,      &launch_n<1>,  &launch_n<2>,  &launch_n
                            &launch_n<12>, &launch_n<13>, &launch_n<14>, &launch_n<15>, &launch_n<16>};
 }  // namespace
 
-// block/words must be one of the shapes rabia_gpu.hip picks: {512, wmax}, {256, wmax}, {128, 1}.
+// block/words must be one of the shapes rabia_gpu.hip picks: {512, wmax}, {256, wmax}, {128, 1};
+// block 0 = the persistent lag kernel (512 x (n <= 5 ? 2 : 1) tiles by ticket, grid = resident workgroups).
 void launch_ref_shard(int n, int block, int words, uint32_t grid, hipStream_t s, const StepParams& p) {
   kTable[n](block, words, grid, s, p);
 }
