@@ -137,12 +137,13 @@ int rg_get_state(rg_ctx* ctx, rg_engine_state* st);
 /* Phase step over one slot window [slot_base, slot_base + n_slots).
  * `phase` is the WMVC phase number (>= 1; ignored in REF). `max_phase` is
  * EngineState.current_phase for commit_phase's ordering check (state.rs:70-75);
- * 0 disables it. Calls on one context must be stream-ordered, and so must REF
- * steps of different contexts on one device: two look-back launches running at
- * once on one GPU can hold the CUs each other's earlier tiles need (the bounded
- * spin then reports RG_ESTATE).
+ * 0 disables it. Phase steps on one context must be stream-ordered (they share the
+ * context's launch records). Steps of different contexts may run concurrently on
+ * one device: large REF launches take their tiles by ticket, so no launch waits on
+ * a tile another launch keeps off the GPU (the tiled kernel of small
+ * launches relies on dispatch order and is serialised by callers that overlap).
  *  _async: device pointers, enqueued on `stream`; result_dev may be NULL
- *          (then fetch it with rg_last_result).
+ *          (then fetch it with rg_last_result: the last phase step's result).
  *  plain : host pointers; copies in, runs, copies out, synchronises. */
 int rg_phase_step_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev,
                         uint64_t n_slots, uint64_t stride_words, uint64_t slot_base,
@@ -170,7 +171,12 @@ int rg_last_result(rg_ctx* ctx, rg_step_result* out_host);
  *     the context's engine state (last_committed, contiguous watermark, steps),
  *     leaving every rank's state equal to one evaluator's over the whole window.
  * Steps (1) never wait on (2)-(4), so they pipeline: the output buffer of a window
- * must not be reused before its fix-up ran. row_dev / result_dev may be NULL. */
+ * must not be reused before its fix-up ran. Stage (1) may run on one stream while
+ * (3)-(4) of earlier windows run on another: each stage writes only the engine
+ * fields it owns (shard_draws; rng_next; last_committed / watermark / steps) and its
+ * own context-internal scratch. Each stage's calls must be stream-ordered among
+ * themselves, and (3)/(4) of a window after (3)/(4) of the window before it.
+ * row_dev / result_dev may be NULL. */
 int rg_phase_step_shard_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev,
                               uint64_t n_slots, uint64_t stride_words, uint64_t slot_base,
                               uint64_t max_phase, uint64_t* records_dev, uint64_t records_cap,

@@ -52,6 +52,11 @@ struct rg_ctx {
   unsigned long long* cluster_part = nullptr;  // [blocks][kClusterStats]
   unsigned long long* cluster_stats = nullptr;  // [kClusterStats]
   unsigned long long* fix_acc = nullptr;        // sharded REF fix-up accumulator [4]
+  unsigned long long* follow_acc = nullptr;     // follower commit accumulator [4]
+  // results of the shard fix-up / shard commit / follower commit: each stage writes
+  // its own (a fix-up may run on another stream than the next window's step, whose
+  // result is ctx->result, the one rg_last_result reads)
+  DevResult* stage_result = nullptr;            // [3]
   uint32_t n_cu = 256;                          // compute units (persistent lag-kernel grid)
   std::string err;
 };
@@ -310,6 +315,10 @@ int rg_create(rg_ctx** out, const rg_config* cfg) {
   if ((e = hipMalloc(&ctx->rec, 2 * sizeof(Record))) != hipSuccess) return bail(e, "hipMalloc(rec)");
   if ((e = hipMalloc(&ctx->state, sizeof(DevState))) != hipSuccess) return bail(e, "hipMalloc(state)");
   if ((e = hipMalloc(&ctx->result, sizeof(DevResult))) != hipSuccess) return bail(e, "hipMalloc(result)");
+  if ((e = hipMalloc(&ctx->stage_result, 3 * sizeof(DevResult))) != hipSuccess) return bail(e, "hipMalloc(stage_result)");
+  if ((e = hipMalloc(&ctx->fix_acc, 4 * sizeof(unsigned long long))) != hipSuccess) return bail(e, "hipMalloc(fix_acc)");
+  if ((e = hipMalloc(&ctx->follow_acc, 4 * sizeof(unsigned long long))) != hipSuccess)
+    return bail(e, "hipMalloc(follow_acc)");
   Record recs[2] = {fresh_record(), fresh_record()};
   DevState st{0, 0, 1, 0, 0};  // PhaseIds start at 1 (state.rs:59-63)
   DevResult res;
@@ -344,6 +353,8 @@ int rg_destroy(rg_ctx* ctx) {
   (void)hipFree(ctx->cluster_part);
   (void)hipFree(ctx->cluster_stats);
   (void)hipFree(ctx->fix_acc);
+  (void)hipFree(ctx->follow_acc);
+  (void)hipFree(ctx->stage_result);
   (void)hipFree(ctx->d_votes);
   (void)hipFree(ctx->d_out);
   (void)hipFree(ctx->d_user_result);
@@ -504,7 +515,6 @@ int rg_shard_fixup_async(rg_ctx* ctx, uint32_t* out_dev, uint64_t n_slots, uint6
   Layout lout;
   uint64_t need;
   if (int rc = make_layout(ctx, kOutPlanes, n_words, stride_words, &lout, &need, "rg_shard_fixup")) return rc;
-  if (!ctx->fix_acc) RG_HIP(ctx, hipMalloc(&ctx->fix_acc, 4 * sizeof(unsigned long long)));
   hipStream_t s = pick_stream(ctx, stream);
   RG_HIP(ctx, hipMemsetAsync(ctx->fix_acc, 0, 3 * sizeof(unsigned long long), s));
   RG_HIP(ctx, hipMemsetAsync(ctx->fix_acc + 3, 0xFF, sizeof(unsigned long long), s));
@@ -527,7 +537,7 @@ int rg_shard_fixup_async(rg_ctx* ctx, uint32_t* out_dev, uint64_t n_slots, uint6
   const uint64_t g = (blocks_max + 255) / 256;
   const uint32_t grid = (uint32_t)(g < 1024 ? g : 1024);
   hipLaunchKernelGGL(shard_fixup_kernel, dim3(grid), dim3(256), 0, s, f);
-  hipLaunchKernelGGL(shard_fixup_finish_kernel, dim3(1), dim3(64), 0, s, f, ctx->result,
+  hipLaunchKernelGGL(shard_fixup_finish_kernel, dim3(1), dim3(64), 0, s, f, ctx->stage_result + 0,
                      reinterpret_cast<DevResult*>(row_dev));
   RG_HIP(ctx, hipGetLastError());
   return RG_OK;
@@ -544,10 +554,9 @@ int rg_follower_commit_async(rg_ctx* ctx, const uint32_t* out_dev, uint64_t n_sl
   Layout lout;
   uint64_t need;
   if (int rc = make_layout(ctx, kOutPlanes, n_words, stride_words, &lout, &need, "rg_follower_commit")) return rc;
-  if (!ctx->fix_acc) RG_HIP(ctx, hipMalloc(&ctx->fix_acc, 4 * sizeof(unsigned long long)));
   hipStream_t s = pick_stream(ctx, stream);
-  RG_HIP(ctx, hipMemsetAsync(ctx->fix_acc, 0, 3 * sizeof(unsigned long long), s));
-  RG_HIP(ctx, hipMemsetAsync(ctx->fix_acc + 3, 0xFF, sizeof(unsigned long long), s));
+  RG_HIP(ctx, hipMemsetAsync(ctx->follow_acc, 0, 3 * sizeof(unsigned long long), s));
+  RG_HIP(ctx, hipMemsetAsync(ctx->follow_acc + 3, 0xFF, sizeof(unsigned long long), s));
   FollowParams f;
   f.out = out_dev;
   f.lout = lout;
@@ -557,11 +566,11 @@ int rg_follower_commit_async(rg_ctx* ctx, const uint32_t* out_dev, uint64_t n_sl
   f.max_phase = max_phase;
   f.state = ctx->state;
   f.applied = applied_dev;
-  f.acc = ctx->fix_acc;
+  f.acc = ctx->follow_acc;
   const uint64_t g = (n_words + 255) / 256;
   hipLaunchKernelGGL(follower_kernel, dim3((uint32_t)(g < 2048 ? g : 2048)), dim3(256), 0, s, f);
   hipLaunchKernelGGL(follower_finish_kernel, dim3(1), dim3(64), 0, s, f,
-                     reinterpret_cast<unsigned long long*>(gate_dev), ctx->result,
+                     reinterpret_cast<unsigned long long*>(gate_dev), ctx->stage_result + 2,
                      reinterpret_cast<DevResult*>(result_dev));
   RG_HIP(ctx, hipGetLastError());
   return RG_OK;
@@ -574,7 +583,7 @@ int rg_shard_commit_async(rg_ctx* ctx, const rg_step_result* rows_dev, uint32_t 
   RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
   hipLaunchKernelGGL(shard_commit_kernel, dim3(1), dim3(64), 0, pick_stream(ctx, stream),
                      reinterpret_cast<const DevResult*>(rows_dev), n_shards, window_base, window_slots, ctx->state,
-                     ctx->result, reinterpret_cast<DevResult*>(result_dev));
+                     ctx->stage_result + 1, reinterpret_cast<DevResult*>(result_dev));
   RG_HIP(ctx, hipGetLastError());
   return RG_OK;
 }

@@ -1821,11 +1821,10 @@ static __global__ void shard_fixup_finish_kernel(FixParams f, DevResult* row_ctx
   if (f.acc[2] && f.acc[2] - 1 > r.last_committed_max) r.last_committed_max = f.acc[2] - 1;
   if (f.acc[3] < r.first_undecided) r.first_undecided = f.acc[3];
   if (r.n_draws > f.vq_cap) r.flags |= 8ull;  // records did not fit: the patch is incomplete
-  DevState s = *f.state;
-  s.rng_next += total;
-  r.rng_next = s.rng_next;
+  // only rng_next: a later window's shard step (shard_draws) may run on another stream
+  r.rng_next = f.state->rng_next + total;
   r.commit_watermark = 0;
-  *f.state = s;
+  f.state->rng_next = r.rng_next;
   *row_ctx = r;
   if (row_user) *row_user = r;
 }
@@ -1861,10 +1860,9 @@ static __global__ void shard_commit_kernel(const DevResult* rows, uint32_t n_sha
   g.first_undecided = fu;
   g.rng_next = s.rng_next;
   g.commit_watermark = wm;
-  s.last_committed = lc;
-  s.commit_watermark = wm;
-  s.steps += 1;
-  *state = s;
+  state->last_committed = lc;  // the fields it owns (the shard step and fix-up own the others)
+  state->commit_watermark = wm;
+  state->steps = s.steps + 1;
   *res_ctx = g;
   if (res_user) *res_user = g;
 }
@@ -1954,9 +1952,8 @@ static __global__ void follower_finish_kernel(FollowParams f, unsigned long long
   r.rng_next = s.rng_next;
   r.commit_watermark = wm;
   r.flags = 0;
-  s.last_committed = lc;
-  s.commit_watermark = wm;
-  *f.state = s;
+  f.state->last_committed = lc;
+  f.state->commit_watermark = wm;
   *res_ctx = r;
   if (res_user) *res_user = r;
 }
