@@ -118,16 +118,80 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def granted_cpus() -> dict:
+    """The CPUs this process may actually run on: the affinity mask, capped by the
+    cgroup CPU quota (cgroup v2 cpu.max, v1 cfs_quota/period) when one is set."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            with open(path) as f:
+                q, per = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+        except (OSError, ValueError):
+            pass
+    if quota is None:
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                per = int(f.read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    granted = aff if quota is None else max(1, min(aff, int(quota)))
+    return {"granted": granted, "affinity": aff, "cgroup_quota": quota, "host_cpus": os.cpu_count()}
+
+
 def cpu_threads(a) -> int:
     if a.cpu_threads > 0:
         return a.cpu_threads
-    env = os.environ.get("OMP_NUM_THREADS")
-    if env and env.isdigit() and int(env) > 0:
-        return int(env)
-    return max(1, min(os.cpu_count() or 1, 16))
+    return granted_cpus()["granted"]
 
 
-def cpu_baseline(a, n: int, ev: PhaseEvaluator, stream) -> dict:
+def cpu_baseline_c3(a, gpu_info) -> dict:
+    """C3 CPU baseline: the C cluster restatement (oracle/rabia_oracle.c:or_wmvc_cluster,
+    one replica set per slot, phases to termination) on all granted cores, one
+    contiguous slot range per thread (ctypes drops the GIL), on the first slots of the
+    GPU's own trace; checked against the GPU's per-slot info words."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    th = cpu_threads(a)
+    n, S = 5, min(1 << 22, a.c3_slots)
+    q, fp1 = n // 2 + 1, (n - 1) // 2 + 1
+    states = O.cluster_trace(n, SEED, 1, S)
+    chunks = np.array_split(np.arange(S), th)
+    outs = [None] * th
+
+    def run(i):
+        lo, hi = int(chunks[i][0]), int(chunks[i][-1]) + 1
+        outs[i] = O.wmvc_cluster(n, q, fp1, SEED, 1, 99, 32, 1 + lo, states[lo:hi])
+
+    ts = [threading.Thread(target=run, args=(i,)) for i in range(th) if len(chunks[i])]
+    t0 = time.perf_counter()
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    dt = time.perf_counter() - t0
+    info = np.concatenate([o for o in outs if o is not None])
+    decided = int(((info & 0xFF) != 3).sum())  # dec code 3 (none) = not all replicas decided
+    agree = bool(np.array_equal(info, gpu_info[:S]))
+    g = granted_cpus()
+    return {"value": decided / dt, "unit": "slots decided/s", "cores": th, "kind": "port",
+            "cpu_model": cpu_model(), "host_cpus": g["host_cpus"], "granted_cpus": g["granted"],
+            "affinity_cpus": g["affinity"], "cgroup_quota_cpus": g["cgroup_quota"],
+            "sample": f"C cluster restatement (oracle/rabia_oracle.c:or_wmvc_cluster), {th} threads over the "
+                      f"first {S} slots of the GPU's adversarial trace (n=5, <= 32 phases): {dt:.3f} s; "
+                      f"per-slot info words equal the GPU's: {agree}"}
+
+
+def cpu_baseline(a, n: int, ev: PhaseEvaluator, stream, windows: int = 256) -> dict:
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
     th = cpu_threads(a)
@@ -156,7 +220,7 @@ def cpu_baseline(a, n: int, ev: PhaseEvaluator, stream) -> dict:
     dtp = time.perf_counter() - t0
     sfp = sum(x[0] for x in out) / dtp
     # (3) SoA all cores on the GPU's own planar planes (same trace kind/seed)
-    S3 = 256 * WINDOW  # the GPU step's size: 704 MB of planes, past the host's L3
+    S3 = windows * WINDOW  # 256 windows at n=5: 704 MB of planes, past the host's L3
     stride = ((S3 + 127) // 128) * 4
     planar = PhaseEvaluator(n, self_lane=lane, seed=SEED, tile_words=0)
     votes = torch.empty((4 * n + 1) * stride, dtype=torch.int32, device="cuda")
@@ -179,10 +243,12 @@ def cpu_baseline(a, n: int, ev: PhaseEvaluator, stream) -> dict:
     soa = sres["n_decided"] / dt3
     # the CPU fast path and the GPU agree on the same planes (decided count, draws)
     agree = int(gpu_res[1]) == sres["n_decided"] and int(gpu_res[4]) == sres["n_draws"]
+    g = granted_cpus()
     return {"value": soa, "unit": "slots decided/s", "cores": th, "kind": "port",
-            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+            "cpu_model": cpu_model(), "host_cpus": g["host_cpus"], "granted_cpus": g["granted"],
+            "affinity_cpus": g["affinity"], "cgroup_quota_cpus": g["cgroup_quota"],
             "sample": f"SoA all-core path (oracle/rabia_cpu_soa.c, {th} OpenMP threads) over {S3} slots "
-                      f"(256 x 2^20, agree90, n={n}, the GPU's planar planes), median of 5 = {dt3:.3f} s; "
+                      f"({windows} x 2^20, agree90, n={n}, the GPU's planar planes), median of 5 = {dt3:.3f} s; "
                       f"agrees with the GPU step on decided/draws: {agree}",
             "structure_faithful_1t": {"value": sf1, "slots": S1, "seconds": dt1},
             "structure_faithful_per_core": {"value": sfp, "instances": th, "slots_each": S1, "seconds": dtp},
@@ -466,7 +532,8 @@ def run_c3(a, world, rank, dist):
         total_ms, kern_ms = float(tm[0]), float(tm[1])
     last = shard.combine_cluster(rows[n_total - 1].tolist())
     return {"total_ms": total_ms, "kern_ms": kern_ms, "decided": decided, "ev": ev, "S": S, "total": total,
-            "mean_phases": last["sum_phases"] / max(last["all_decided"], 1), "max_phases": last["max_phases"]}
+            "mean_phases": last["sum_phases"] / max(last["all_decided"], 1), "max_phases": last["max_phases"],
+            "info": info}
 
 
 def main():
@@ -506,7 +573,9 @@ def main():
                            "mean_phases": r["mean_phases"], "max_phases": r["max_phases"],
                            "parallelism": f"slot-shard x{world}, stats + decided bitmaps all-gathered"},
                 "roofline": c3_roofline(r, bytes_slot),
-                "cpu_baseline": None, "sweep_1m_us": None,
+                "cpu_baseline": (None if (a.no_cpu_baseline or world > 1)
+                                 else cpu_baseline_c3(a, r["info"].cpu().numpy().view(np.uint32))),
+                "sweep_1m_us": None,
             }
             print(json.dumps(line), flush=True)
         r["ev"].close()
@@ -528,8 +597,8 @@ def main():
         value = r["decided"] / (r["total_ms"] / 1000.0)
         alg_bytes = S * bytes_per_slot_ref(n)
         achieved = alg_bytes / (r["kern_ms"] / 1000.0) / 1e9
-        cpu = None if (a.no_cpu_baseline or world > 1 or a.config != "c2") else cpu_baseline(a, n, r["ev"],
-                                                                                              r["stream"])
+        cpu = None if (a.no_cpu_baseline or world > 1) else cpu_baseline(
+            a, n, r["ev"], r["stream"], windows=256 if a.config == "c2" else a.c5_windows)
         par = f"slot-shard x{world}" + (", one engine: sharded draws + fix-up" if world > 1 else "")
         if a.config == "c5":
             metric = "consensus slots decided/sec (9 replicas, 2^26 slots per step, bitmap all-gather)"

@@ -138,10 +138,12 @@ int rg_get_state(rg_ctx* ctx, rg_engine_state* st);
  * `phase` is the WMVC phase number (>= 1; ignored in REF). `max_phase` is
  * EngineState.current_phase for commit_phase's ordering check (state.rs:70-75);
  * 0 disables it. Phase steps on one context must be stream-ordered (they share the
- * context's launch records). Steps of different contexts may run concurrently on
- * one device: large REF launches take their tiles by ticket, so no launch waits on
- * a tile another launch keeps off the GPU (the tiled kernel of small
- * launches relies on dispatch order and is serialised by callers that overlap).
+ * context's launch records). Steps of different contexts may be issued on
+ * concurrent streams of one device: large REF launches take their tiles by ticket,
+ * so no launch waits on a tile another launch keeps off the GPU; the tiled kernels
+ * of smaller launches rely on dispatch order, so while several contexts live on a
+ * device the library chains those launches behind each other (one event per device;
+ * DESIGN.md §4). Processes sharing one GPU must order such launches themselves.
  *  _async: device pointers, enqueued on `stream`; result_dev may be NULL
  *          (then fetch it with rg_last_result: the last phase step's result).
  *  plain : host pointers; copies in, runs, copies out, synchronises. */

@@ -11,13 +11,12 @@ extern "C" {
 #endif
 /* diag bits: 1 skip the look-back wait (wrong draws), 2 skip per-tile statistics
  * and the step result, 4 record per-tile s_memrealtime stamps (100 MHz);
- * bits 8-10: 0 = automatic tile shape, 1 big (512 x W), 2 mid (256 x W), 3 small (128 x 1),
- *            4 big (512 x 2), 5 mid (256 x 2) (REF, n = 5 only);
- * bits 16-18 (REF, n = 5): 1 the round-1 tiled kernel (both rounds' planes live
- * across the look-back), 2 the tiled kernel at 6 waves per SIMD;
+ * bits 8-10: tiled kernel shape, 0 = automatic, 1 big (512 x W), 2 mid (256 x W), 3 small (128 x 1);
  * bit 20: large REF launches keep the tiled kernel instead of the persistent lag kernel;
- * bit 21: the lag kernel at any launch size; bits 24-31: lag-kernel grid (0 = two
- * workgroups per CU). */
+ * bit 21: the lag kernel at any launch size;
+ * bit 22: the lag kernel as two 512-thread workgroups per CU (the shape of launches of < 2
+ *         1024-thread tiles per CU; A/B on large ones);
+ * bits 24-31: lag-kernel grid (0 = one workgroup per CU, two in the 512-thread shape). */
 int rg_debug_set(rg_ctx* ctx, uint32_t diag);
 int rg_debug_stamps(rg_ctx* ctx, uint64_t* host_out, uint64_t n_words);
 /* REF kernel memory pattern (20 in-planes, 8 out-planes, 16 B/lane) without protocol.

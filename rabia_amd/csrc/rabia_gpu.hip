@@ -11,6 +11,7 @@
 
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <string>
 
@@ -58,12 +59,29 @@ struct rg_ctx {
   // result is ctx->result, the one rg_last_result reads)
   DevResult* stage_result = nullptr;            // [3]
   uint32_t n_cu = 256;                          // compute units (persistent lag-kernel grid)
+  bool chained = false;                         // counted in g_chain[device].live
   std::string err;
 };
 
 namespace {
 
 thread_local std::string g_err;  // errors before a context exists
+
+// Look-back launches of the tiled kernels (ref_step_kernel, wmvc_step_kernel) rely on
+// dispatch order for forward progress, so two of them running at once on one GPU can
+// wait on each other across kernels. While more than one context lives
+// on a device, every such launch is chained behind the device's previous one through
+// one event (a stream wait when the previous launch came from another context or
+// stream). Large REF launches run the ticketed lag kernel and need no chain.
+struct DevChain {
+  std::mutex mu;
+  int live = 0;                  // contexts on the device
+  hipEvent_t ev = nullptr;       // after the device's last chained launch
+  const rg_ctx* owner = nullptr;
+  hipStream_t stream = nullptr;
+};
+constexpr int kMaxDevices = 64;
+DevChain g_chain[kMaxDevices];
 
 int fail(rg_ctx* ctx, int code, const std::string& msg) {
   if (ctx) ctx->err = msg;
@@ -83,21 +101,18 @@ int hip_fail(rg_ctx* ctx, hipError_t e, const char* what) {
   } while (0)
 
 constexpr int wmax_for(int n) { return n <= 5 ? 4 : (n <= 10 ? 2 : 1); }
-// persistent lag kernel: 512-thread workgroups, two per CU, lag_words(n) words per thread
-constexpr int kLagBlock = 512;
+// persistent lag kernel: one 1024-thread workgroup per CU (launches of >= 2 tiles per
+// CU), else two 512-thread workgroups per CU; lag_words(n) words per thread
+constexpr int kLagBlock = 1024, kLagBlockSmall = 512;
 constexpr int lag_words(int n) { return n <= 5 ? 2 : 1; }
 
-// Tile shapes: {threads, words per thread}. Big tiles keep the per-launch count
-// of tiles and look-back hand-offs low on large windows; small tiles fill
-// the 256 CUs on single 2^20-slot windows.
-enum TileCfg { kCfgBig = 0, kCfgMid = 1, kCfgSmall = 2, kCfgBigW2 = 3, kCfgMidW2 = 4, kCfgLegacyBig = 5,
-               kCfgDefBig6 = 6 };
-constexpr int cfg_block(int c) {
-  return (c == kCfgBig || c == kCfgBigW2 || c == kCfgLegacyBig || c == kCfgDefBig6) ? 512 : (c == kCfgSmall ? 128 : 256);
-}
-inline int cfg_words(int c, int n) {
-  return c == kCfgSmall ? 1 : (c >= kCfgLegacyBig ? 4 : (c >= kCfgBigW2 ? 2 : wmax_for(n)));
-}
+// Tile shapes of the tiled kernel: {threads, words per thread}. Big tiles keep the
+// per-launch count of tiles and look-back hand-offs low on large windows; small
+// tiles fill the 256 CUs on single 2^20-slot windows. (Large REF launches run the
+// persistent lag kernel instead.)
+enum TileCfg { kCfgBig = 0, kCfgMid = 1, kCfgSmall = 2 };
+constexpr int cfg_block(int c) { return c == kCfgBig ? 512 : (c == kCfgSmall ? 128 : 256); }
+inline int cfg_words(int c, int n) { return c == kCfgSmall ? 1 : wmax_for(n); }
 
 int pick_cfg(int n, uint64_t n_words) {
   const uint64_t wm = (uint64_t)wmax_for(n);
@@ -112,33 +127,19 @@ template <int N>
 struct Disp {
   static constexpr int WM = wmax_for(N);
   static void ref(int c, uint32_t grid, hipStream_t s, const StepParams& p) {
-    if constexpr (N == 5) {  // diagnostic shapes (rg_debug_set force 4, 5): 2 words per thread
-      if (c == kCfgBigW2) {
-        hipLaunchKernelGGL((ref_step_kernel<N, 2, 512, false>), dim3(grid), dim3(512), 0, s, p);
-        return;
-      }
-      if (c == kCfgMidW2) {
-        hipLaunchKernelGGL((ref_step_kernel<N, 2, 256, false>), dim3(grid), dim3(256), 0, s, p);
-        return;
-      }
-    }
-    if constexpr (N == 5) {  // A/B shapes (rg_debug_set bits 16-18)
-      if (c == kCfgLegacyBig) {  // round-1 kernel: both rounds' planes live across the look-back
-        hipLaunchKernelGGL((ref_step_kernel<N, 4, 512, false, 0, 4>), dim3(grid), dim3(512), 0, s, p);
-        return;
-      }
-      if (c == kCfgDefBig6) {  // 6 waves per SIMD (a few spills)
-        hipLaunchKernelGGL((ref_step_kernel<N, 4, 512, false, 1, 6>), dim3(grid), dim3(512), 0, s, p);
-        return;
-      }
-    }
-    if (c == kCfgBig) hipLaunchKernelGGL((ref_step_kernel<N, WM, 512, false, 1>), dim3(grid), dim3(512), 0, s, p);
-    else if (c == kCfgMid) hipLaunchKernelGGL((ref_step_kernel<N, WM, 256, false, 1>), dim3(grid), dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((ref_step_kernel<N, 1, 128, false, 1>), dim3(grid), dim3(128), 0, s, p);
+    if (c == kCfgBig) hipLaunchKernelGGL((ref_step_kernel<N, WM, 512, false>), dim3(grid), dim3(512), 0, s, p);
+    else if (c == kCfgMid) hipLaunchKernelGGL((ref_step_kernel<N, WM, 256, false>), dim3(grid), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((ref_step_kernel<N, 1, 128, false>), dim3(grid), dim3(128), 0, s, p);
   }
   // persistent lag kernel (large launches): grid = resident workgroups, tiles by ticket
-  static void ref_lag(uint32_t grid, hipStream_t s, const StepParams& p) {
-    hipLaunchKernelGGL((ref_lag_kernel<N, lag_words(N), kLagBlock, false>), dim3(grid), dim3(kLagBlock), 0, s, p);
+  static void ref_lag(uint32_t grid, hipStream_t s, const StepParams& p) {  // n <= 10 (step_impl)
+    if constexpr (N <= 10)
+      hipLaunchKernelGGL((ref_lag_kernel<N, lag_words(N), kLagBlock, false>), dim3(grid), dim3(kLagBlock), 0, s, p);
+  }
+  static void ref_lag512(uint32_t grid, hipStream_t s, const StepParams& p) {
+    if constexpr (N <= 10)
+      hipLaunchKernelGGL((ref_lag_kernel<N, lag_words(N), kLagBlockSmall, false>), dim3(grid), dim3(kLagBlockSmall),
+                         0, s, p);
   }
   static void wmvc(int c, uint32_t grid, hipStream_t s, const StepParams& p) {
     if (c == kCfgBig) hipLaunchKernelGGL((wmvc_step_kernel<N, WM, 512>), dim3(grid), dim3(512), 0, s, p);
@@ -152,12 +153,6 @@ struct Disp {
     else
       hipLaunchKernelGGL((digest_kernel<N, false>), dim3(grid), dim3(kBlock), 0, s, dg, ds, out, n, q);
   }
-  static void cluster(uint32_t grid, hipStream_t s, const uint32_t* st, uint64_t stride, uint64_t n_slots,
-                      uint64_t base, uint32_t q, uint32_t fp1, Key key, uint64_t cs, uint64_t dseed,
-                      uint32_t maxp, uint32_t* info, unsigned long long* part) {
-    hipLaunchKernelGGL((wmvc_cluster_kernel<N>), dim3(grid), dim3(256), 0, s, st, stride, n_slots, base, q, fp1,
-                       key, cs, dseed, maxp, info, part);
-  }
   static void cluster_lc(uint32_t grid, hipStream_t s, const uint32_t* st, uint64_t stride, uint64_t n_slots,
                          uint64_t base, uint32_t q, uint32_t fp1, Key key, uint64_t cs, uint64_t dseed,
                          uint32_t maxp, uint32_t* info, unsigned long long* part, const uint32_t* coins,
@@ -166,9 +161,6 @@ struct Disp {
                        key, cs, dseed, maxp, info, part, coins, coin_phases, chunk);
   }
 };
-
-using ClusterLaunch = void (*)(uint32_t, hipStream_t, const uint32_t*, uint64_t, uint64_t, uint64_t, uint32_t,
-                               uint32_t, Key, uint64_t, uint64_t, uint32_t, uint32_t*, unsigned long long*);
 
 using DigestLaunch = void (*)(uint32_t, hipStream_t, const uint64_t*, uint64_t, uint32_t*, uint64_t,
                               uint32_t);
@@ -181,9 +173,9 @@ using DigestLaunch = void (*)(uint32_t, hipStream_t, const uint64_t*, uint64_t, 
 const StepLaunch kRefLaunch[17] = RG_TABLE(ref);
 using LagLaunch = void (*)(uint32_t, hipStream_t, const StepParams&);
 const LagLaunch kRefLagLaunch[17] = RG_TABLE(ref_lag);
+const LagLaunch kRefLag512Launch[17] = RG_TABLE(ref_lag512);
 const StepLaunch kWmvcLaunch[17] = RG_TABLE(wmvc);
 const DigestLaunch kDigestLaunch[17] = RG_TABLE(digest);
-const ClusterLaunch kClusterLaunch[17] = RG_TABLE(cluster);
 using ClusterLcLaunch = void (*)(uint32_t, hipStream_t, const uint32_t*, uint64_t, uint64_t, uint64_t, uint32_t,
                                  uint32_t, Key, uint64_t, uint64_t, uint32_t, uint32_t*, unsigned long long*,
                                  const uint32_t*, uint32_t, uint64_t);
@@ -312,6 +304,14 @@ int rg_create(rg_ctx** out, const rg_config* cfg) {
   if ((e = hipSetDevice(cfg->device)) != hipSuccess) return bail(e, "hipSetDevice");
   if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamDefault)) != hipSuccess)
     return bail(e, "hipStreamCreate");
+  if (cfg->device < kMaxDevices) {
+    DevChain& dc = g_chain[cfg->device];
+    std::lock_guard<std::mutex> lk(dc.mu);
+    if (!dc.ev && (e = hipEventCreateWithFlags(&dc.ev, hipEventDisableTiming)) != hipSuccess)
+      return bail(e, "hipEventCreate(chain)");
+    dc.live++;
+    ctx->chained = true;
+  }
   if ((e = hipMalloc(&ctx->rec, 2 * sizeof(Record))) != hipSuccess) return bail(e, "hipMalloc(rec)");
   if ((e = hipMalloc(&ctx->state, sizeof(DevState))) != hipSuccess) return bail(e, "hipMalloc(state)");
   if ((e = hipMalloc(&ctx->result, sizeof(DevResult))) != hipSuccess) return bail(e, "hipMalloc(result)");
@@ -340,6 +340,12 @@ int rg_destroy(rg_ctx* ctx) {
   if (!ctx) return RG_OK;
   (void)hipSetDevice(ctx->cfg.device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->chained) {
+    DevChain& dc = g_chain[ctx->cfg.device];
+    std::lock_guard<std::mutex> lk(dc.mu);
+    dc.live--;
+    if (dc.owner == ctx) dc.owner = nullptr;  // (its launches are complete: the caller synchronised)
+  }
   (void)hipFree(ctx->rec);
   (void)hipFree(ctx->state);
   (void)hipFree(ctx->result);
@@ -415,24 +421,28 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
   uint64_t need_in, need_out;
   if (int rc = make_layout(ctx, 4 * n + 1, n_words, stride_words, &lin, &need_in, "rg_phase_step")) return rc;
   if (int rc = make_layout(ctx, kOutPlanes, n_words, stride_words, &lout, &need_out, "rg_phase_step")) return rc;
-  uint32_t force = (ctx->diag >> 8) & 7u;  // diagnostics: force a tile shape
-  if ((force == 4 || force == 5) && (n != 5 || wmvc || shard)) force = 0;
-  if (force > 5) force = 0;
-  const uint32_t dforce = (ctx->diag >> 16) & 7u;  // diagnostics: A/B shapes (REF, n = 5)
-  if (dforce && (dforce > 2 || n != 5 || wmvc || shard)) return fail(ctx, RG_EINVAL, "rg_debug_set: bad shape");
-  int cfg = dforce ? kCfgLegacyBig + (int)dforce - 1 : force ? (int)force - 1 : pick_cfg(n, n_words);
-  // Large REF launches run the persistent lag kernel (512 x lag_words tiles, taken by
-  // ticket): two resident workgroups per CU. diag bit 20 keeps the tiled kernel
-  // (A/B), bit 21 forces the lag kernel at any size.
-  const bool lag_ok = !wmvc && cfg == kCfgBig && !dforce && !force && !(ctx->diag & 0x7u);
+  uint32_t force = (ctx->diag >> 8) & 7u;  // diagnostics: force a tile shape of the tiled kernel
+  if (force > 3) force = 0;
+  int cfg = force ? (int)force - 1 : pick_cfg(n, n_words);
+  // Large REF launches run the persistent lag kernel (tiles taken by ticket): one
+  // 1024-thread workgroup per CU when the launch gives every CU >= 2 such tiles, else
+  // two 512-thread workgroups per CU. diag bit 20 keeps the tiled kernel (A/B), bit 21
+  // forces the lag kernel at any size, bit 22 forces the 512-thread shape.
+  const bool lag_ok = !wmvc && cfg == kCfgBig && !force && !(ctx->diag & 0x3u);  // (diag 4: stamps, both kernels)
   // (its buffer offsets are 31-bit: every plane of a tile within 2 GiB of the tile base)
   const bool lag_fits = (uint64_t)(4 * n + 1) * lin.pstride * 4 + 4096 < (1ull << 31) &&
                         (uint64_t)kOutPlanes * lout.pstride * 4 + 4096 < (1ull << 31);
-  const bool lag = lag_fits && ((ctx->diag & 0x200000u) ? !wmvc : (lag_ok && !(ctx->diag & 0x100000u)));
-  uint64_t tile_words = lag ? (uint64_t)kLagBlock * lag_words(n) : (uint64_t)cfg_block(cfg) * cfg_words(cfg, n);
+  // n <= 10: the lag kernel's planes fit its registers without spills; above that the
+  // tiled kernel runs (no configuration of SURVEY.md §8 has n > 9)
+  const bool lag = lag_fits && n <= 10 &&
+                   ((ctx->diag & 0x200000u) ? !wmvc : (lag_ok && !(ctx->diag & 0x100000u)));
+  const bool lag1024 = lag && !(ctx->diag & 0x400000u) &&
+                       n_words >= 2ull * ctx->n_cu * kLagBlock * (uint64_t)lag_words(n);
+  const uint64_t lag_block = lag1024 ? kLagBlock : kLagBlockSmall;
+  uint64_t tile_words = lag ? lag_block * lag_words(n) : (uint64_t)cfg_block(cfg) * cfg_words(cfg, n);
   uint64_t n_tiles = (n_words + tile_words - 1) / tile_words;
   const uint32_t grid_force = (ctx->diag >> 24) & 0xFFu;  // diagnostics: lag-kernel grid (tests: many tiles per WG)
-  const uint64_t lag_grid_max = grid_force ? grid_force : 2ull * ctx->n_cu;
+  const uint64_t lag_grid_max = grid_force ? grid_force : (lag1024 ? 1ull : 2ull) * ctx->n_cu;
   const uint32_t lag_grid = (uint32_t)(n_tiles < lag_grid_max ? n_tiles : lag_grid_max);
   const uint64_t gran_tiles = lag ? (n_tiles > 3ull * lag_grid ? n_tiles : 3ull * lag_grid) : n_tiles;
   if (int rc = ensure_tiles(ctx, gran_tiles, false)) return rc;
@@ -467,24 +477,42 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
   p.n_tiles = (uint32_t)n_tiles;
   p.diag = ctx->diag & 0xffu;
   p.dbg = nullptr;
+  p.in_bytes = need_in * 4;
+  p.out_bytes = need_out * 4;
   p.vq_rec = reinterpret_cast<unsigned long long*>(records_dev);
   p.vq_cap = records_cap;
-  if (ctx->diag & 4u) {
-    if (ctx->dbg_cap < n_tiles * 8) {
+  if (ctx->diag & 4u) {  // stamps: [n_tiles][8] (tiled kernel) or [grid][12] (lag kernel)
+    const uint64_t words = lag && 12ull * lag_grid > 8 * n_tiles ? 12ull * lag_grid : 8 * n_tiles;
+    if (ctx->dbg_cap < words) {
       RG_HIP(ctx, hipDeviceSynchronize());
       (void)hipFree(ctx->dbg);
       ctx->dbg = nullptr;
-      RG_HIP(ctx, hipMalloc(&ctx->dbg, n_tiles * 8 * 8));
-      ctx->dbg_cap = n_tiles * 8;
+      RG_HIP(ctx, hipMalloc(&ctx->dbg, words * 8));
+      ctx->dbg_cap = words;
     }
-    RG_HIP(ctx, hipMemsetAsync(ctx->dbg, 0, n_tiles * 8 * 8, pick_stream(ctx, stream)));
+    RG_HIP(ctx, hipMemsetAsync(ctx->dbg, 0, words * 8, pick_stream(ctx, stream)));
     p.dbg = ctx->dbg;
   }
   hipStream_t s = pick_stream(ctx, stream);
-  if (shard) launch_ref_shard(n, lag ? 0 : cfg_block(cfg), cfg_words(cfg, n), lag ? lag_grid : (uint32_t)n_tiles, s, p);
-  else if (lag) kRefLagLaunch[n](lag_grid, s, p);
+  std::unique_lock<std::mutex> chain_lk;
+  DevChain* dc = (!lag && ctx->chained) ? &g_chain[ctx->cfg.device] : nullptr;
+  if (dc) {
+    chain_lk = std::unique_lock<std::mutex>(dc->mu);
+    if (dc->live < 2) dc = nullptr;
+    else if (dc->owner && (dc->owner != ctx || dc->stream != s)) RG_HIP(ctx, hipStreamWaitEvent(s, dc->ev, 0));
+  }
+  if (shard)
+    launch_ref_shard(n, lag ? (lag1024 ? -1 : 0) : cfg_block(cfg), cfg_words(cfg, n),
+                     lag ? lag_grid : (uint32_t)n_tiles, s, p);
+  else if (lag1024) kRefLagLaunch[n](lag_grid, s, p);
+  else if (lag) kRefLag512Launch[n](lag_grid, s, p);
   else (wmvc ? kWmvcLaunch : kRefLaunch)[n](cfg, (uint32_t)n_tiles, s, p);
   RG_HIP(ctx, hipGetLastError());
+  if (dc) {
+    RG_HIP(ctx, hipEventRecord(dc->ev, s));
+    dc->owner = ctx;
+    dc->stream = s;
+  }
   return RG_OK;
 }
 

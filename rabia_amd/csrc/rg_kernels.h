@@ -51,6 +51,7 @@ struct StepParams {
   uint32_t diag;                  // diagnostic build switches (0 in production):
                                   //  1 skip the look-back wait, 2 skip finish_tile, 4 stamps
   unsigned long long* dbg;        // [n_tiles][8] s_memrealtime stamps when diag & 4
+  uint64_t in_bytes, out_bytes;   // the plane buffers' extents (RG_LAG_CHECK builds check every access)
   unsigned long long* vq_rec;     // sharded REF: draw records [vq_cap] (rg_common.h)
   uint64_t vq_cap;
 };
@@ -269,11 +270,7 @@ __device__ __forceinline__ uint32_t lookback_exclusive(unsigned long long* statu
         }
         break;
       }
-#ifdef RG_LB_SLEEP  // build-time experiment: longer back-off between polls
-      for (int z = 0; z < RG_LB_SLEEP; z++) __builtin_amdgcn_s_sleep(1);
-#else
       __builtin_amdgcn_s_sleep(1);
-#endif
       continue;
     }
     const uint32_t v = (lane <= first) ? (uint32_t)g : 0u;
@@ -289,7 +286,7 @@ __device__ __forceinline__ uint32_t lookback_exclusive(unsigned long long* statu
 // Look-back polling K x 64 predecessor granules per round trip (lane l loads the
 // granules at distance 64k + l + 1, k < K, all in flight at once). kfirst = K of
 // the first poll, knext = K of the later ones; sleep = s_sleep between spins.
-// (Diagnostic variants of lookback_exclusive, selected by StepParams.diag bits 12-14.)
+// Used by the first-generation tiles of launches of <= 1024 tiles (ref_step_kernel).
 template <int KMAX>
 __device__ __forceinline__ uint32_t lookback_exclusive_wide(unsigned long long* status, uint32_t tile, uint32_t seq,
                                                             uint32_t agg, int lane, unsigned long long* err,
@@ -623,25 +620,6 @@ __device__ __forceinline__ TileStats thread_stats(const uint32_t (&committed)[W]
 // Occupancy: 4 waves per SIMD (<= 128 VGPRs) so that at least two 512-thread or
 // four 256-thread tiles are resident per CU and one tile's look-back / stores
 // overlap another's loads.
-template <int N, int W>
-__device__ __forceinline__ void load_planes(const StepParams& p, uint64_t w0, bool active, int first_plane,
-                                            uint32_t (&lo)[N][W], uint32_t (&hi)[N][W]) {
-  if (active) {
-    const uint32_t* base = p.votes + p.lin.base(w0);
-    const uint64_t ps = p.lin.pstride;
-#pragma unroll
-    for (int j = 0; j < N; j++) {
-      load_words<W>(base + (first_plane + 2 * j) * ps, lo[j]);
-      load_words<W>(base + (first_plane + 2 * j + 1) * ps, hi[j]);
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < N; j++)
-#pragma unroll
-      for (int i = 0; i < W; i++) lo[j][i] = hi[j][i] = ~0u;
-  }
-}
-
 // Plane loads without a branch: a thread past the window loads word 0 instead
 // (its valid masks are 0, so the values are never used). A conditional load makes
 // hipcc wait for it right away, which would drain the ring's prefetch.
@@ -657,58 +635,7 @@ __device__ __forceinline__ void load_planes_any(const StepParams& p, uint64_t w0
   }
 }
 
-// Decision code masks (lo, hi) of count_votes over the round-2 lanes of word i
-// (messages.rs:185-211; 3 = None): V0 0/0, V1 1/0, VQ 0/1, None 1/1.
-template <int N, int W>
-__device__ __forceinline__ void r2_decision(const uint32_t (&lo)[N][W], const uint32_t (&hi)[N][W], int i,
-                                            uint32_t q, uint32_t& dlo, uint32_t& dhi) {
-  constexpr int B = ctr_bits(N);
-  Ctr<B> c0, c1, cq;
-  ctr_zero(c0); ctr_zero(c1); ctr_zero(cq);
-#pragma unroll
-  for (int j = 0; j < N; j++) {
-    const uint32_t l = lo[j][i], h = hi[j][i];
-    ctr_add(c0, ~l & ~h);
-    ctr_add(c1, l & ~h);
-    ctr_add(cq, ~l & h);
-  }
-  const uint32_t d0 = ctr_ge(c0, q);
-  const uint32_t d1 = ~d0 & ctr_ge(c1, q);
-  const uint32_t dq = ~d0 & ~d1 & ctr_ge(cq, q);
-  const uint32_t dn = ~(d0 | d1 | dq);
-  dlo = d1 | dn;
-  dhi = dq | dn;
-}
-
-// The same with the own round-2 vote at lane `self` (engine.rs:540-542) selected
-// per lane instead of written into the plane registers: no runtime-indexed array
-// write (the ring kernel's register budget has no room for the scratch copy the
-// compiler otherwise keeps of the self lane's planes).
-template <int N, int W>
-__device__ __forceinline__ void r2_decision_own(const uint32_t (&lo)[N][W], const uint32_t (&hi)[N][W], int i,
-                                                uint32_t q, int self, uint32_t own, uint32_t pend, uint32_t& dlo,
-                                                uint32_t& dhi) {
-  constexpr int B = ctr_bits(N);
-  Ctr<B> c0, c1, cq;
-  ctr_zero(c0); ctr_zero(c1); ctr_zero(cq);
-#pragma unroll
-  for (int j = 0; j < N; j++) {
-    const bool me = j == self;
-    const uint32_t l = me ? ((lo[j][i] & pend) | (own & ~pend)) : lo[j][i];
-    const uint32_t h = me ? (hi[j][i] & pend) : hi[j][i];
-    ctr_add(c0, ~l & ~h);
-    ctr_add(c1, l & ~h);
-    ctr_add(cq, ~l & h);
-  }
-  const uint32_t d0 = ctr_ge(c0, q);
-  const uint32_t d1 = ~d0 & ctr_ge(c1, q);
-  const uint32_t dq = ~d0 & ~d1 & ctr_ge(cq, q);
-  const uint32_t dn = ~(d0 | d1 | dq);
-  dlo = d1 | dn;
-  dhi = dq | dn;
-}
-
-// Decisions of count_votes(R2') for both possible own votes at once (DEF path):
+// Decisions of count_votes(R2') for both possible own votes at once:
 // A = own V0 on the VQ slots, B = own V1 (engine.rs:540-542, 613-628). The other
 // lanes are tallied once; the self lane is added per variant. On non-VQ slots the
 // own vote is already known (V0, V1, or none when round 1 is pending), so A == B.
@@ -753,11 +680,11 @@ __device__ __forceinline__ void r2_decision_ab(const uint32_t (&lo)[N][W], const
 // the shard's provisional stream position, every VQ slot also leaves a draw
 // record (its decision under both own votes) for rg_shard_fixup_async, and the
 // tile statistics leave the VQ slots out.
-// DEF = issue the R2 loads after the round-1 tally (the R1 registers are dead by
-// then), so that the kernel fits OCC waves per SIMD and more tiles are resident per
-// CU while one waits in the look-back; the ChaCha12 staging rows shrink to 128.
-template <int N, int W, int BLOCK, bool SHARD, int DEF = 0, int OCC = 4>
-__global__ __launch_bounds__(BLOCK, OCC) void ref_step_kernel(StepParams p) {
+// The R2 loads go out after the round-1 tally (the R1 registers are dead by then),
+// so the kernel fits 4 waves per SIMD: two 512-thread tiles resident per CU, one
+// tile's look-back overlapping the other's loads.
+template <int N, int W, int BLOCK, bool SHARD>
+__global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
   constexpr int B = ctr_bits(N);
   constexpr int WAVES = BLOCK / 64;
   __shared__ uint32_t s_wave[WAVES];
@@ -772,31 +699,20 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_step_kernel(StepParams p) {
   const uint64_t w0 = (uint64_t)tile * BLOCK * W + tw0;
   const bool active = w0 < p.n_words;
 
-  // Issue every plane load up front (R2 stays in flight across the look-back).
   uint32_t r1lo[N][W], r1hi[N][W], r2lo[N][W], r2hi[N][W];
-  if constexpr (DEF == 1) {
-    load_planes_any<N, W>(p, w0, 0, r1lo, r1hi);  // branchless: past the window they read word 0
-  } else if constexpr (DEF == 2) {  // both rounds up front, decisions still before the barrier
-    load_planes_any<N, W>(p, w0, 0, r1lo, r1hi);
-    load_planes_any<N, W>(p, w0, 2 * N, r2lo, r2hi);
-  } else {
-    load_planes<N, W>(p, w0, active, 0, r1lo, r1hi);
-    load_planes<N, W>(p, w0, active, 2 * N, r2lo, r2hi);
-  }
+  load_planes_any<N, W>(p, w0, 0, r1lo, r1hi);  // branchless: past the window they read word 0
 
   // ---- round 1: count_votes + |votes| >= quorum fallback (engine.rs:495-505).
   // Only what the draws need survives the tally: per-slot (c1 > c0), (c1 < c0).
   uint32_t r1v1[W], r1vq[W], pend[W];
   uint32_t vq_count = 0;
-  uint32_t seq0 = 0;  // DEF: a zero the compiler cannot see through, chaining word i+1 after word i
+  uint32_t seq0 = 0;  // a zero the compiler cannot see through, chaining word i+1 after word i
 #pragma unroll
   for (int i = 0; i < W; i++) {
     const uint32_t vm = valid_mask(w0 + i, p.n_words, p.n_slots);
     Ctr<B> c0, c1, cp;
     ctr_zero(c0); ctr_zero(c1); ctr_zero(cp);
-    if constexpr (DEF != 0) {
-      c0.b[0] = c1.b[0] = cp.b[0] = seq0;  // (the word tallies one after another: no 4-word ILP)
-    }
+    c0.b[0] = c1.b[0] = cp.b[0] = seq0;  // (the words tally one after another: no 4-word ILP)
 #pragma unroll
     for (int j = 0; j < N; j++) {
       const uint32_t lo = r1lo[j][i], hi = r1hi[j][i];
@@ -814,16 +730,16 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_step_kernel(StepParams p) {
     s_cls[2 * i][tid] = gt & r1vq[i];
     s_cls[2 * i + 1][tid] = lt & r1vq[i];
     vq_count += __builtin_popcount(r1vq[i]);
-    if constexpr (DEF != 0) asm volatile("" : "+v"(seq0), "+v"(r1v1[i]), "+v"(r1vq[i]), "+v"(pend[i]));
+    asm volatile("" : "+v"(seq0), "+v"(r1v1[i]), "+v"(r1vq[i]), "+v"(pend[i]));
   }
-  if constexpr (DEF == 1) load_planes_any<N, W>(p, w0, 2 * N, r2lo, r2hi);
+  load_planes_any<N, W>(p, w0, 2 * N, r2lo, r2hi);
 
   // ---- exclusive prefix of VQ slots: block scan + cross-tile look-back
   const uint32_t incl = wave_incl_scan32(vq_count, lane);
   if (lane == 63) s_wave[wave] = incl;
   lds_barrier();
   uint32_t wave_off = 0, tile_total = 0;
-  if constexpr (DEF != 0) {  // one LDS read per lane, the sums as wave-uniform scalars
+  {  // one LDS read per lane, the sums as wave-uniform scalars
     const uint32_t sw = lane < WAVES ? s_wave[lane] : 0u;
     const int wv = __builtin_amdgcn_readfirstlane(wave);
 #pragma unroll
@@ -832,72 +748,36 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_step_kernel(StepParams p) {
       wave_off += (w < wv) ? x : 0u;
       tile_total += x;
     }
-  } else {
-#pragma unroll
-    for (int w = 0; w < WAVES; w++) {
-      wave_off += (w < wave) ? s_wave[w] : 0u;
-      tile_total += s_wave[w];
-    }
   }
   stamp(p, tile, 1, tid);
-#ifdef RG_EARLY_STORES  // build-time experiment: the round-1-only planes (0, 1, 3) stored before the wait
-  // (1: every wave before the look-back; 2: wave 0 after its look-back, the others before)
-  auto early_stores = [&]() {
-    if (active) {
-      uint32_t* ob = p.out + p.lout.base(w0);
-      const uint64_t ps = p.lout.pstride;
-      uint32_t v[W];
-#pragma unroll
-      for (int i = 0; i < W; i++) v[i] = r1v1[i] | pend[i];
-      store_words_nt<W>(ob, v);
-#pragma unroll
-      for (int i = 0; i < W; i++) v[i] = r1vq[i] | pend[i];
-      store_words_nt<W>(ob + ps, v);
-      store_words_nt<W>(ob + 3 * ps, pend);
-    }
-  };
-  if (DEF != 0 && (RG_EARLY_STORES == 1 || wave != 0)) early_stores();
-#endif
   if (wave == 0) {
-#ifdef RG_LB_WIDE  // build-time experiment: K-wide polls (tools/ab_variants.sh)
-    const uint32_t e = (p.diag & 1u) ? 0u
-                                     : lookback_exclusive_wide<4>(p.lookback, tile, p.seq, tile_total, lane,
-                                                                  &rec->error.v, RG_LB_WIDE);
-#else
     // The launch's first tiles all start together, and tile t needs the aggregates of
     // all t predecessors: with 64 granules per poll the inclusive frontier crosses the
     // first generation in t/64 round trips while the later tiles hold their CUs.
     // In launches of at most 1024 tiles (a single 2^20 window: 14.1 -> 13.2 us) those
-    // tiles poll kLBWide x 64 predecessors at once; large launches and steady-state
-    // tiles keep the one-granule-per-lane poll (wider polls measured slower there).
+    // tiles poll kLBWide x 64 predecessors at once; larger launches keep the
+    // one-granule-per-lane poll (wider polls measured slower there).
     uint32_t e = 0;
     if (!(p.diag & 1u)) {
-      if (DEF != 0 && tile < 64u * kLBWide && p.n_tiles <= 1024u && !(p.diag & 16u)) {
+      if (tile < 64u * kLBWide && p.n_tiles <= 1024u && !(p.diag & 16u)) {
         const int kf = (int)((tile + 63u) / 64u);
         e = lookback_exclusive_wide<kLBWide>(p.lookback, tile, p.seq, tile_total, lane, &rec->error.v, kf, kLBWide, 1);
       } else {
         e = lookback_exclusive(p.lookback, tile, p.seq, tile_total, lane, &rec->error.v);
       }
     }
-#endif
     if (lane == 0) s_excl = e;
-#ifdef RG_EARLY_STORES
-    if (DEF != 0 && RG_EARLY_STORES == 2) early_stores();
-#endif
   }
-  // DEF: both-outcome decisions while wave 0 looks back; the R2 registers die here,
+  // both-outcome decisions while wave 0 looks back; the R2 registers die here,
   // before the ChaCha12 blocks need theirs
   uint32_t dalo[W], dahi[W], dblo[W], dbhi[W];
-  if constexpr (DEF != 0) {
 #pragma unroll
-    for (int i = 0; i < W; i++)
-    {
-      r2_decision_ab<N, W>(r2lo, r2hi, i, p.q, p.self_lane, r1v1[i], r1vq[i], pend[i], dalo[i], dahi[i], dblo[i],
-                           dbhi[i]);
-      // pin the results here (volatile asm keeps its order with the barrier below):
-      // otherwise the decisions sink to their use and R2 stays live across ChaCha
-      asm volatile("" : "+v"(dalo[i]), "+v"(dahi[i]), "+v"(dblo[i]), "+v"(dbhi[i]));
-    }
+  for (int i = 0; i < W; i++) {
+    r2_decision_ab<N, W>(r2lo, r2hi, i, p.q, p.self_lane, r1v1[i], r1vq[i], pend[i], dalo[i], dahi[i], dblo[i],
+                         dbhi[i]);
+    // pin the results here (volatile asm keeps its order with the barrier below):
+    // otherwise the decisions sink to their use and R2 stays live across ChaCha
+    asm volatile("" : "+v"(dalo[i]), "+v"(dahi[i]), "+v"(dblo[i]), "+v"(dbhi[i]));
   }
   lds_barrier();
   stamp(p, tile, 2, tid);
@@ -916,7 +796,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_step_kernel(StepParams p) {
     mq[i] = r1vq[i];
   }
   if (tile_total) {
-    constexpr int kRows = DEF ? (BLOCK < 128 ? BLOCK : 128) : BLOCK;
+    constexpr int kRows = BLOCK < 128 ? BLOCK : 128;
     __shared__ uint32_t s_blk[kRows][17];  // +1 word: conflict-free rows
     const unsigned long long b_first = k_tile >> 3, b_last = (k_tile + tile_total - 1) >> 3;
     for (unsigned long long cb = b_first; cb <= b_last; cb += kRows) {
@@ -954,70 +834,24 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_step_kernel(StepParams p) {
   unsigned long long kr = k_first - k_base;  // SHARD: local draw number of this thread's first VQ slot
 #pragma unroll
   for (int i = 0; i < W; i++) {
-    if constexpr (DEF != 0) {
-      const uint32_t sel = own_lo[i] & r1vq[i];  // VQ slots whose draw gave V1
-      dlo[i] = (dalo[i] & ~sel) | (dblo[i] & sel);
-      dhi[i] = (dahi[i] & ~sel) | (dbhi[i] & sel);
-      if constexpr (SHARD) {  // draw records: both decisions are at hand already
-        uint32_t m = r1vq[i];
-        const uint32_t gtm = m ? s_cls[2 * i][tid] : 0u, ltm = m ? s_cls[2 * i + 1][tid] : 0u;
-        while (m) {  // indexed by local draw number (ascending slot order)
-          const int b = __builtin_ctz(m);
-          m &= m - 1;
-          const uint32_t own = (own_lo[i] >> b) & 1u;
-          const uint32_t d_v0 = ((dalo[i] >> b) & 1u) | (((dahi[i] >> b) & 1u) << 1);
-          const uint32_t d_v1 = ((dblo[i] >> b) & 1u) | (((dbhi[i] >> b) & 1u) << 1);
-          const uint32_t cls = ((gtm >> b) & 1u) ? kRecGt : (((ltm >> b) & 1u) ? kRecLt : 0u);
-          const uint32_t info = cls | (d_v0 << 2) | (d_v1 << 4) | (own << 6);
-          const uint32_t off = (uint32_t)(32u * (w0 + i) + b);
-          if (kr < p.vq_cap) p.vq_rec[kr] = ((unsigned long long)info << 32) | off;
-          kr++;
-        }
-      }
-    } else if constexpr (SHARD) {
-      uint32_t alo = 0, ahi = 0;
-      if (r1vq[i]) {  // the decision under the other own vote, for the draw records
-#pragma unroll
-        for (int j = 0; j < N; j++)
-          if (j == p.self_lane) {
-            const uint32_t l = r2lo[j][i], h = r2hi[j][i];
-            r2lo[j][i] = (l & pend[i]) | ((own_lo[i] ^ r1vq[i]) & ~pend[i]);
-            r2hi[j][i] = h & pend[i];
-            r2_decision<N, W>(r2lo, r2hi, i, p.q, alo, ahi);
-            r2lo[j][i] = l;
-            r2hi[j][i] = h;
-          }
-      }
-#pragma unroll
-      for (int j = 0; j < N; j++)
-        if (j == p.self_lane) {
-          r2lo[j][i] = (r2lo[j][i] & pend[i]) | (own_lo[i] & ~pend[i]);
-          r2hi[j][i] &= pend[i];
-        }
-      r2_decision<N, W>(r2lo, r2hi, i, p.q, dlo[i], dhi[i]);
+    const uint32_t sel = own_lo[i] & r1vq[i];  // VQ slots whose draw gave V1
+    dlo[i] = (dalo[i] & ~sel) | (dblo[i] & sel);
+    dhi[i] = (dahi[i] & ~sel) | (dbhi[i] & sel);
+    if constexpr (SHARD) {  // draw records: both decisions are at hand already
       uint32_t m = r1vq[i];
       const uint32_t gtm = m ? s_cls[2 * i][tid] : 0u, ltm = m ? s_cls[2 * i + 1][tid] : 0u;
-      while (m) {  // draw records, indexed by local draw number (ascending slot order)
+      while (m) {  // indexed by local draw number (ascending slot order)
         const int b = __builtin_ctz(m);
         m &= m - 1;
         const uint32_t own = (own_lo[i] >> b) & 1u;
-        const uint32_t dp = ((dlo[i] >> b) & 1u) | (((dhi[i] >> b) & 1u) << 1);
-        const uint32_t da = ((alo >> b) & 1u) | (((ahi >> b) & 1u) << 1);
-        const uint32_t d_v0 = own ? da : dp, d_v1 = own ? dp : da;
+        const uint32_t d_v0 = ((dalo[i] >> b) & 1u) | (((dahi[i] >> b) & 1u) << 1);
+        const uint32_t d_v1 = ((dblo[i] >> b) & 1u) | (((dbhi[i] >> b) & 1u) << 1);
         const uint32_t cls = ((gtm >> b) & 1u) ? kRecGt : (((ltm >> b) & 1u) ? kRecLt : 0u);
         const uint32_t info = cls | (d_v0 << 2) | (d_v1 << 4) | (own << 6);
         const uint32_t off = (uint32_t)(32u * (w0 + i) + b);
         if (kr < p.vq_cap) p.vq_rec[kr] = ((unsigned long long)info << 32) | off;
         kr++;
       }
-    } else {
-#pragma unroll
-      for (int j = 0; j < N; j++)
-        if (j == p.self_lane) {
-          r2lo[j][i] = (r2lo[j][i] & pend[i]) | (own_lo[i] & ~pend[i]);
-          r2hi[j][i] &= pend[i];
-        }
-      r2_decision<N, W>(r2lo, r2hi, i, p.q, dlo[i], dhi[i]);
     }
     const uint32_t vm = valid_mask(w0 + i, p.n_words, p.n_slots);
     dlo[i] &= vm;
@@ -1033,23 +867,16 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_step_kernel(StepParams p) {
     uint32_t* ob = p.out + p.lout.base(w0);
     const uint64_t ps = p.lout.pstride;
     uint32_t v[W];
-#ifdef RG_EARLY_STORES
-    constexpr bool late = DEF == 0;
-#else
-    constexpr bool late = true;
-#endif
-    if (late) {
 #pragma unroll
-      for (int i = 0; i < W; i++) v[i] = r1v1[i] | pend[i];
-      store_words_nt<W>(ob, v);
+    for (int i = 0; i < W; i++) v[i] = r1v1[i] | pend[i];
+    store_words_nt<W>(ob, v);
 #pragma unroll
-      for (int i = 0; i < W; i++) v[i] = r1vq[i] | pend[i];
-      store_words_nt<W>(ob + ps, v);
-    }
+    for (int i = 0; i < W; i++) v[i] = r1vq[i] | pend[i];
+    store_words_nt<W>(ob + ps, v);
 #pragma unroll
     for (int i = 0; i < W; i++) v[i] = own_lo[i] | pend[i];
     store_words_nt<W>(ob + 2 * ps, v);
-    if (late) store_words_nt<W>(ob + 3 * ps, pend);
+    store_words_nt<W>(ob + 3 * ps, pend);
     store_words_nt<W>(ob + 4 * ps, dlo);
     store_words_nt<W>(ob + 5 * ps, dhi);
     store_words_nt<W>(ob + 6 * ps, st_dec);
@@ -1066,7 +893,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_step_kernel(StepParams p) {
     st_vm[i] = valid_mask(w0 + i, p.n_words, p.n_slots) & keep;
   }
   const TileStats ts = thread_stats<W>(st_dec, st_v1, pend, st_vm, vq_count, w0, tw0, p);
-  finish_tile<SHARD ? kFinShard : kFinRef, BLOCK, W, (OCC > 4 ? 2 : 8)>(p, rec, ts, tile, tid, lane, wave);
+  finish_tile<SHARD ? kFinShard : kFinRef, BLOCK, W>(p, rec, ts, tile, tid, lane, wave);
   stamp(p, tile, 4, tid);
 }
 
@@ -1270,20 +1097,38 @@ __device__ __forceinline__ uint32_t take_ticket(Record* rec) {
 }
 
 template <int N, int W, int BLOCK, bool SHARD>
-__global__ __launch_bounds__(BLOCK, 2 * BLOCK / 256) void ref_lag_kernel(StepParams p) {
+__global__ __launch_bounds__(BLOCK, 4) void ref_lag_kernel(StepParams p) {  // 4 waves/SIMD: 2 x 512 or 1 x 1024 per CU
   constexpr int B = ctr_bits(N);
   constexpr int WAVES = BLOCK / 64;
   constexpr int kRows = BLOCK < 128 ? BLOCK : 128;
   constexpr uint32_t kTW = (uint32_t)BLOCK * W;  // words per tile
   __shared__ __attribute__((aligned(16))) uint32_t s_park[2][kParkFields][BLOCK][W];
   __shared__ uint32_t s_blk[kRows][17];  // ChaCha12 blocks of the parked tile's draws (+1 word: no conflicts)
-  __shared__ uint32_t s_wave[WAVES];
-  __shared__ unsigned long long s_lb[WAVES];  // per-wave look-back result: sum | inclusive << 32 | blocked << 33
-  __shared__ uint32_t s_bcast[4];        // [0] next ticket, [1] parked tile's prefix (continued look-back)
+  // Broadcast slots written before a barrier and read after it are double-buffered by
+  // iteration parity: the next iteration's writes come before ITS barrier, so with one
+  // buffer a wave still reading this iteration's value could see them.
+  __shared__ uint32_t s_wave[2][WAVES];
+  __shared__ unsigned long long s_lb[2][8];  // per-wave look-back result: sum | inclusive << 32 | blocked << 33
+  __shared__ uint32_t s_bcast[2][4];        // [0] next ticket, [1] parked tile's prefix (continued look-back)
   Record* rec = p.rec + (p.seq & 1u);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t tag_agg = p.seq << 1, tag_inc = tag_agg | 1u;
   const unsigned long long k_base = SHARD ? p.state->shard_draws : p.state->rng_next;  // StdRng position
+  // diag & 4: per-workgroup phase times (s_memrealtime, 100 MHz) -> p.dbg[blockIdx.x][12]:
+  //   0 start->loop, 1 tally (incl. the round-1 wait), 2 scan barrier, 3 decisions (incl.
+  //   the round-2 wait), 4 draws of the parked tile, 5 its stores, 6 loop end->record, 7 iterations,
+  //   [8] look-back completion inside the draws, [9] continued look-backs, [10] start, [11] end (absolute)
+  const bool stamps = (p.diag & 4u) != 0;
+  unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // [8] look-back completion, [9] continued
+  unsigned long long st_t = stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+  const unsigned long long st_begin = st_t;
+  auto lap = [&](int k) {
+    if (stamps) {
+      const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+      st_acc[k] += t - st_t;
+      st_t = t;
+    }
+  };
 
   // this thread's byte offsets inside a tile's planes; plane strides in bytes
   const uint32_t in_lane = (uint32_t)p.lin.base((uint64_t)tid * W) * 4u;
@@ -1296,13 +1141,34 @@ __global__ __launch_bounds__(BLOCK, 2 * BLOCK / 256) void ref_lag_kernel(StepPar
   // and its stores go out of range (dropped)
   auto in_off = [&](uint32_t t) { return active(t) ? in_lane : 0u; };
   auto out_off = [&](uint32_t t) { return active(t) ? out_lane : kOffNone; };
+#ifdef RG_LAG_CHECK  // experiment build: report (printf) the first out-of-extent access of a launch
+  // returns the offset to use: a bad one is reported and replaced (0 for loads,
+  // out of range for stores), so the checked build never faults
+  auto chk = [&](const char* what, uint64_t base_words, uint32_t voff, uint32_t soff, uint64_t extent,
+                 uint32_t safe) -> uint32_t {
+    if (voff == kOffNone) return voff;
+    const uint64_t end = base_words * 4 + voff + soff + 4 * W;
+    if (end <= extent) return voff;
+    if (atomicOr(&rec->error.v, 64ull) == 0)
+      printf("RG_LAG_CHECK %s: tile base %llu words, voff %u, soff %u, end %llu > extent %llu (tid %d)\n", what,
+             (unsigned long long)base_words, voff, soff, (unsigned long long)end, (unsigned long long)extent, tid);
+    return safe;
+  };
+#define LAG_CHK_IN(t, voff, first) \
+  voff = chk("load", p.lin.base((uint64_t)(t) * kTW), voff, (uint32_t)((first) + 2 * N - 1) * in_pb, p.in_bytes, 0u)
+#define LAG_CHK_OUT(t, voff, plane) \
+  voff = chk("store", p.lout.base((uint64_t)(t) * kTW), voff, (plane) * out_pb, p.out_bytes, kOffNone)
+#else
+#define LAG_CHK_IN(t, voff, first) ((void)0)
+#define LAG_CHK_OUT(t, voff, plane) ((void)0)
+#endif
 
   // tickets: c = the tile being tallied (its round-1 planes were loaded during the
   // previous iteration); the ticket after it is requested one iteration ahead
   uint32_t nt = 0;
-  if (tid == 0) s_bcast[0] = take_ticket(rec);
+  if (tid == 0) s_bcast[1][0] = take_ticket(rec);
   lds_barrier();
-  uint32_t c = s_bcast[0];
+  uint32_t c = s_bcast[1][0];
   if (tid == 0) nt = take_ticket(rec);
   uint32_t r1lo[N][W], r1hi[N][W];
   unsigned long long lbg;  // the look-back poll of the tile parked next (issued before its successor's loads)
@@ -1318,11 +1184,13 @@ __global__ __launch_bounds__(BLOCK, 2 * BLOCK / 256) void ref_lag_kernel(StepPar
   // (wave w: distances 64w .. 64w + 63 below p; one load per lane, so every wave
   // issues the same memory operations) with the round-1 planes' wait, evaluates them
   // after the tally, and the waves' results combine after the scan barrier.
+  constexpr int kPollWaves = WAVES < 8 ? WAVES : 8;  // 512 granules per poll (waves 8-15 repeat 0-7)
   auto lb_poll = [&]() -> unsigned long long {
-    const int32_t idx = park_tile - 1 - (64 * wave + lane);
+    const int32_t idx = park_tile - 1 - (64 * (wave % kPollWaves) + lane);
     return atomic_load_agent(p.lookback + (idx > prev_tile ? idx : 0));
   };
   auto lb_eval = [&](unsigned long long g) {
+    if (wave >= kPollWaves) return;
     const int32_t idx = park_tile - 1 - (64 * wave + lane);
     const uint32_t tag = (uint32_t)(g >> 32);
     const bool synth = idx <= prev_tile;  // prev_tile is inclusive (this WG computed it)
@@ -1334,15 +1202,15 @@ __global__ __launch_bounds__(BLOCK, 2 * BLOCK / 256) void ref_lag_kernel(StepPar
     const uint32_t val = idx == prev_tile ? prev_incl : (synth ? 0u : (uint32_t)g);
     const uint32_t sum = wave_sum32(lane <= f ? val : 0u);
     if (lane == 0)
-      s_lb[wave] = (unsigned long long)sum | ((unsigned long long)(f < 64) << 32) |
+      s_lb[pk][wave] = (unsigned long long)sum | ((unsigned long long)(f < 64) << 32) |
                    ((unsigned long long)((nr & need) != 0) << 33);
   };
   // after the barrier (uniform): true and the prefix when the polls reached an inclusive
   auto lb_combine = [&](uint32_t& excl) -> bool {
     excl = 0;
 #pragma unroll
-    for (int w = 0; w < WAVES; w++) {
-      const unsigned long long x = s_lb[w];
+    for (int w = 0; w < kPollWaves; w++) {
+      const unsigned long long x = s_lb[pk][w];
       if (x >> 33) return false;  // a granule it needs is not published yet
       excl += (uint32_t)x;
       if ((x >> 32) & 1u) return true;
@@ -1354,15 +1222,18 @@ __global__ __launch_bounds__(BLOCK, 2 * BLOCK / 256) void ref_lag_kernel(StepPar
   auto draw_parked = [&](uint32_t (&own)[W]) {
     uint32_t(&pp)[kParkFields][BLOCK][W] = s_park[pk ^ 1u];
     uint32_t excl;
-    if (!lb_combine(excl)) {  // uniform: the rare continued look-back (wave 0, 256 granules per poll)
+    const bool lb_done = lb_combine(excl);
+    if (!lb_done) {  // uniform: the rare continued look-back (wave 0, 256 granules per poll)
       if (wave == 0) {
         const uint32_t e = lag_finish(p.lookback, park_tile - 1 + 64 * kLagPoll, prev_tile, prev_incl, p.seq, lane,
                                       0u, false, &rec->error.v);
-        if (lane == 0) s_bcast[1] = e;
+        if (lane == 0) s_bcast[pk][1] = e;
       }
       lds_barrier();
-      excl = s_bcast[1];
+      excl = s_bcast[pk][1];
     }
+    if (stamps) st_acc[9] += lb_done ? 0 : 1;
+    lap(8);
     if (tid == 0)
       atomic_store_agent(p.lookback + park_tile, ((unsigned long long)tag_inc << 32) | (excl + park_total));
     prev_tile = park_tile;
@@ -1449,7 +1320,8 @@ __global__ __launch_bounds__(BLOCK, 2 * BLOCK / 256) void ref_lag_kernel(StepPar
     const uint32_t pt = have_park ? (uint32_t)park_tile : 0u;
     const uint32_t pw0 = pt * kTW + (uint32_t)tid * W;
     const __amdgpu_buffer_rsrc_t orr = out_rsrc(pt);
-    const uint32_t oo = have_park ? out_off(pt) : kOffNone;
+    uint32_t oo = have_park ? out_off(pt) : kOffNone;
+    LAG_CHK_OUT(pt, oo, 7);
     {  // plane 2: own round-2 vote lo
       uint32_t v[W];
       lds_ld<W>(pp[0][tid], v);
@@ -1504,17 +1376,29 @@ __global__ __launch_bounds__(BLOCK, 2 * BLOCK / 256) void ref_lag_kernel(StepPar
     buf_st<W>(orr, oo, 7 * out_pb, dhi);
   };
 
-  // The vector memory counter retires in issue order, so an iteration issues, in this
-  // order: [tally's stores] [round 2 of tile c] [the parked tile's stores] [the
-  // look-back poll of tile c] [round 1 of the next tile]. The next tally waits for the
-  // round-1 planes, and the poll (older) has landed by then. The operations issued do
-  // not depend on whether a tile is parked (the poll and stores without one are
-  // harmless), so the compiler's waits count exactly on every path.
-  {
-    lbg = lb_poll();
+  // Software pipeline. Tile c's round-1 planes (r1) were issued right after the
+  // previous tile's tally and its round-2 planes (r2) right after the previous
+  // tile's decisions, so one tile of planes is in flight through the whole
+  // iteration. The vector memory counter retires in issue order and every operation
+  // below is issued on every path (dummy loads past the last tile, out-of-range
+  // stores without a parked tile), so the compiler's waits count exactly:
+  //   tally(c) <- r1  | early stores | look-back eval (poll of the last iteration)
+  //   | scan barrier | r1 <- next | decisions(c) <- r2 | r2 <- next | park c
+  //   | draws + stores of the parked tile | poll for c
+  uint32_t r2lo[N][W], r2hi[N][W];
+  {  // in the order the loop leaves them: r1, r2, five stores (here out of range), poll
     const bool any = c < p.n_tiles;
-    buf_ld_planes<N, W>(in_rsrc(any ? c : 0u), any ? in_off(c) : 0u, in_pb, 0, r1lo, r1hi);
+    uint32_t voff0 = any ? in_off(c) : 0u;
+    LAG_CHK_IN(any ? c : 0u, voff0, 2 * N);
+    buf_ld_planes<N, W>(in_rsrc(any ? c : 0u), voff0, in_pb, 0, r1lo, r1hi);
+    buf_ld_planes<N, W>(in_rsrc(any ? c : 0u), voff0, in_pb, 2 * N, r2lo, r2hi);
+    const uint32_t z[W] = {};
+    const __amdgpu_buffer_rsrc_t orr = out_rsrc(0u);
+#pragma unroll
+    for (int k = 0; k < 5; k++) buf_st<W>(orr, kOffNone, (uint32_t)k * 4u, z);
+    lbg = lb_poll();  // no parked tile yet: a harmless poll
   }
+  lap(0);
   while (c < p.n_tiles) {
     const bool have_park = park_tile >= 0;
     uint32_t(&pc)[kParkFields][BLOCK][W] = s_park[pk];
@@ -1559,7 +1443,8 @@ __global__ __launch_bounds__(BLOCK, 2 * BLOCK / 256) void ref_lag_kernel(StepPar
       lds_st<W>(pc[2][tid], e0);
       lds_st<W>(pc[3][tid], e1);
       const __amdgpu_buffer_rsrc_t orr = out_rsrc(c);
-      const uint32_t oo = out_off(c);
+      uint32_t oo = out_off(c);
+      LAG_CHK_OUT(c, oo, 3);
       buf_st<W>(orr, oo, 0, x);
 #pragma unroll
       for (int i = 0; i < W; i++) x[i] = vq[i] | pd[i];
@@ -1567,14 +1452,15 @@ __global__ __launch_bounds__(BLOCK, 2 * BLOCK / 256) void ref_lag_kernel(StepPar
       buf_st<W>(orr, oo, 3 * out_pb, pd);
     }
     lb_eval(lbg);
-    // (2) VQ prefix inside the tile; publish the tile's aggregate; the next ticket
+    lap(1);
+    // (2) VQ prefix inside the tile; publish the tile's aggregate; the next tickets
     const uint32_t incl = wave_incl_scan32(vq_count, lane);
-    if (lane == 63) s_wave[wave] = incl;
-    if (tid == 0) s_bcast[0] = nt;
+    if (lane == 63) s_wave[pk][wave] = incl;
+    if (tid == 0) s_bcast[pk][0] = nt;
     lds_barrier();
     uint32_t wave_off = 0, total = 0;
     {
-      const uint32_t sw = lane < WAVES ? s_wave[lane] : 0u;
+      const uint32_t sw = lane < WAVES ? s_wave[pk][lane] : 0u;
       const int wv = __builtin_amdgcn_readfirstlane(wave);
 #pragma unroll
       for (int w = 0; w < WAVES; w++) {
@@ -1583,29 +1469,20 @@ __global__ __launch_bounds__(BLOCK, 2 * BLOCK / 256) void ref_lag_kernel(StepPar
         total += x;
       }
     }
-    const uint32_t nx = s_bcast[0];
+    const uint32_t nx = s_bcast[pk][0];
+    lap(2);
     if (tid == 0) {
       atomic_store_agent(p.lookback + c, ((unsigned long long)(c == 0 ? tag_inc : tag_agg) << 32) | total);
       if (nx < p.n_tiles) nt = take_ticket(rec);
     }
-    // (3) round 2 of tile c in flight behind the parked tile's draws and stores; then
-    //     round 1 of the next tile. The vector memory counter retires in issue order:
-    //     the stores go before the next tile's loads, so the next tally's wait covers
-    //     them and the look-back poll issued after it waits for nothing else.
-    uint32_t r2lo[N][W], r2hi[N][W];
-    buf_ld_planes<N, W>(in_rsrc(c), in_off(c), in_pb, 2 * N, r2lo, r2hi);
-    uint32_t own[W] = {};
-    if (have_park) draw_parked(own);
-    store_parked(own, have_park);
-    const int32_t prev_park = park_tile;
-    park_tile = (int32_t)c;  // the look-back poll of tile c (prev_tile: the tile just finished)
-    lbg = lb_poll();
-    park_tile = prev_park;
-    {  // unconditional: past the last tile every lane reads tile c's first word
-      const bool more = nx < p.n_tiles;
-      buf_ld_planes<N, W>(in_rsrc(more ? nx : c), more ? in_off(nx) : 0u, in_pb, 0, r1lo, r1hi);
-    }
-    // (4) round-2 decisions of tile c for both own votes (engine.rs:540-542, 613-628)
+    // (3) the next tile's round-1 planes in flight (past the last tile: tile c's first word)
+    const bool more = nx < p.n_tiles;
+    const __amdgpu_buffer_rsrc_t nrr = in_rsrc(more ? nx : c);
+    uint32_t noff = more ? in_off(nx) : 0u;
+    LAG_CHK_IN(more ? nx : c, noff, 2 * N);
+    buf_ld_planes<N, W>(nrr, noff, in_pb, 0, r1lo, r1hi);
+    // (4) round-2 decisions of tile c for both own votes (engine.rs:540-542, 613-628);
+    //     then the next tile's round-2 planes in flight
     {
       uint32_t x[W], pd[W], e0[W], e1[W];
       lds_ld<W>(pc[0][tid], x);
@@ -1620,15 +1497,25 @@ __global__ __launch_bounds__(BLOCK, 2 * BLOCK / 256) void ref_lag_kernel(StepPar
         const uint32_t vm = valid_mask(w0 + i, p.n_words, p.n_slots);
         alo[i] &= vm; ahi[i] &= vm; blo[i] &= vm; bhi[i] &= vm;
       }
+      buf_ld_planes<N, W>(nrr, noff, in_pb, 2 * N, r2lo, r2hi);
       lds_st<W>(pc[4][tid], alo);
       lds_st<W>(pc[5][tid], ahi);
       lds_st<W>(pc[6][tid], blo);
       lds_st<W>(pc[7][tid], bhi);
     }
+    lap(3);
+    // (5) the parked tile: draws, decisions, stores
+    uint32_t own[W] = {};
+    if (have_park) draw_parked(own);
+    lap(4);
+    store_parked(own, have_park);
+    lap(5);
+    st_acc[7]++;
     a_draws += vq_count;
-    park_tile = (int32_t)c;
+    park_tile = (int32_t)c;  // tile c is parked; its look-back poll (prev_tile: the tile just finished)
     park_total = total;
     park_thr = wave_off + incl - vq_count;
+    lbg = lb_poll();
     pk ^= 1u;
     c = nx;
   }
@@ -1649,6 +1536,13 @@ __global__ __launch_bounds__(BLOCK, 2 * BLOCK / 256) void ref_lag_kernel(StepPar
     const uint32_t mx = wave_max32(a_max1), mn = wave_min32(a_min);
     if (lane == 0) { red[wave][0] = s0; red[wave][1] = s1; red[wave][2] = mx; red[wave][3] = mn; }
     lds_barrier();
+    if (stamps && tid == 0) {
+      lap(6);
+#pragma unroll
+      for (int k = 0; k < 10; k++) p.dbg[(uint64_t)blockIdx.x * 12 + k] = st_acc[k];
+      p.dbg[(uint64_t)blockIdx.x * 12 + 10] = st_begin;
+      p.dbg[(uint64_t)blockIdx.x * 12 + 11] = st_t;
+    }
     if (tid == 0) {
       unsigned long long t[kLagStatGranules] = {0, 0, 0, 0, 0, 0xFFFFFFFFull};
 #pragma unroll 1
@@ -2510,88 +2404,6 @@ __device__ __forceinline__ uint32_t heard_mask(uint64_t dseed, uint64_t slot, ui
 }
 
 constexpr int kClusterStats = 8;  // all_decided, v1, sum_phases, max_phases, sum_coin_phases, sum_first, slots, -
-
-template <int N>
-__global__ __launch_bounds__(256) void wmvc_cluster_kernel(const uint32_t* states, uint64_t stride, uint64_t n_slots,
-                                                           uint64_t slot_base, uint32_t q, uint32_t fp1, Key ckey,
-                                                           uint64_t coin_stream, uint64_t dseed, uint32_t max_phases,
-                                                           uint32_t* info, unsigned long long* partials) {
-  constexpr uint32_t kAll = (1u << N) - 1u;
-  unsigned long long acc[kClusterStats] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s < n_slots; s += (uint64_t)gridDim.x * 256) {
-    const uint64_t id = slot_base + s;
-    uint32_t st = 0;
-#pragma unroll
-    for (int r = 0; r < N; r++) st |= ((states[(uint64_t)r * stride + s / 32] >> (s & 31)) & 1u) << r;
-    uint32_t decided = 0, decv = 0, phases = 0, first = 0, coins = 0;
-    for (uint32_t p = 1; p <= max_phases && decided != kAll; p++) {
-      uint32_t v1 = 0, vq = 0;  // round 1 (phase_rnd1): unanimous heard states -> vote, else '?'
-#pragma unroll
-      for (int r = 0; r < N; r++) {
-        const uint32_t h = heard_mask<N>(dseed, id, p, 1, r, q);
-        const uint32_t c1 = __builtin_popcount(h & st), c0 = __builtin_popcount(h & ~st);
-        if (c1 >= q) v1 |= 1u << r;
-        else if (c0 < q) vq |= 1u << r;
-      }
-      uint32_t nst = 0;
-      int coin = -1;
-#pragma unroll
-      for (int r = 0; r < N; r++) {  // round 2 (phase_rnd2): f+1 decide / adopt / common coin
-        const uint32_t h = heard_mask<N>(dseed, id, p, 2, r, q);
-        const uint32_t c1 = __builtin_popcount(h & v1), cq = __builtin_popcount(h & vq);
-        const uint32_t c0 = q - c1 - cq;
-        int nv = c0 >= fp1 ? 0 : (c1 >= fp1 ? 1 : -1);
-        if (nv >= 0 && !((decided >> r) & 1u)) {
-          decided |= 1u << r;
-          decv |= (uint32_t)nv << r;
-          if (!first) first = p;
-        }
-        if (nv < 0) {
-          if (c0 > 0) nv = 0;
-          else if (c1 > 0) nv = 1;
-          else {
-            if (coin < 0) {
-              uint32_t blk[16];
-              chacha_block<12>(ckey, ((uint64_t)(p - 1) << 40) | (id >> 9), coin_stream, blk);
-              coin = (int)((select16(blk, (uint32_t)(id >> 5) & 15u) >> (id & 31)) & 1u);
-              coins++;
-            }
-            nv = coin;
-          }
-        }
-        if ((decided >> r) & 1u) nv = (int)((decv >> r) & 1u);
-        nst |= (uint32_t)nv << r;
-      }
-      st = nst;
-      if (decided == kAll) phases = p;
-    }
-    // all replicas decided: their common value (kCodeVQ = they disagree, an agreement
-    // violation of weak_mvc.ivy the property tests assert never occurs)
-    const uint32_t dec = decided == kAll ? ((decv == 0 || decv == kAll) ? (decv & 1u) : kCodeVQ) : kCodeNone;
-    info[s] = dec | (phases << 8) | (first << 16) | (coins << 24);
-    acc[0] += decided == kAll;
-    acc[1] += dec == kCodeV1;
-    acc[2] += phases;
-    acc[3] = phases > acc[3] ? phases : acc[3];
-    acc[4] += coins;
-    acc[5] += first;
-    acc[6] += 1;
-  }
-  __shared__ unsigned long long red[4][kClusterStats];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int k = 0; k < kClusterStats; k++) acc[k] = k == 3 ? wave_max64(acc[k]) : wave_sum64(acc[k]);
-  if (lane == 0)
-#pragma unroll
-    for (int k = 0; k < kClusterStats; k++) red[wave][k] = acc[k];
-  lds_barrier();
-  if (threadIdx.x < kClusterStats) {
-    const int k = threadIdx.x;
-    unsigned long long v = 0;
-    for (int w = 0; w < 4; w++) v = k == 3 ? (red[w][k] > v ? red[w][k] : v) : v + red[w][k];
-    partials[(uint64_t)blockIdx.x * kClusterStats + k] = v;  // plain stores: folded by the next launch
-  }
-}
 
 // Common-coin table for the cluster kernel: coin bits of phases 1..P for the
 // window's slots, [P][n_words]; one thread per 512-slot group (16 words) computes

@@ -2,23 +2,28 @@
 //
 // Semantics: KVStoreSMR::apply_commands (examples/kvstore_smr/src/smr_impl.rs:72-127)
 // over KVStore (store.rs:144-262) applied to the commands in total order. Parallel
-// form (one launch chain per batch, no host round trip):
-//   1 decode    one thread per command: bincode KVOperation (operations.rs:10-19),
-//               key/value validation (store.rs:463-478), 64-bit key hash
-//   2 sort      stable radix sort of (hash, command index): each key's commands
+// form (one stream-ordered launch chain per batch, no host round trip):
+//   1 decode    thread per command: bincode KVOperation (operations.rs:10-19), UTF-8
+//               and key/value validation (store.rs:463-478), 64-bit key hash, a u32
+//               sort key (hash bucket; "not applied" sorts last), per-block worst-case
+//               growth for the capacity refusal; short commands in one load round trip
+//   2 sort      stable radix sort of (bucket, command index): each key's commands
 //               become one contiguous run, still in total order
-//   3 plan      one thread per hash run ("walker"): looks every distinct key of its
-//               run up in the table, replays the key's commands in order and sizes
-//               what the commit writes (new key bytes + final value bytes)
-//   4 decide    one thread folds the per-block plan partials: can StoreFull (the
+//   3 plan      wave per 1024 sorted positions, decoded fields staged in LDS; run
+//               heads compacted per wave, each lane replays one key's commands in
+//               order (one table lookup per key), writes the result bytes and a
+//               per-key commit record (slot, version, key/value sources, in-place or
+//               new allocation); multi-key runs (bucket or hash collisions) take a
+//               general path over global memory
+//   4 decide    one 1024-thread block folds the plan partials: can StoreFull (the
 //               only cross-key dependency: store.rs:153-158 reads data.len()) occur?
-//               live + keys created <= max_keys => no, the keyed replay is exact.
-//   5 commit    the same walkers write results, table entries and heap bytes at
-//               offsets from an exclusive scan of the plan sizes
-//   6 ordered   otherwise ONE thread replays the batch in total order (exact,
-//               slow; counted in rg_kv_stats.ordered_batches)
-//   7 finish    folds the per-block counter deltas into the store counters
-//               (6, 7 and the refusal results are one launch, kv_close_kernel)
+//               live + keys created <= max_keys => no, the keyed replay is exact;
+//               capacity refusal; exclusive scan of the heap bytes
+//   5 commit    lookup-free write pass over the commit records: table claims for new
+//               keys, key/value bytes at the scanned heap offsets, entry fields
+//   6 close     one launch: the ordered replay (one thread, only when StoreFull can
+//               fire: exact, slow, counted in rg_kv_stats.ordered_batches), the
+//               counter fold, or the refusal results
 // Key equality is byte equality (hash runs are split by comparing key bytes).
 // Deleted keys keep their table slot (version 0 = not live) so probe chains stay
 // intact; a later SET of the same key reuses it with a fresh ValueEntry (version 1).

@@ -10,10 +10,16 @@ namespace {
 template <int N>
 void launch_n(int block, int words, uint32_t grid, hipStream_t s, const StepParams& p) {
   constexpr int WM = N <= 5 ? 4 : (N <= 10 ? 2 : 1);
-  if (block == 0) hipLaunchKernelGGL((ref_lag_kernel<N, (N <= 5 ? 2 : 1), 512, true>), dim3(grid), dim3(512), 0, s, p);
-  else if (block == 512) hipLaunchKernelGGL((ref_step_kernel<N, WM, 512, true, 1>), dim3(grid), dim3(512), 0, s, p);
-  else if (block == 256) hipLaunchKernelGGL((ref_step_kernel<N, WM, 256, true, 1>), dim3(grid), dim3(256), 0, s, p);
-  else hipLaunchKernelGGL((ref_step_kernel<N, 1, 128, true, 1>), dim3(grid), dim3(128), 0, s, p);
+  if (block <= 0) {  // the lag kernel (n <= 10, step_impl): -1 one 1024-thread WG per CU, 0 two 512-thread
+    if constexpr (N <= 10) {
+      if (block < 0)
+        hipLaunchKernelGGL((ref_lag_kernel<N, (N <= 5 ? 2 : 1), 1024, true>), dim3(grid), dim3(1024), 0, s, p);
+      else
+        hipLaunchKernelGGL((ref_lag_kernel<N, (N <= 5 ? 2 : 1), 512, true>), dim3(grid), dim3(512), 0, s, p);
+    }
+  } else if (block == 512) hipLaunchKernelGGL((ref_step_kernel<N, WM, 512, true>), dim3(grid), dim3(512), 0, s, p);
+  else if (block == 256) hipLaunchKernelGGL((ref_step_kernel<N, WM, 256, true>), dim3(grid), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL((ref_step_kernel<N, 1, 128, true>), dim3(grid), dim3(128), 0, s, p);
   (void)words;
 }
 using Launch = void (*)(int, int, uint32_t, hipStream_t, const StepParams&);
@@ -23,7 +29,8 @@ const Launch kTable[17] = {nullptr,      &launch_n<1>,  &launch_n<2>,  &launch_n
 }  // namespace
 
 // block/words must be one of the shapes rabia_gpu.hip picks: {512, wmax}, {256, wmax}, {128, 1};
-// block 0 = the persistent lag kernel (512 x (n <= 5 ? 2 : 1) tiles by ticket, grid = resident workgroups).
+// block <= 0 = the persistent lag kernel ((1024 | 512) x (n <= 5 ? 2 : 1) tiles by ticket, grid = resident
+// workgroups; -1: 1024 threads, 0: 512).
 void launch_ref_shard(int n, int block, int words, uint32_t grid, hipStream_t s, const StepParams& p) {
   kTable[n](block, words, grid, s, p);
 }

@@ -136,11 +136,18 @@ class ShardedRefStep:
     stages of one window on this rank's evaluator, the two row exchanges going
     through torch.distributed (all_gather_into_tensor on device rows for "nccl";
     host copies for "gloo"). Synchronous per window; bench.py pipelines the same
-    calls across windows."""
+    calls across windows.
 
-    def __init__(self, ev, rank: int, world: int, n_slots_cap: int, group=None):
+    shared_gpu=True: the ranks share one GPU (a rehearsal: one process per rank on one
+    device). Their step launches then take turns: a tiled-kernel look-back launch
+    (small shards) relies on dispatch order, and two such launches running at once on
+    one GPU can wait on each other across kernels (include/rabia_gpu.h).
+    The in-process chain of the C ABI cannot order launches of other processes."""
+
+    def __init__(self, ev, rank: int, world: int, n_slots_cap: int, group=None, shared_gpu: bool = False):
         import torch
         self.ev, self.rank, self.world, self.group = ev, rank, world, group
+        self.shared_gpu = shared_gpu
         self.cap = int(n_slots_cap)
         self.records = torch.empty(max(self.cap, 1), dtype=torch.int64, device="cuda")
         self.row = torch.zeros(10, dtype=torch.int64, device="cuda")
@@ -163,9 +170,14 @@ class ShardedRefStep:
         [window_base, window_base + window_slots); returns the global step result."""
         import torch
         ev = self.ev
-        ev.phase_step_shard_async(votes_ptr, out_ptr, n_slots, stride, shard_base, self.records.data_ptr(),
-                                  self.cap, self.row.data_ptr(), max_phase, stream)
-        torch.cuda.synchronize()
+        for r in (range(self.world) if self.shared_gpu and self.world > 1 else [self.rank]):
+            if r == self.rank:
+                ev.phase_step_shard_async(votes_ptr, out_ptr, n_slots, stride, shard_base, self.records.data_ptr(),
+                                          self.cap, self.row.data_ptr(), max_phase, stream)
+                torch.cuda.synchronize()
+            if self.shared_gpu and self.world > 1:
+                import torch.distributed as dist
+                dist.barrier(self.group)
         rows = self._gather(self.row).contiguous()
         ev.shard_fixup_async(out_ptr, n_slots, stride, shard_base, self.records.data_ptr(), self.cap,
                              rows.data_ptr(), self.rank, self.world, self.fixed.data_ptr(), max_phase, stream)

@@ -73,14 +73,15 @@ def _device_step(torch, diag, n, S, kind, seed, windows=1):
     return out, res.cpu().numpy().view(np.uint64), st
 
 
+@pytest.mark.parametrize("shape", [0, 0x400000])  # one 1024-thread WG per CU (default); 2 x 512-thread WGs per CU
 @pytest.mark.parametrize("kind", [N.RG_TRACE_AGREE90, N.RG_TRACE_SPLIT, N.RG_TRACE_UNIFORM])
-def test_lag_equals_tiled_large(kind):
-    """2^25 slots (1024 lag tiles over 512 workgroups), three windows back to back:
+def test_lag_equals_tiled_large(kind, shape):
+    """2^25 slots (512 lag tiles over 256 workgroups, or 1024 over 512), three windows back to back:
     the lag kernel's outputs, step results and engine state equal the tiled kernel's."""
     torch = torch_cuda()
     n, S = 5, 1 << 25
     o1, r1, s1 = _device_step(torch, TILED, n, S, kind, 7, windows=3)
-    o2, r2, s2 = _device_step(torch, 0, n, S, kind, 7, windows=3)
+    o2, r2, s2 = _device_step(torch, shape, n, S, kind, 7, windows=3)
     assert (r1[:, 9] == 0).all() and (r2[:, 9] == 0).all()
     assert torch.equal(o1, o2)
     assert (r1 == r2).all()
@@ -98,13 +99,16 @@ def test_lag_small_grid_large_launch():
     assert torch.equal(o1, o2) and (r1 == r2).all() and s1 == s2
 
 
-def test_lag_concurrent_contexts_two_streams():
-    """Two contexts on one GPU launch 2^26-slot REF steps on two streams at once. The
-    lag kernel takes tiles by ticket, so neither launch can wait on a workgroup that
-    the other holds off the GPU (the tiled kernel's cross-kernel look-back cycle):
-    both finish with flags 0 and outputs equal to serial runs."""
+@pytest.mark.parametrize("S", [1 << 26, 1 << 23])
+def test_lag_concurrent_contexts_two_streams(S):
+    """Two contexts on one GPU launch REF steps on two streams at once. At 2^26 slots
+    the lag kernel takes tiles by ticket, so neither launch can wait on a workgroup
+    that the other holds off the GPU (the tiled kernel's cross-kernel look-back
+    cycle); at 2^23 slots the tiled kernel runs and the C ABI chains the two contexts'
+    launches through its per-device event. Both finish with flags 0 and outputs equal
+    to serial runs."""
     torch = torch_cuda()
-    n, S = 5, 1 << 26
+    n = 5
     stride = ((S + 127) // 128) * 4
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
     votes = [torch.empty((4 * n + 1) * stride, dtype=torch.int32, device="cuda") for _ in range(2)]

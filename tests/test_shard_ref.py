@@ -247,7 +247,7 @@ def _rank(rank, world, port, q):
         torch.cuda.synchronize()
         with PE(n, self_lane=2, seed=42) as ev:  # the same engine seed on every rank
             ev.trace_generate_async(1, 9, 1 + start, cnt, stride, votes.data_ptr())
-            drv = SH.ShardedRefStep(ev, rank, world, cnt)
+            drv = SH.ShardedRefStep(ev, rank, world, cnt, shared_gpu=True)  # both ranks on the one GPU
             g = drv.step(votes.data_ptr(), out.data_ptr(), cnt, stride, 1 + start, 1, S)
             st = ev.get_state()
         planes = out.view(8, stride).cpu().numpy().view(np.uint32)
@@ -258,7 +258,9 @@ def _rank(rank, world, port, q):
 
 def test_two_process_gloo(oracle):
     """Two ranks (processes) on the one GPU, rows exchanged over gloo: the folded
-    global result and every rank's state == the oracle's single engine."""
+    global result and every rank's state == the oracle's single engine. The ranks'
+    step launches take turns (ShardedRefStep shared_gpu: the rule of include/rabia_gpu.h
+    for tiled-kernel look-back launches of different processes on one device)."""
     torch_cuda()
     import torch.multiprocessing as mp
     world = 2

@@ -2,7 +2,7 @@
 # Experiment builds of librabia_gpu.so (A/B via RABIA_GPU_LIB, tools/ab_variants.py).
 set -e
 cd "$(dirname "$0")/.."
-rm -f rabia_amd/lib/variants/*.so
+mkdir -p rabia_amd/lib/variants && rm -f rabia_amd/lib/variants/*.so
 for v in "$@"; do
   name=${v%%:*}; defs=${v#*:}
   args=()

@@ -12,7 +12,7 @@ timeout -k 10 900 python -u -m pytest tests/test_lag_kernel.py -m gpu -x -v --ti
   > $OUT/${TAG}_tests.log 2>&1 || { echo "lag tests failed"; tail -60 $OUT/${TAG}_tests.log; exit 1; }
 tail -3 $OUT/${TAG}_tests.log
 for S in 268435456 1073741824; do
-  AB_SLOTS=$S AB_DIAGS="tiled:0x100000" AB_ROUNDS=3 timeout -k 10 600 python -u tools/ab_variants.py \
+  AB_SLOTS=$S AB_DIAGS=${AB_DIAGS:-"tiled:0x100000,l1024:0x400000"} AB_ROUNDS=3 timeout -k 10 600 python -u tools/ab_variants.py \
     > $OUT/${TAG}_ab_$S.json 2> $OUT/${TAG}_ab_$S.err || { echo "A/B failed"; tail -30 $OUT/${TAG}_ab_$S.err; exit 1; }
   cat $OUT/${TAG}_ab_$S.json
 done

@@ -30,7 +30,7 @@ for i in range(8):
 torch.cuda.synchronize()
 
 variants = {}
-for shape, force in (("auto", 0), ("512x4", 1), ("256x4", 2), ("128x1", 3), ("512x2", 4), ("256x2", 5)):
+for shape, force in (("auto", 0), ("512x4", 1), ("256x4", 2), ("128x1", 3)):
     for tag, d in (("", 0), ("_no_lookback", 1), ("_no_stats", 2), ("_neither", 3)):
         variants[shape + tag] = (force << 8) | d
 times = {k: [] for k in variants}
