@@ -481,8 +481,8 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
   p.out_bytes = need_out * 4;
   p.vq_rec = reinterpret_cast<unsigned long long*>(records_dev);
   p.vq_cap = records_cap;
-  if (ctx->diag & 4u) {  // stamps: [n_tiles][8] (tiled kernel) or [grid][12] (lag kernel)
-    const uint64_t words = lag && 12ull * lag_grid > 8 * n_tiles ? 12ull * lag_grid : 8 * n_tiles;
+  if (ctx->diag & 4u) {  // stamps: [n_tiles][8] (tiled kernel) or [grid][16] (lag kernel)
+    const uint64_t words = lag && 16ull * lag_grid > 8 * n_tiles ? 16ull * lag_grid : 8 * n_tiles;
     if (ctx->dbg_cap < words) {
       RG_HIP(ctx, hipDeviceSynchronize());
       (void)hipFree(ctx->dbg);

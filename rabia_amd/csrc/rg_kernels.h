@@ -207,13 +207,21 @@ __device__ __forceinline__ unsigned long long wave_min64(unsigned long long v) {
   }
   return v;
 }
-__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t v, int lane) {
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    uint32_t t = __shfl_up(v, o, 64);
-    if (lane >= o) v += t;
-  }
+// Inclusive prefix within each 16-lane row: DPP row shifts (zero fill), no LDS
+// round trip (a __shfl_up ladder is six ds_bpermute + lgkmcnt waits).
+__device__ __forceinline__ uint32_t row_incl_scan32(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);  // row_shr:8
   return v;
+}
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t v, int lane) {
+  v = row_incl_scan32(v);
+  const uint32_t r0 = __builtin_amdgcn_readlane(v, 15), r1 = __builtin_amdgcn_readlane(v, 31),
+                 r2 = __builtin_amdgcn_readlane(v, 47);
+  const int row = lane >> 4;
+  return v + (row >= 1 ? r0 : 0u) + (row >= 2 ? r1 : 0u) + (row >= 3 ? r2 : 0u);
 }
 
 __device__ __forceinline__ unsigned long long atomic_load_agent(unsigned long long* p) {
@@ -374,10 +382,10 @@ __device__ __forceinline__ unsigned long long stat_tag(uint32_t seq) {
   return (unsigned long long)(0x1000u | (seq & 0xFFFu)) << 51;
 }
 
-__device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {  // (wave-uniform result)
+  v = row_incl_scan32(v);
+  return __builtin_amdgcn_readlane(v, 15) + __builtin_amdgcn_readlane(v, 31) + __builtin_amdgcn_readlane(v, 47) +
+         __builtin_amdgcn_readlane(v, 63);
 }
 __device__ __forceinline__ uint32_t wave_max32(uint32_t v) {
 #pragma unroll
@@ -1025,6 +1033,48 @@ __device__ __forceinline__ void lds_st(uint32_t* s, const uint32_t (&v)[W]) {
   }
 }
 
+// ChaCha block computed by the 4 lanes of a quad (rand_chacha 0.3.1 layout, as
+// chacha_block): lane q holds column q (words q, 4+q, 8+q, 12+q), so a column round
+// is one quarter round per lane; for a diagonal round lane q takes rows b, c, d from
+// lanes q+1, q+2, q+3 of its quad (DPP quad permutes) and hands them back after it.
+// A quarter of the dependent-instruction chain of one lane per block. Every lane of
+// a quad must be active.
+__device__ __forceinline__ uint32_t quad_rot(uint32_t v, int by) {  // lane q <- lane (q + by) & 3
+  if (by == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x39, 0xF, 0xF, false);
+  if (by == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x93, 0xF, 0xF, false);
+}
+template <int ROUNDS>
+__device__ __forceinline__ void chacha_block_quad(const Key& key, uint64_t counter, uint64_t stream, int q,
+                                                  uint32_t (&o)[4]) {
+  // the key words as wave-uniform values first: selecting among struct fields by a
+  // lane index otherwise becomes a per-lane load from the kernel arguments (a vector
+  // memory load whose wait covers every plane load in flight)
+  uint32_t k[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) k[i] = __builtin_amdgcn_readfirstlane(key.k[i]);
+  const uint32_t a0 = q == 0 ? 0x61707865u : (q == 1 ? 0x3320646eu : (q == 2 ? 0x79622d32u : 0x6b206574u));
+  const uint32_t b0 = q == 0 ? k[0] : (q == 1 ? k[1] : (q == 2 ? k[2] : k[3]));
+  const uint32_t c0 = q == 0 ? k[4] : (q == 1 ? k[5] : (q == 2 ? k[6] : k[7]));
+  const uint32_t d0 = q == 0 ? (uint32_t)counter
+                             : (q == 1 ? (uint32_t)(counter >> 32) : (q == 2 ? (uint32_t)stream : (uint32_t)(stream >> 32)));
+  uint32_t a = a0, b = b0, c = c0, d = d0;
+#define RG_QR1()                                  \
+  a += b; d = rotl32(d ^ a, 16);                  \
+  c += d; b = rotl32(b ^ c, 12);                  \
+  a += b; d = rotl32(d ^ a, 8);                   \
+  c += d; b = rotl32(b ^ c, 7);
+#pragma unroll
+  for (int r = 0; r < ROUNDS; r += 2) {
+    RG_QR1()
+    b = quad_rot(b, 1); c = quad_rot(c, 2); d = quad_rot(d, 3);
+    RG_QR1()
+    b = quad_rot(b, 3); c = quad_rot(c, 2); d = quad_rot(d, 1);
+  }
+#undef RG_QR1
+  o[0] = a + a0; o[1] = b + b0; o[2] = c + c0; o[3] = d + d0;
+}
+
 // Plane access of the lag kernel through buffer resources: the tile's uniform base in
 // SGPRs, the thread's offset in ONE VGPR for every plane, the plane offset in an SGPR
 // (a global load needs a 64-bit VGPR address per plane: 20 of them in flight at n = 5).
@@ -1100,7 +1150,7 @@ template <int N, int W, int BLOCK, bool SHARD>
 __global__ __launch_bounds__(BLOCK, 4) void ref_lag_kernel(StepParams p) {  // 4 waves/SIMD: 2 x 512 or 1 x 1024 per CU
   constexpr int B = ctr_bits(N);
   constexpr int WAVES = BLOCK / 64;
-  constexpr int kRows = BLOCK < 128 ? BLOCK : 128;
+  constexpr int kRows = BLOCK / 4;  // ChaCha12 blocks per pass, one per quad of lanes
   constexpr uint32_t kTW = (uint32_t)BLOCK * W;  // words per tile
   __shared__ __attribute__((aligned(16))) uint32_t s_park[2][kParkFields][BLOCK][W];
   __shared__ uint32_t s_blk[kRows][17];  // ChaCha12 blocks of the parked tile's draws (+1 word: no conflicts)
@@ -1117,9 +1167,10 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_lag_kernel(StepParams p) {  // 4
   // diag & 4: per-workgroup phase times (s_memrealtime, 100 MHz) -> p.dbg[blockIdx.x][12]:
   //   0 start->loop, 1 tally (incl. the round-1 wait), 2 scan barrier, 3 decisions (incl.
   //   the round-2 wait), 4 draws of the parked tile, 5 its stores, 6 loop end->record, 7 iterations,
-  //   [8] look-back completion inside the draws, [9] continued look-backs, [10] start, [11] end (absolute)
+  //   [8] look-back completion inside the draws, [9] continued look-backs, [10] start, [11] end (absolute),
+  //   inside the draws (thread 0): [12] ChaCha blocks, [13] the barrier after them, [14] the selection loop
   const bool stamps = (p.diag & 4u) != 0;
-  unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // [8] look-back completion, [9] continued
+  unsigned long long st_acc[13] = {};  // [8] look-back completion, [9] continued, [10-12] draws split
   unsigned long long st_t = stamps ? __builtin_amdgcn_s_memrealtime() : 0;
   const unsigned long long st_begin = st_t;
   auto lap = [&](int k) {
@@ -1185,8 +1236,8 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_lag_kernel(StepParams p) {  // 4
   // issues the same memory operations) with the round-1 planes' wait, evaluates them
   // after the tally, and the waves' results combine after the scan barrier.
   constexpr int kPollWaves = WAVES < 8 ? WAVES : 8;  // 512 granules per poll (waves 8-15 repeat 0-7)
-  auto lb_poll = [&]() -> unsigned long long {
-    const int32_t idx = park_tile - 1 - (64 * (wave % kPollWaves) + lane);
+  auto lb_poll = [&](int32_t tile) -> unsigned long long {
+    const int32_t idx = tile - 1 - (64 * (wave % kPollWaves) + lane);
     return atomic_load_agent(p.lookback + (idx > prev_tile ? idx : 0));
   };
   auto lb_eval = [&](unsigned long long g) {
@@ -1218,7 +1269,24 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_lag_kernel(StepParams p) {  // 4
     return false;  // every polled granule was an aggregate: continue further back
   };
 
+  // ChaCha12 blocks cb .. min(cb + kRows, b_last + 1) - 1 into s_blk, block r by the
+  // lanes 4r .. 4r + 3 (quad-uniform condition)
+  auto chacha_rows = [&](unsigned long long cb, unsigned long long b_last) {
+    const uint32_t r = (uint32_t)tid >> 2;
+    if (cb + r <= b_last) {
+      uint32_t o[4];
+      chacha_block_quad<12>(p.key, cb + r, 0, tid & 3, o);
+      const int q = tid & 3;
+      s_blk[r][q] = o[0];
+      s_blk[r][4 + q] = o[1];
+      s_blk[r][8 + q] = o[2];
+      s_blk[r][12 + q] = o[3];
+    }
+  };
+
   // Draws of the parked tile: own round-2 votes of its VQ slots (bits set = V1).
+  // (Its ChaCha blocks computed right after the scan barrier instead, while the
+  // round-2 planes are in flight: 727 vs 713 us per 2^30 slots, not kept.)
   auto draw_parked = [&](uint32_t (&own)[W]) {
     uint32_t(&pp)[kParkFields][BLOCK][W] = s_park[pk ^ 1u];
     uint32_t excl;
@@ -1254,13 +1322,10 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_lag_kernel(StepParams p) {  // 4
       unsigned long long k = k_tile + park_thr;
       const unsigned long long b_first = k_tile >> 3, b_last = (k_tile + park_total - 1) >> 3;
       for (unsigned long long cb = b_first; cb <= b_last; cb += kRows) {
-        if (tid < kRows && cb + tid <= b_last) {
-          uint32_t x[16];
-          chacha_block<12>(p.key, cb + tid, 0, x);
-#pragma unroll
-          for (int j = 0; j < 16; j++) s_blk[tid][j] = x[j];
-        }
+        chacha_rows(cb, b_last);
+        lap(10);
         lds_barrier();
+        lap(11);
         const unsigned long long k_lim = (cb + kRows) << 3;
 #pragma unroll
         for (int i = 0; i < W; i++) {
@@ -1278,6 +1343,7 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_lag_kernel(StepParams p) {  // 4
             k++;
           }
         }
+        lap(12);
         lds_barrier();
       }
     }
@@ -1391,12 +1457,17 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_lag_kernel(StepParams p) {  // 4
     uint32_t voff0 = any ? in_off(c) : 0u;
     LAG_CHK_IN(any ? c : 0u, voff0, 2 * N);
     buf_ld_planes<N, W>(in_rsrc(any ? c : 0u), voff0, in_pb, 0, r1lo, r1hi);
+#ifdef RG_POLL_EARLY
+    lbg = lb_poll(park_tile);  // no parked tile yet: a harmless poll
+#endif
     buf_ld_planes<N, W>(in_rsrc(any ? c : 0u), voff0, in_pb, 2 * N, r2lo, r2hi);
     const uint32_t z[W] = {};
     const __amdgpu_buffer_rsrc_t orr = out_rsrc(0u);
 #pragma unroll
     for (int k = 0; k < 5; k++) buf_st<W>(orr, kOffNone, (uint32_t)k * 4u, z);
-    lbg = lb_poll();  // no parked tile yet: a harmless poll
+#ifndef RG_POLL_EARLY
+    lbg = lb_poll(park_tile);  // no parked tile yet: a harmless poll
+#endif
   }
   lap(0);
   while (c < p.n_tiles) {
@@ -1475,12 +1546,16 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_lag_kernel(StepParams p) {  // 4
       atomic_store_agent(p.lookback + c, ((unsigned long long)(c == 0 ? tag_inc : tag_agg) << 32) | total);
       if (nx < p.n_tiles) nt = take_ticket(rec);
     }
+
     // (3) the next tile's round-1 planes in flight (past the last tile: tile c's first word)
     const bool more = nx < p.n_tiles;
     const __amdgpu_buffer_rsrc_t nrr = in_rsrc(more ? nx : c);
     uint32_t noff = more ? in_off(nx) : 0u;
     LAG_CHK_IN(more ? nx : c, noff, 2 * N);
     buf_ld_planes<N, W>(nrr, noff, in_pb, 0, r1lo, r1hi);
+#ifdef RG_POLL_EARLY  // experiment: tile c's look-back poll ahead of the next round-2 loads
+    lbg = lb_poll((int32_t)c);
+#endif
     // (4) round-2 decisions of tile c for both own votes (engine.rs:540-542, 613-628);
     //     then the next tile's round-2 planes in flight
     {
@@ -1515,7 +1590,9 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_lag_kernel(StepParams p) {  // 4
     park_tile = (int32_t)c;  // tile c is parked; its look-back poll (prev_tile: the tile just finished)
     park_total = total;
     park_thr = wave_off + incl - vq_count;
-    lbg = lb_poll();
+#ifndef RG_POLL_EARLY
+    lbg = lb_poll(park_tile);
+#endif
     pk ^= 1u;
     c = nx;
   }
@@ -1539,9 +1616,10 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_lag_kernel(StepParams p) {  // 4
     if (stamps && tid == 0) {
       lap(6);
 #pragma unroll
-      for (int k = 0; k < 10; k++) p.dbg[(uint64_t)blockIdx.x * 12 + k] = st_acc[k];
-      p.dbg[(uint64_t)blockIdx.x * 12 + 10] = st_begin;
-      p.dbg[(uint64_t)blockIdx.x * 12 + 11] = st_t;
+      for (int k = 0; k < 10; k++) p.dbg[(uint64_t)blockIdx.x * 16 + k] = st_acc[k];
+      p.dbg[(uint64_t)blockIdx.x * 16 + 10] = st_begin;
+      p.dbg[(uint64_t)blockIdx.x * 16 + 11] = st_t;
+      for (int k = 10; k < 13; k++) p.dbg[(uint64_t)blockIdx.x * 16 + k + 2] = st_acc[k];
     }
     if (tid == 0) {
       unsigned long long t[kLagStatGranules] = {0, 0, 0, 0, 0, 0xFFFFFFFFull};

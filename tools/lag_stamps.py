@@ -42,15 +42,17 @@ def main():
             ts.append(e0.elapsed_time(e1) * 1000.0)
         out[name + "_us"] = float(np.median(ts[2:]))
     grid = 512 if extra & 0x400000 else 256  # 2 x 512 (diag bit 22) or 1 x 1024 per CU
-    buf = np.zeros(grid * 12, dtype=np.uint64)
+    buf = np.zeros(grid * 16, dtype=np.uint64)
     N.check(ev.lib.rg_debug_stamps(ev.ctx, buf.ctypes.data, buf.size), ev.ctx)
-    d = buf.reshape(grid, 12).astype(np.float64)
+    d = buf.reshape(grid, 16).astype(np.float64)
     it = d[:, 7]
     ph = {PHASES[k]: float(np.sum(d[:, k]) / max(np.sum(it), 1) * 0.01) for k in range(1, 6)}  # us per iteration
     ph["draws.lookback_part"] = float(np.sum(d[:, 8]) / max(np.sum(it), 1) * 0.01)
+    for k, nm in ((12, "draws.chacha"), (13, "draws.chacha_barrier"), (14, "draws.select")):
+        ph[nm] = float(np.sum(d[:, k]) / max(np.sum(it), 1) * 0.01)
     out["continued_lookbacks_frac"] = float(np.sum(d[:, 9]) / max(np.sum(it), 1))
     out["per_iteration_us"] = ph
-    out["per_iteration_total_us"] = sum(v for k, v in ph.items() if "." not in k)
+    out["per_iteration_total_us"] = sum(ph.values())  # "draws" is what the "draws.*" parts leave
     out["iterations_per_wg"] = {"min": int(it.min()), "max": int(it.max()), "mean": float(it.mean())}
     t0 = d[:, 10].min()
     out["start_spread_us"] = float((d[:, 10].max() - t0) * 0.01)
