@@ -1457,17 +1457,12 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_lag_kernel(StepParams p) {  // 4
     uint32_t voff0 = any ? in_off(c) : 0u;
     LAG_CHK_IN(any ? c : 0u, voff0, 2 * N);
     buf_ld_planes<N, W>(in_rsrc(any ? c : 0u), voff0, in_pb, 0, r1lo, r1hi);
-#ifdef RG_POLL_EARLY
-    lbg = lb_poll(park_tile);  // no parked tile yet: a harmless poll
-#endif
     buf_ld_planes<N, W>(in_rsrc(any ? c : 0u), voff0, in_pb, 2 * N, r2lo, r2hi);
     const uint32_t z[W] = {};
     const __amdgpu_buffer_rsrc_t orr = out_rsrc(0u);
 #pragma unroll
     for (int k = 0; k < 5; k++) buf_st<W>(orr, kOffNone, (uint32_t)k * 4u, z);
-#ifndef RG_POLL_EARLY
     lbg = lb_poll(park_tile);  // no parked tile yet: a harmless poll
-#endif
   }
   lap(0);
   while (c < p.n_tiles) {
@@ -1553,9 +1548,6 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_lag_kernel(StepParams p) {  // 4
     uint32_t noff = more ? in_off(nx) : 0u;
     LAG_CHK_IN(more ? nx : c, noff, 2 * N);
     buf_ld_planes<N, W>(nrr, noff, in_pb, 0, r1lo, r1hi);
-#ifdef RG_POLL_EARLY  // experiment: tile c's look-back poll ahead of the next round-2 loads
-    lbg = lb_poll((int32_t)c);
-#endif
     // (4) round-2 decisions of tile c for both own votes (engine.rs:540-542, 613-628);
     //     then the next tile's round-2 planes in flight
     {
@@ -1590,9 +1582,8 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_lag_kernel(StepParams p) {  // 4
     park_tile = (int32_t)c;  // tile c is parked; its look-back poll (prev_tile: the tile just finished)
     park_total = total;
     park_thr = wave_off + incl - vq_count;
-#ifndef RG_POLL_EARLY
-    lbg = lb_poll(park_tile);
-#endif
+    lbg = lb_poll(park_tile);  // (issued ahead of the next round-2 loads instead: 877 vs 705 us per 2^30
+                               // slots, its predecessors not yet published: continued look-backs)
     pk ^= 1u;
     c = nx;
   }
