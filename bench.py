@@ -92,7 +92,13 @@ def parse():
     ap.add_argument("--config", choices=["c2", "c3", "c5"], default="c2",
                     help="c2: the headline (weak scaling); c5: 9 replicas x 2^26 slots per step split over the "
                          "ranks (strong scaling) with the decision bitmaps all-gathered every step")
-    ap.add_argument("--c5-windows", type=int, default=64, help="C5: 2^20-slot windows per step, all ranks")
+    ap.add_argument("--c5-windows", type=int, default=64, help="C5: 2^20-slot windows per C5 window, all ranks")
+    ap.add_argument("--c5-batch", type=int, default=8,
+                    help="C5 sharded pipeline: consecutive C5 windows per shard-step launch (a bench step)")
+    ap.add_argument("--c5-sharded", action="store_true",
+                    help="C5 on 1 GPU: run the sharded pipeline (shard step + fix-up + commit) with one shard")
+    ap.add_argument("--diag", type=lambda x: int(x, 0), default=0,
+                    help="rg_debug_set switches for experiments (include/rabia_gpu_debug.h); 0 = the product path")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl = RCCL over xGMI; gloo = several ranks on one GPU (rehearsal only)")
     return ap.parse_args()
@@ -284,6 +290,8 @@ def run_single(a, n, S, label):
     torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
     ev = PhaseEvaluator(n, self_lane=n - 1, mode="ref", seed=SEED, tile_words=T)
+    if a.diag:
+        N.check(ev.lib.rg_debug_set(ev.ctx, a.diag), ev.ctx)
     sets = []
     for i in range(a.sets):
         votes = torch.empty(in_words, dtype=torch.int32, device="cuda")
@@ -354,80 +362,105 @@ def make_gather(dist, backend):
 
 
 def run_sharded(a, n, S, window_slots, world, rank, dist, bitmaps):
+    """One engine over windows split into `world` contiguous shards. A step is K =
+    a.c5_batch consecutive windows: every rank's shard step runs the K windows' shards
+    in ONE launch (rg_phase_step_shard_windows_async; K = 1: rg_phase_step_shard_async),
+    then per window: rows all-gathered, fix-up, final rows all-gathered, commit, and
+    (C5) the committed/V1 bitmaps all-gathered, on a second stream. world = 1 runs the
+    same pipeline with one shard (the 1-GPU measurement of a shard-size step)."""
     T = a.tile_words
-    gather = make_gather(dist, a.backend)
+    K = max(1, a.c5_batch)
+    gather = make_gather(dist, a.backend) if world > 1 else (lambda out, inp: out.copy_(inp.unsqueeze(0)))
     stride, in_words, out_words = layout(n, S, T)
     comp = torch.cuda.Stream()
     fix = torch.cuda.Stream()
     torch.cuda.set_stream(comp)
     ev = PhaseEvaluator(n, self_lane=n - 1, mode="ref", seed=SEED, tile_words=T)  # one seed on every rank
-    cap = max(S // 8, 1 << 16)  # draw records per shard step (agree90: ~1 % of slots are VQ); overflow -> flags
+    if a.diag:
+        N.check(ev.lib.rg_debug_set(ev.ctx, a.diag), ev.ctx)
+    cap = max(S // 8, 1 << 16)  # draw records per shard window (agree90: ~1 % of slots are VQ); overflow -> flags
     sets = []
     start = rank * S
     for i in range(a.sets):
-        votes = torch.empty(in_words, dtype=torch.int32, device="cuda")
-        out = torch.empty(out_words, dtype=torch.int32, device="cuda")
-        rec = torch.empty(cap, dtype=torch.int64, device="cuda")
-        ev.trace_generate_async(N.RG_TRACE_AGREE90, 1000 + i, 1 + i * window_slots + start, S, stride,
-                                votes.data_ptr(), comp.cuda_stream)
+        votes = torch.empty(K * in_words, dtype=torch.int32, device="cuda")
+        out = torch.empty(K * out_words, dtype=torch.int32, device="cuda")
+        rec = torch.empty(K * cap, dtype=torch.int64, device="cuda")
+        for k in range(K):
+            ev.trace_generate_async(N.RG_TRACE_AGREE90, 1000 + i * K + k, 1 + (i * K + k) * window_slots + start, S,
+                                    stride, votes.data_ptr() + 4 * k * in_words, comp.cuda_stream)
         sets.append((votes, out, rec))
     n_total = a.warmup + a.steps
     i64 = dict(dtype=torch.int64, device="cuda")
-    rows = torch.zeros((n_total, 10), **i64)
-    g_rows = torch.zeros((n_total, world, 10), **i64)
-    fixed = torch.zeros((n_total, 10), **i64)
-    g_fixed = torch.zeros((n_total, world, 10), **i64)
-    result = torch.zeros((n_total, 10), **i64)
+    rows = torch.zeros((n_total, K, 10), **i64)
+    g_rows = torch.zeros((n_total, K, world, 10), **i64)
+    fixed = torch.zeros((n_total, K, 10), **i64)
+    g_fixed = torch.zeros((n_total, K, world, 10), **i64)
+    result = torch.zeros((n_total, K, 10), **i64)
     nw = (S + 31) // 32
     if bitmaps:
-        bm = torch.zeros((n_total, 2, nw), dtype=torch.int32, device="cuda")
-        bm_all = torch.zeros((n_total, world, 2, nw), dtype=torch.int32, device="cuda")
+        bm = torch.zeros((n_total, K, 2, nw), dtype=torch.int32, device="cuda")
+        bm_all = torch.zeros((n_total, K, world, 2, nw), dtype=torch.int32, device="cuda")
     torch.cuda.synchronize()
     e_main = [torch.cuda.Event() for _ in range(n_total)]
     e_done = [torch.cuda.Event() for _ in range(n_total)]
 
+    def shard_step(votes, out, rec, base, t):
+        if K == 1:
+            ev.phase_step_shard_async(votes.data_ptr(), out.data_ptr(), S, stride, base + start, rec.data_ptr(), cap,
+                                      rows[t, 0].data_ptr(), stream=comp.cuda_stream)
+        else:
+            ev.phase_step_shard_windows_async(K, votes.data_ptr(), in_words, out.data_ptr(), out_words, S, stride,
+                                              base + start, window_slots, rec.data_ptr(), cap, rows[t].data_ptr(),
+                                              stream=comp.cuda_stream)
+
     def step(t, evs=None):
         votes, out, rec = sets[t % a.sets]
-        base = 1 + t * window_slots
-        if t >= a.sets:  # the output buffer and records of window t - sets must be fixed up first
+        base = 1 + t * K * window_slots
+        if t >= a.sets:  # the output buffers and records of step t - sets must be fixed up first
             comp.wait_event(e_done[t - a.sets])
         if evs is not None:
             evs[0].record(comp)
         if a.backend == "gloo" and world > 1:
-            # Rehearsal: the ranks share one GPU, and two look-back launches running at
-            # once on one GPU can wait on each other across kernels (each holds CUs its
-            # partner's predecessors need: the bounded spin then flags a fault). Real
-            # runs have one GPU per rank. So the ranks' step kernels take turns here.
+            # Rehearsal: the ranks share one GPU, and two tiled-kernel look-back launches
+            # of different processes running at once on one GPU can wait on each other
+            # across kernels (include/rabia_gpu.h). Real runs have one GPU per rank. So
+            # the ranks' step kernels take turns here.
             for r in range(world):
                 if r == rank:
-                    ev.phase_step_shard_async(votes.data_ptr(), out.data_ptr(), S, stride, base + start,
-                                              rec.data_ptr(), cap, rows[t].data_ptr(), stream=comp.cuda_stream)
+                    shard_step(votes, out, rec, base, t)
                     comp.synchronize()
                 dist.barrier()
         else:
-            ev.phase_step_shard_async(votes.data_ptr(), out.data_ptr(), S, stride, base + start, rec.data_ptr(), cap,
-                                      rows[t].data_ptr(), stream=comp.cuda_stream)
+            shard_step(votes, out, rec, base, t)
         if evs is not None:
             evs[1].record(comp)
         e_main[t].record(comp)
         with torch.cuda.stream(fix):
             fix.wait_event(e_main[t])
-            gather(g_rows[t], rows[t])
-            ev.shard_fixup_async(out.data_ptr(), S, stride, base + start, rec.data_ptr(), cap, g_rows[t].data_ptr(),
-                                 rank, world, fixed[t].data_ptr(), stream=fix.cuda_stream)
-            gather(g_fixed[t], fixed[t])
-            ev.shard_commit_async(g_fixed[t].data_ptr(), world, base, window_slots, result[t].data_ptr(),
-                                  stream=fix.cuda_stream)
-            if bitmaps:
-                ev.decision_bitmap_async(out.data_ptr(), S, stride, bm[t, 0].data_ptr(), bm[t, 1].data_ptr(),
-                                         fix.cuda_stream)
-                gather(bm_all[t], bm[t])
+            for k in range(K):
+                bk = base + k * window_slots
+                o_k = out.data_ptr() + 4 * k * out_words
+                gather(g_rows[t, k], rows[t, k])
+                ev.shard_fixup_async(o_k, S, stride, bk + start, rec.data_ptr() + 8 * k * cap, cap,
+                                     g_rows[t, k].data_ptr(), rank, world, fixed[t, k].data_ptr(),
+                                     stream=fix.cuda_stream)
+                gather(g_fixed[t, k], fixed[t, k])
+                ev.shard_commit_async(g_fixed[t, k].data_ptr(), world, bk, window_slots, result[t, k].data_ptr(),
+                                      stream=fix.cuda_stream)
+                if bitmaps:
+                    ev.decision_bitmap_async(o_k, S, stride, bm[t, k, 0].data_ptr(), bm[t, k, 1].data_ptr(),
+                                             fix.cuda_stream)
+                    gather(bm_all[t, k], bm[t, k])
             e_done[t].record(fix)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
 
     for t in range(a.warmup):
         step(t)
     torch.cuda.synchronize()
-    dist.barrier()
+    barrier()
     torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
     t_begin, t_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -437,28 +470,30 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, bitmaps):
     comp.wait_event(e_done[n_total - 1])
     t_end.record(comp)
     torch.cuda.synchronize()
-    dist.barrier()
+    barrier()
     torch.cuda.synchronize()
     total_ms = t_begin.elapsed_time(t_end)
     kern_ms = float(np.mean([b.elapsed_time(e) for b, e in evs]))
-    res = result.cpu().numpy().view(np.uint64)
-    fx = fixed.cpu().numpy().view(np.uint64)
+    res = result.reshape(-1, 10).cpu().numpy().view(np.uint64)
+    fx = fixed.reshape(-1, 10).cpu().numpy().view(np.uint64)
     if int(res[:, 9].max()) != 0 or int(fx[:, 9].max()) != 0:
         raise RuntimeError("device-side fault flagged in a step result (1/2 look-back/fold timeout, 4 stale record "
                            f"ring, 8 draw-record overflow): result flags {sorted(set(res[:, 9].tolist()))}, shard "
                            f"flags {sorted(set(fx[:, 9].tolist()))}, rows flags "
-                           f"{sorted(set(rows.cpu().numpy().view(np.uint64)[:, 9].tolist()))}")
-    timed = res[a.warmup:]
+                           f"{sorted(set(rows.reshape(-1, 10).cpu().numpy().view(np.uint64)[:, 9].tolist()))}")
+    timed = res[a.warmup * K:]
     assert (timed[:, 0] == window_slots).all(), "a timed window did not complete"
     decided = int(timed[:, 1].sum())  # global (every shard), identical on every rank
     if bitmaps:  # the gathered committed bitmaps carry exactly the folded decided count
         b_all = bm_all[a.warmup:].cpu().numpy().view(np.uint32)
-        pop = int(np.unpackbits(b_all[:, :, 0].view(np.uint8)).sum())
+        pop = int(np.unpackbits(b_all[:, :, :, 0].view(np.uint8)).sum())
         assert pop == decided, (pop, decided)
-    tm = torch.tensor([total_ms, kern_ms], dtype=torch.float64, device="cuda" if a.backend == "nccl" else "cpu")
-    dist.all_reduce(tm, op=dist.ReduceOp.MAX)
-    return {"total_ms": float(tm[0]), "kern_ms": float(tm[1]), "decided": decided, "sweep_us": None, "ev": ev,
-            "stream": comp}
+    if dist is not None:
+        tm = torch.tensor([total_ms, kern_ms], dtype=torch.float64, device="cuda" if a.backend == "nccl" else "cpu")
+        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+        total_ms, kern_ms = float(tm[0]), float(tm[1])
+    return {"total_ms": total_ms, "kern_ms": kern_ms, "decided": decided, "sweep_us": None, "ev": ev,
+            "stream": comp, "windows_per_launch": K}
 
 
 # ---------------------------------------------------------------------------
@@ -589,22 +624,25 @@ def main():
     else:
         n, S = a.replicas, a.windows * WINDOW
         window_slots = S * world
-    if world == 1:
+    if world == 1 and not (a.config == "c5" and a.c5_sharded):
         r = run_single(a, n, S, a.config)
     else:
         r = run_sharded(a, n, S, window_slots, world, rank, dist, bitmaps=a.config == "c5")
+    K = r.get("windows_per_launch", 1)
     if rank == 0:
         value = r["decided"] / (r["total_ms"] / 1000.0)
-        alg_bytes = S * bytes_per_slot_ref(n)
+        alg_bytes = K * S * bytes_per_slot_ref(n)
         achieved = alg_bytes / (r["kern_ms"] / 1000.0) / 1e9
         cpu = None if (a.no_cpu_baseline or world > 1) else cpu_baseline(
             a, n, r["ev"], r["stream"], windows=256 if a.config == "c2" else a.c5_windows)
-        par = f"slot-shard x{world}" + (", one engine: sharded draws + fix-up" if world > 1 else "")
+        sharded = "windows_per_launch" in r
+        par = f"slot-shard x{world}" + (f", one engine: sharded draws + fix-up, {K} C5 windows per shard launch"
+                                        if sharded else "")
         if a.config == "c5":
             metric = "consensus slots decided/sec (9 replicas, 2^26 slots per step, bitmap all-gather)"
-            workload = (f"C5: {n} replicas x {window_slots} slots per step (one engine), REF sweep split over "
-                        f"{world} GPU(s)" + (", committed + V1 bitmaps and shard rows all-gathered every step"
-                                             if world > 1 else ""))
+            workload = (f"C5: {n} replicas x {window_slots}-slot windows, {K} per step (one engine), REF sweep "
+                        f"split over {world} GPU(s)" + (", committed + V1 bitmaps and shard rows all-gathered per "
+                                                        "window" if sharded else ""))
             scaling = "strong"
         else:
             metric = "consensus slots decided/sec (5 replicas, 1M slots) + HBM GB/s as % of peak"
@@ -625,7 +663,7 @@ def main():
             "dtype": "u32 bit-sliced 2-bit vote codes (integer only)",
             "data": "synthetic (seeded agree90 vote trace generated on device)",
             "config": {"workload": workload, "replicas": n, "slots_per_window": WINDOW,
-                       "slots_per_step_per_gpu": S, "slots_per_step": window_slots, "mode": "ref",
+                       "slots_per_step_per_gpu": K * S, "slots_per_step": K * window_slots, "mode": "ref",
                        "layout": f"slot-tiled {a.tile_words}" if a.tile_words else "planar", "parallelism": par},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,

@@ -183,6 +183,23 @@ int rg_phase_step_shard_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* 
                               uint64_t n_slots, uint64_t stride_words, uint64_t slot_base,
                               uint64_t max_phase, uint64_t* records_dev, uint64_t records_cap,
                               rg_step_result* row_dev, void* stream);
+/* Stage (1) for n_windows consecutive windows of this shard in ONE launch (the shard
+ * step's fixed ramp/drain cost is paid once, not per window): window w's shard is
+ * [slot_base + w * window_stride, + n_slots), its planes at votes_dev + w *
+ * votes_pitch_words / out_dev + w * out_pitch_words (each a buffer in the context
+ * layout, stride_words as for one window), its draw records at records_dev + w *
+ * records_cap, its row at rows_dev[w] (required). Equivalent to n_windows calls of
+ * rg_phase_step_shard_async in window order, except that every window takes its
+ * provisional draws from the same position and shard_draws does not advance (the
+ * fix-up re-draws every VQ slot at its global position, so the fixed outputs, rows
+ * and engine state are the same). Stages (2)-(4) then run per window as above, with
+ * that window's out buffer, records and rows. The context's last result is the last
+ * window's row. */
+int rg_phase_step_shard_windows_async(rg_ctx* ctx, uint32_t n_windows, const uint32_t* votes_dev,
+                                      uint64_t votes_pitch_words, uint32_t* out_dev, uint64_t out_pitch_words,
+                                      uint64_t n_slots, uint64_t stride_words, uint64_t slot_base,
+                                      uint64_t window_stride, uint64_t max_phase, uint64_t* records_dev,
+                                      uint64_t records_cap, rg_step_result* rows_dev, void* stream);
 int rg_shard_fixup_async(rg_ctx* ctx, uint32_t* out_dev, uint64_t n_slots, uint64_t stride_words,
                          uint64_t slot_base, uint64_t max_phase, const uint64_t* records_dev,
                          uint64_t records_cap, const rg_step_result* rows_dev, uint32_t shard,

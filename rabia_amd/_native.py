@@ -86,6 +86,8 @@ _SIGS = {
     "rg_phase_step_async": (ctypes.c_int, [vp, vp, vp, u64, u64, u64, u64, u64, vp, vp]),
     "rg_phase_step": (ctypes.c_int, [vp, vp, vp, u64, u64, u64, u64, u64, ctypes.POINTER(RgStepResult)]),
     "rg_phase_step_shard_async": (ctypes.c_int, [vp, vp, vp, u64, u64, u64, u64, vp, u64, vp, vp]),
+    "rg_phase_step_shard_windows_async": (ctypes.c_int, [vp, u32, vp, u64, vp, u64, u64, u64, u64, u64, u64, vp, u64,
+                                                         vp, vp]),
     "rg_shard_fixup_async": (ctypes.c_int, [vp, vp, u64, u64, u64, u64, vp, u64, vp, u32, u32, vp, vp]),
     "rg_shard_commit_async": (ctypes.c_int, [vp, vp, u32, u64, u64, vp, vp]),
     "rg_last_result": (ctypes.c_int, [vp, ctypes.POINTER(RgStepResult)]),

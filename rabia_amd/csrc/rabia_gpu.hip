@@ -397,9 +397,16 @@ int rg_get_state(rg_ctx* ctx, rg_engine_state* st) {
   return RG_OK;
 }
 
+// Multi-window sharded launches (rg_phase_step_shard_windows_async): window w at
+// votes + w * in_pitch, out + w * out_pitch, slot ids + w * id_stride.
+struct WinArgs {
+  uint32_t n = 1;
+  uint64_t in_pitch = 0, out_pitch = 0, id_stride = 0;
+};
+
 static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, uint64_t n_slots, uint64_t stride_words,
               uint64_t slot_base, uint64_t phase, uint64_t max_phase, rg_step_result* result_dev, void* stream,
-              bool shard, uint64_t* records_dev, uint64_t records_cap) {
+              bool shard, uint64_t* records_dev, uint64_t records_cap, WinArgs win = WinArgs()) {
   if (!ctx) return fail(nullptr, RG_EINVAL, "rg_phase_step: null context");
   if (shard && ctx->cfg.mode != RG_MODE_REF)
     return fail(ctx, RG_EINVAL, "rg_phase_step_shard: REF mode only (WMVC coins are shard-invariant already)");
@@ -434,8 +441,13 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
                         (uint64_t)kOutPlanes * lout.pstride * 4 + 4096 < (1ull << 31);
   // n <= 10: the lag kernel's planes fit its registers without spills; above that the
   // tiled kernel runs (no configuration of SURVEY.md §8 has n > 9)
-  const bool lag = lag_fits && n <= 10 &&
-                   ((ctx->diag & 0x200000u) ? !wmvc : (lag_ok && !(ctx->diag & 0x100000u)));
+  // Measured (tools/ab_variants.py, tools/gpu_c5diag.sh): the lag kernel wins once every
+  // CU runs many of its tiles (n = 5: 2^30 slots 700 vs 732 us), the tiled kernel below
+  // that (2^28: 195 vs 203; n = 9, 2^26: 90 vs 96; 2^23: 21 vs 41) -> lag from 32
+  // 1024-thread tiles per CU. Multi-window shard launches run the tiled kernel.
+  const bool lag_big = n_words >= 32ull * ctx->n_cu * kLagBlock * (uint64_t)lag_words(n);
+  const bool lag = lag_fits && n <= 10 && win.n == 1 &&
+                   ((ctx->diag & 0x200000u) ? !wmvc : (lag_ok && lag_big && !(ctx->diag & 0x100000u)));
   const bool lag1024 = lag && !(ctx->diag & 0x400000u) &&
                        n_words >= 2ull * ctx->n_cu * kLagBlock * (uint64_t)lag_words(n);
   const uint64_t lag_block = lag1024 ? kLagBlock : kLagBlockSmall;
@@ -444,7 +456,7 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
   const uint32_t grid_force = (ctx->diag >> 24) & 0xFFu;  // diagnostics: lag-kernel grid (tests: many tiles per WG)
   const uint64_t lag_grid_max = grid_force ? grid_force : (lag1024 ? 1ull : 2ull) * ctx->n_cu;
   const uint32_t lag_grid = (uint32_t)(n_tiles < lag_grid_max ? n_tiles : lag_grid_max);
-  const uint64_t gran_tiles = lag ? (n_tiles > 3ull * lag_grid ? n_tiles : 3ull * lag_grid) : n_tiles;
+  const uint64_t gran_tiles = lag ? (n_tiles > 3ull * lag_grid ? n_tiles : 3ull * lag_grid) : n_tiles * win.n;
   if (int rc = ensure_tiles(ctx, gran_tiles, false)) return rc;
   // Statistics granules carry 12 bits of seq and look-back granules 31: start a
   // fresh epoch on zeroed granules whenever either wraps.
@@ -481,6 +493,10 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
   p.out_bytes = need_out * 4;
   p.vq_rec = reinterpret_cast<unsigned long long*>(records_dev);
   p.vq_cap = records_cap;
+  p.n_win = win.n;
+  p.win_in_pitch = win.in_pitch;
+  p.win_out_pitch = win.out_pitch;
+  p.win_id_stride = win.id_stride;
   if (ctx->diag & 4u) {  // stamps: [n_tiles][8] (tiled kernel) or [grid][16] (lag kernel)
     const uint64_t words = lag && 16ull * lag_grid > 8 * n_tiles ? 16ull * lag_grid : 8 * n_tiles;
     if (ctx->dbg_cap < words) {
@@ -528,6 +544,30 @@ int rg_phase_step_shard_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* 
                               uint64_t records_cap, rg_step_result* row_dev, void* stream) {
   return step_impl(ctx, votes_dev, out_dev, n_slots, stride_words, slot_base, 1, max_phase, row_dev, stream, true,
                    records_dev, records_cap);
+}
+
+int rg_phase_step_shard_windows_async(rg_ctx* ctx, uint32_t n_windows, const uint32_t* votes_dev,
+                                      uint64_t votes_pitch_words, uint32_t* out_dev, uint64_t out_pitch_words,
+                                      uint64_t n_slots, uint64_t stride_words, uint64_t slot_base,
+                                      uint64_t window_stride, uint64_t max_phase, uint64_t* records_dev,
+                                      uint64_t records_cap, rg_step_result* rows_dev, void* stream) {
+  if (!ctx) return fail(nullptr, RG_EINVAL, "rg_phase_step_shard_windows: null context");
+  if (n_windows < 1 || n_windows > 65535) return fail(ctx, RG_EINVAL, "rg_phase_step_shard_windows: 1..65535 windows");
+  if (n_windows > 1 && !rows_dev) return fail(ctx, RG_EINVAL, "rg_phase_step_shard_windows: null rows buffer");
+  if (n_windows > 1) {
+    if ((votes_pitch_words | out_pitch_words) & 3u)
+      return fail(ctx, RG_EINVAL, "rg_phase_step_shard_windows: pitches must be multiples of 4 words (16 B)");
+    if (window_stride < n_slots)
+      return fail(ctx, RG_EINVAL, "rg_phase_step_shard_windows: window_stride must be >= n_slots (disjoint windows)");
+    if (records_cap && !records_dev) return fail(ctx, RG_EINVAL, "rg_phase_step_shard_windows: null records buffer");
+  }
+  WinArgs win;
+  win.n = n_windows;
+  win.in_pitch = votes_pitch_words;
+  win.out_pitch = out_pitch_words;
+  win.id_stride = window_stride;
+  return step_impl(ctx, votes_dev, out_dev, n_slots, stride_words, slot_base, 1, max_phase, rows_dev, stream, true,
+                   records_dev, records_cap, win);
 }
 
 int rg_shard_fixup_async(rg_ctx* ctx, uint32_t* out_dev, uint64_t n_slots, uint64_t stride_words,

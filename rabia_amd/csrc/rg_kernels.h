@@ -54,6 +54,13 @@ struct StepParams {
   uint64_t in_bytes, out_bytes;   // the plane buffers' extents (RG_LAG_CHECK builds check every access)
   unsigned long long* vq_rec;     // sharded REF: draw records [vq_cap] (rg_common.h)
   uint64_t vq_cap;
+  // Sharded REF over n_win windows in one launch (grid.y = window; tiled kernel): window
+  // w reads votes + w * win_in_pitch, writes out + w * win_out_pitch, its shard's slot
+  // ids start at slot_base + w * win_id_stride, its records at vq_rec + w * vq_cap, its
+  // row at result_user[w]; its look-back chain and statistics granules are its own
+  // (lookback / stats + w * n_tiles tiles). n_win = 1: one window, as before.
+  uint32_t n_win;
+  uint64_t win_in_pitch, win_out_pitch, win_id_stride;
 };
 
 // finish_tile flavours
@@ -549,13 +556,15 @@ __device__ __forceinline__ void step_commit(const StepParams& p, Record* rec, co
     // (their decisions wait for the global draw positions); draws advance only
     // the provisional counter. The global engine state is left to the fix-up and
     // rg_shard_commit (state.rs:65-103 over the whole window).
+    // (a multi-window launch draws every window from the same provisional position and
+    // leaves shard_draws alone: the fix-up re-draws every VQ slot at its global position)
     r.last_committed_max = v[4] ? v[4] - 1 : 0;
     r.first_undecided = fu;
     r.rng_next = p.state->shard_draws + r.n_draws;
     r.commit_watermark = 0;
     r.flags = err;
-    p.state->shard_draws = r.rng_next;
-    *p.result = r;
+    if (p.n_win <= 1) p.state->shard_draws = r.rng_next;
+    if (p.result) *p.result = r;
     if (p.result_user) *p.result_user = r;
     return;
   }
@@ -692,7 +701,21 @@ __device__ __forceinline__ void r2_decision_ab(const uint32_t (&lo)[N][W], const
 // so the kernel fits 4 waves per SIMD: two 512-thread tiles resident per CU, one
 // tile's look-back overlapping the other's loads.
 template <int N, int W, int BLOCK, bool SHARD>
-__global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p) {
+__global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p_arg) {
+  StepParams p = p_arg;
+  if constexpr (SHARD) {
+    if (p.n_win > 1) {  // window blockIdx.y of a multi-window shard launch (uniform values)
+      const uint32_t w = blockIdx.y;
+      p.votes += w * p.win_in_pitch;
+      p.out += w * p.win_out_pitch;
+      p.slot_base += w * p.win_id_stride;
+      p.lookback += (uint64_t)w * p.n_tiles;
+      p.stats += (uint64_t)w * p.n_tiles * kStatGranules;
+      p.vq_rec += w * p.vq_cap;
+      p.result_user += w;
+      if (w + 1 != p.n_win) p.result = nullptr;  // the context's result: the last window's row
+    }
+  }
   constexpr int B = ctr_bits(N);
   constexpr int WAVES = BLOCK / 64;
   __shared__ uint32_t s_wave[WAVES];

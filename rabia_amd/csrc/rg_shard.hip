@@ -9,6 +9,7 @@ namespace rg {
 namespace {
 template <int N>
 void launch_n(int block, int words, uint32_t grid, hipStream_t s, const StepParams& p) {
+  const dim3 g(grid, p.n_win > 1 ? p.n_win : 1);  // grid.y: windows of a multi-window launch (tiled kernel)
   constexpr int WM = N <= 5 ? 4 : (N <= 10 ? 2 : 1);
   if (block <= 0) {  // the lag kernel (n <= 10, step_impl): -1 one 1024-thread WG per CU, 0 two 512-thread
     if constexpr (N <= 10) {
@@ -17,9 +18,9 @@ void launch_n(int block, int words, uint32_t grid, hipStream_t s, const StepPara
       else
         hipLaunchKernelGGL((ref_lag_kernel<N, (N <= 5 ? 2 : 1), 512, true>), dim3(grid), dim3(512), 0, s, p);
     }
-  } else if (block == 512) hipLaunchKernelGGL((ref_step_kernel<N, WM, 512, true>), dim3(grid), dim3(512), 0, s, p);
-  else if (block == 256) hipLaunchKernelGGL((ref_step_kernel<N, WM, 256, true>), dim3(grid), dim3(256), 0, s, p);
-  else hipLaunchKernelGGL((ref_step_kernel<N, 1, 128, true>), dim3(grid), dim3(128), 0, s, p);
+  } else if (block == 512) hipLaunchKernelGGL((ref_step_kernel<N, WM, 512, true>), g, dim3(512), 0, s, p);
+  else if (block == 256) hipLaunchKernelGGL((ref_step_kernel<N, WM, 256, true>), g, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL((ref_step_kernel<N, 1, 128, true>), g, dim3(128), 0, s, p);
   (void)words;
 }
 using Launch = void (*)(int, int, uint32_t, hipStream_t, const StepParams&);

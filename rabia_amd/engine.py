@@ -261,6 +261,17 @@ class PhaseEvaluator:
                                                    max_phase, records_ptr, records_cap, row_ptr or None,
                                                    stream or None), self.ctx)
 
+    def phase_step_shard_windows_async(self, n_windows, votes_ptr, votes_pitch, out_ptr, out_pitch, n_slots, stride,
+                                       slot_base, window_stride, records_ptr, records_cap, rows_ptr, max_phase=0,
+                                       stream=0):
+        """Stage 1 for n_windows consecutive windows of this shard in one launch (pitches
+        in 32-bit words; window w's records at records_ptr + 8 * w * records_cap, its row
+        at rows_ptr + 80 * w)."""
+        N.check(self.lib.rg_phase_step_shard_windows_async(self.ctx, n_windows, votes_ptr, votes_pitch, out_ptr,
+                                                           out_pitch, n_slots, stride, slot_base, window_stride,
+                                                           max_phase, records_ptr, records_cap, rows_ptr,
+                                                           stream or None), self.ctx)
+
     def shard_fixup_async(self, out_ptr, n_slots, stride, slot_base, records_ptr, records_cap, rows_ptr, shard,
                           n_shards, row_ptr=0, max_phase=0, stream=0):
         """Stage 3: re-draw this shard's VQ slots at their global stream positions."""

@@ -162,3 +162,39 @@ def test_c5_full_size_step(oracle):
     assert torch.equal(out1, out2)
     assert st1["rng_next"] == st2["rng_next"] and st1["last_committed"] == st2["last_committed"]
     assert st1["commit_watermark"] == st2["commit_watermark"]
+
+
+def test_c3_two_shards_equal_one_run():
+    """A C3 window split into 2 contiguous shards (two contexts, as two ranks would
+    run it; shard states generated at the shards' global slot ids) == one run over
+    the window: identical per-slot info words and folded statistics
+    (shard.combine_cluster)."""
+    torch = torch_cuda()
+    from rabia_amd import shard as SH
+    n, S, maxp = 5, (1 << 22) + 1000, 32
+    stride = plane_stride(S)
+    states = torch.zeros(n * stride, dtype=torch.int32, device="cuda")
+    info = torch.zeros(S, dtype=torch.int32, device="cuda")
+    stats = torch.zeros(8, dtype=torch.int64, device="cuda")
+    with PhaseEvaluator(n, mode="wmvc", coin_seed=7, epoch=3) as ev:
+        ev.cluster_trace_async(42, 1, S, stride, states.data_ptr())
+        ev.wmvc_cluster_async(states.data_ptr(), stride, S, 1, 99, maxp, info.data_ptr(), stats.data_ptr())
+        ev.sync()
+    rows, parts = [], []
+    for rank in range(2):
+        start, cnt = SH.shard_range(S, 2, rank)
+        st = plane_stride(cnt)
+        s_states = torch.zeros(n * st, dtype=torch.int32, device="cuda")
+        s_info = torch.zeros(cnt, dtype=torch.int32, device="cuda")
+        s_stats = torch.zeros(8, dtype=torch.int64, device="cuda")
+        with PhaseEvaluator(n, mode="wmvc", coin_seed=7, epoch=3) as ev:
+            ev.cluster_trace_async(42, 1 + start, cnt, st, s_states.data_ptr())
+            ev.wmvc_cluster_async(s_states.data_ptr(), st, cnt, 1 + start, 99, maxp, s_info.data_ptr(),
+                                  s_stats.data_ptr())
+            ev.sync()
+        parts.append(s_info)
+        rows.append(s_stats.cpu().numpy().view(np.uint64).tolist())
+    assert torch.equal(torch.cat(parts), info)
+    one = SH.combine_cluster([stats.cpu().numpy().view(np.uint64).tolist()])
+    assert SH.combine_cluster(rows) == one
+    assert one["slots"] == S

@@ -103,6 +103,52 @@ def run_sharded(n, world, window_sizes, votes, out, stride, seed=42, self_lane=N
     return [rows_of(result[w]) for w in range(len(window_sizes))], states, rows_of(rows[0]), rows_of(fixed[0])
 
 
+def run_sharded_windows(n, world, K, S, votes, out, stride, seed=42, self_lane=None, state=None, max_phase=0):
+    """As run_sharded over K equal windows, but stage 1 of each shard runs as ONE
+    multi-window launch (rg_phase_step_shard_windows_async) over its K windows."""
+    torch = torch_cuda()
+    self_lane = n // 2 if self_lane is None else self_lane
+    Sp = ((S + 127) // 128) * 128
+    ctxs = [PhaseEvaluator(n, self_lane=self_lane, seed=seed) for _ in range(world)]
+    try:
+        for ev in ctxs:
+            if state:
+                ev.set_state(**state)
+        rows = torch.zeros((K, world, 10), dtype=torch.int64, device="cuda")
+        fixed = torch.zeros((K, world, 10), dtype=torch.int64, device="cuda")
+        result = torch.zeros((K, world, 10), dtype=torch.int64, device="cuda")
+        parts = [shard.shard_range(S, world, r, align=128) for r in range(world)]
+        recs = [torch.zeros(K * max(cnt, 1), dtype=torch.int64, device="cuda") for _, cnt in parts]
+        rows_r = [torch.zeros((K, 10), dtype=torch.int64, device="cuda") for _ in range(world)]
+        torch.cuda.synchronize()
+        for r, (start, cnt) in enumerate(parts):
+            w0 = start // 32
+            ctxs[r].phase_step_shard_windows_async(K, votes.data_ptr() + 4 * w0, Sp // 32, out.data_ptr() + 4 * w0,
+                                                   Sp // 32, cnt, stride, 1 + start, S, recs[r].data_ptr(), cnt,
+                                                   rows_r[r].data_ptr(), max_phase=max_phase)
+        torch.cuda.synchronize()
+        for r in range(world):
+            rows[:, r] = rows_r[r]
+        for w in range(K):
+            base, off = 1 + w * S, w * Sp
+            g = rows[w].contiguous()
+            for r, (start, cnt) in enumerate(parts):
+                w0 = (off + start) // 32
+                ctxs[r].shard_fixup_async(out.data_ptr() + 4 * w0, cnt, stride, base + start,
+                                          recs[r].data_ptr() + 8 * w * cnt, cnt, g.data_ptr(), r, world,
+                                          fixed[w, r].data_ptr(), max_phase=max_phase)
+            torch.cuda.synchronize()
+            fg = fixed[w].contiguous()
+            for r in range(world):
+                ctxs[r].shard_commit_async(fg.data_ptr(), world, base, S, result[w, r].data_ptr())
+            torch.cuda.synchronize()
+        states = [ev.get_state() for ev in ctxs]
+    finally:
+        for ev in ctxs:
+            ev.close()
+    return [rows_of(result[w]) for w in range(K)], states, [rows_of(rows[w]) for w in range(K)]
+
+
 def run_single(n, window_sizes, votes, out, stride, seed=42, self_lane=None, state=None, max_phase=0):
     torch = torch_cuda()
     self_lane = n // 2 if self_lane is None else self_lane
@@ -178,6 +224,36 @@ def test_sharded_equals_one_engine(oracle, n, world, sizes, kind):
         rng, lc = eres["rng_next"], eres["last_committed_max"]
         base += S
         off += ((S + 127) // 128) * 128
+
+
+@pytest.mark.parametrize("n,world,K,S,kind", [
+    (5, 2, 4, 300_032, 1),
+    (9, 3, 3, 1 << 20, 1),
+    (7, 1, 5, 262_144, 2),
+    (3, 4, 2, 100_096, 0),
+])
+def test_shard_windows_launch_equals_per_window(n, world, K, S, kind):
+    """K windows of one shard in ONE launch (rg_phase_step_shard_windows_async) ==
+    K per-window shard launches: identical fixed outputs, per-window shard rows
+    (counts, extremes, n_draws), global results (rng_next, watermarks) and engine state."""
+    torch = torch_cuda()
+    votes, stride, total = make_votes(n, [S] * K, kind)
+    out_m = torch.zeros(8 * stride, dtype=torch.int32, device="cuda")
+    out_w = torch.zeros(8 * stride, dtype=torch.int32, device="cuda")
+    state = {"rng_next": 99, "last_committed": 5, "commit_watermark": 1, "steps": 0}
+    mp = K * S * 3 // 4
+    res_m, st_m, rows_m = run_sharded_windows(n, world, K, S, votes, out_m, stride, state=state, max_phase=mp)
+    res_w, st_w, _, _ = run_sharded(n, world, [S] * K, votes, out_w, stride, state=state, max_phase=mp)
+    assert torch.equal(out_m, out_w)
+    for w in range(K):
+        for r in range(world):
+            assert {k: res_m[w][r][k] for k in RES_CMP} == {k: res_w[w][r][k] for k in RES_CMP}, (w, r)
+        assert all(x["flags"] == 0 for x in rows_m[w])
+    assert st_m == st_w
+    # and against one evaluator over the K windows
+    out_1 = torch.zeros(8 * stride, dtype=torch.int32, device="cuda")
+    res_1, st_1 = run_single(n, [S] * K, votes, out_1, stride, state=state, max_phase=mp)
+    assert torch.equal(out_m, out_1) and all(st == st_1 for st in st_m)
 
 
 def test_sharded_full_size_c5_shape():
