@@ -392,14 +392,14 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, bitmaps):
     n_total = a.warmup + a.steps
     i64 = dict(dtype=torch.int64, device="cuda")
     rows = torch.zeros((n_total, K, 10), **i64)
-    g_rows = torch.zeros((n_total, K, world, 10), **i64)
+    g_rows = torch.zeros((n_total, world, K, 10), **i64)  # rank-major: one all-gather of every rank's K rows
     fixed = torch.zeros((n_total, K, 10), **i64)
-    g_fixed = torch.zeros((n_total, K, world, 10), **i64)
+    g_fixed = torch.zeros((n_total, world, K, 10), **i64)
     result = torch.zeros((n_total, K, 10), **i64)
     nw = (S + 31) // 32
     if bitmaps:
         bm = torch.zeros((n_total, K, 2, nw), dtype=torch.int32, device="cuda")
-        bm_all = torch.zeros((n_total, K, world, 2, nw), dtype=torch.int32, device="cuda")
+        bm_all = torch.zeros((n_total, world, K, 2, nw), dtype=torch.int32, device="cuda")
     torch.cuda.synchronize()
     e_main = [torch.cuda.Event() for _ in range(n_total)]
     e_done = [torch.cuda.Event() for _ in range(n_total)]
@@ -435,22 +435,20 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, bitmaps):
         if evs is not None:
             evs[1].record(comp)
         e_main[t].record(comp)
-        with torch.cuda.stream(fix):
+        with torch.cuda.stream(fix):  # the K windows' later stages: one call / one all-gather each
             fix.wait_event(e_main[t])
-            for k in range(K):
-                bk = base + k * window_slots
-                o_k = out.data_ptr() + 4 * k * out_words
-                gather(g_rows[t, k], rows[t, k])
-                ev.shard_fixup_async(o_k, S, stride, bk + start, rec.data_ptr() + 8 * k * cap, cap,
-                                     g_rows[t, k].data_ptr(), rank, world, fixed[t, k].data_ptr(),
-                                     stream=fix.cuda_stream)
-                gather(g_fixed[t, k], fixed[t, k])
-                ev.shard_commit_async(g_fixed[t, k].data_ptr(), world, bk, window_slots, result[t, k].data_ptr(),
-                                      stream=fix.cuda_stream)
-                if bitmaps:
-                    ev.decision_bitmap_async(o_k, S, stride, bm[t, k, 0].data_ptr(), bm[t, k, 1].data_ptr(),
-                                             fix.cuda_stream)
-                    gather(bm_all[t, k], bm[t, k])
+            fs = fix.cuda_stream
+            gather(g_rows[t], rows[t])
+            ev.shard_fixup_windows_async(K, out.data_ptr(), out_words, S, stride, base + start, window_slots,
+                                         rec.data_ptr(), cap, g_rows[t].data_ptr(), rank, world,
+                                         fixed[t].data_ptr(), stream=fs)
+            gather(g_fixed[t], fixed[t])
+            ev.shard_commit_windows_async(K, g_fixed[t].data_ptr(), world, base, window_slots, result[t].data_ptr(),
+                                          stream=fs)
+            if bitmaps:
+                ev.decision_bitmap_windows_async(K, out.data_ptr(), out_words, S, stride, bm[t, 0, 0].data_ptr(),
+                                                 bm[t, 0, 1].data_ptr(), 2 * nw, stream=fs)
+                gather(bm_all[t], bm[t])
             e_done[t].record(fix)
 
     def barrier():

@@ -204,6 +204,22 @@ int rg_shard_fixup_async(rg_ctx* ctx, uint32_t* out_dev, uint64_t n_slots, uint6
                          uint64_t slot_base, uint64_t max_phase, const uint64_t* records_dev,
                          uint64_t records_cap, const rg_step_result* rows_dev, uint32_t shard,
                          uint32_t n_shards, rg_step_result* row_dev, void* stream);
+/* Stages (3) and (4) for n_windows consecutive windows at once (after
+ * rg_phase_step_shard_windows_async): rows_dev = every shard's n_windows rows,
+ * rank-major [n_shards][n_windows] (one all-gather of each shard's rows); window w's
+ * outputs at out_dev + w * out_pitch_words, its slot ids + w * window_stride, its
+ * records at records_dev + w * records_cap; rows_out_dev[w] = its final row. The
+ * commit folds [n_shards][n_windows] final rows window by window (window w =
+ * [window_base + w * window_slots, + window_slots)) into results_dev[w]. Equivalent
+ * to the per-window calls in window order. */
+int rg_shard_fixup_windows_async(rg_ctx* ctx, uint32_t n_windows, uint32_t* out_dev, uint64_t out_pitch_words,
+                                 uint64_t n_slots, uint64_t stride_words, uint64_t slot_base, uint64_t window_stride,
+                                 uint64_t max_phase, const uint64_t* records_dev, uint64_t records_cap,
+                                 const rg_step_result* rows_dev, uint32_t shard, uint32_t n_shards,
+                                 rg_step_result* rows_out_dev, void* stream);
+int rg_shard_commit_windows_async(rg_ctx* ctx, uint32_t n_windows, const rg_step_result* rows_dev, uint32_t n_shards,
+                                  uint64_t window_base, uint64_t window_slots, rg_step_result* results_dev,
+                                  void* stream);
 int rg_shard_commit_async(rg_ctx* ctx, const rg_step_result* rows_dev, uint32_t n_shards,
                           uint64_t window_base, uint64_t window_slots, rg_step_result* result_dev,
                           void* stream);
@@ -259,6 +275,12 @@ int rg_round1_votes_async(rg_ctx* ctx, const uint64_t* phase_ids_dev, const uint
  * ceil(n_slots/32) words each — the per-shard payload of the multi-GPU exchange. */
 int rg_decision_bitmap_async(rg_ctx* ctx, const uint32_t* out_dev, uint64_t n_slots, uint64_t stride_words,
                              uint32_t* committed_dev, uint32_t* v1_dev, void* stream);
+/* The same for n_windows windows (outputs at out_dev + w * out_pitch_words, bitmaps
+ * at committed_dev / v1_dev + w * bitmap_pitch_words). */
+int rg_decision_bitmap_windows_async(rg_ctx* ctx, uint32_t n_windows, const uint32_t* out_dev,
+                                     uint64_t out_pitch_words, uint64_t n_slots, uint64_t stride_words,
+                                     uint32_t* committed_dev, uint32_t* v1_dev, uint64_t bitmap_pitch_words,
+                                     void* stream);
 
 /* StdRng::seed_from_u64(seed).next_u64() draws first..first+count-1 (random access;
  * the stream the REF mode consumes, engine.rs:461-604). */

@@ -89,6 +89,10 @@ _SIGS = {
     "rg_phase_step_shard_windows_async": (ctypes.c_int, [vp, u32, vp, u64, vp, u64, u64, u64, u64, u64, u64, vp, u64,
                                                          vp, vp]),
     "rg_shard_fixup_async": (ctypes.c_int, [vp, vp, u64, u64, u64, u64, vp, u64, vp, u32, u32, vp, vp]),
+    "rg_shard_fixup_windows_async": (ctypes.c_int, [vp, u32, vp, u64, u64, u64, u64, u64, u64, vp, u64, vp, u32, u32,
+                                                    vp, vp]),
+    "rg_shard_commit_windows_async": (ctypes.c_int, [vp, u32, vp, u32, u64, u64, vp, vp]),
+    "rg_decision_bitmap_windows_async": (ctypes.c_int, [vp, u32, vp, u64, u64, u64, vp, vp, u64, vp]),
     "rg_shard_commit_async": (ctypes.c_int, [vp, vp, u32, u64, u64, vp, vp]),
     "rg_last_result": (ctypes.c_int, [vp, ctypes.POINTER(RgStepResult)]),
     "rg_digest_majority_async": (ctypes.c_int, [vp, vp, u64, vp, u64, vp]),

@@ -52,7 +52,8 @@ struct rg_ctx {
   uint64_t cluster_coins_cap = 0;               // words
   unsigned long long* cluster_part = nullptr;  // [blocks][kClusterStats]
   unsigned long long* cluster_stats = nullptr;  // [kClusterStats]
-  unsigned long long* fix_acc = nullptr;        // sharded REF fix-up accumulator [4]
+  unsigned long long* fix_acc = nullptr;        // sharded REF fix-up accumulators [4][windows]
+  uint64_t fix_acc_cap = 4;
   unsigned long long* follow_acc = nullptr;     // follower commit accumulator [4]
   // results of the shard fix-up / shard commit / follower commit: each stage writes
   // its own (a fix-up may run on another stream than the next window's step, whose
@@ -570,22 +571,33 @@ int rg_phase_step_shard_windows_async(rg_ctx* ctx, uint32_t n_windows, const uin
                    records_dev, records_cap, win);
 }
 
-int rg_shard_fixup_async(rg_ctx* ctx, uint32_t* out_dev, uint64_t n_slots, uint64_t stride_words,
-                         uint64_t slot_base, uint64_t max_phase, const uint64_t* records_dev,
-                         uint64_t records_cap, const rg_step_result* rows_dev, uint32_t shard,
-                         uint32_t n_shards, rg_step_result* row_dev, void* stream) {
+static int fixup_impl(rg_ctx* ctx, uint32_t n_win, uint32_t* out_dev, uint64_t out_pitch, uint64_t n_slots,
+                      uint64_t stride_words, uint64_t slot_base, uint64_t id_stride, uint64_t max_phase,
+                      const uint64_t* records_dev, uint64_t records_cap, const rg_step_result* rows_dev,
+                      uint32_t shard, uint32_t n_shards, rg_step_result* rows_out_dev, void* stream) {
   if (!ctx) return fail(nullptr, RG_EINVAL, "rg_shard_fixup: null context");
   if (ctx->cfg.mode != RG_MODE_REF) return fail(ctx, RG_EINVAL, "rg_shard_fixup: REF mode only");
-  if (!out_dev || !records_dev || !rows_dev || n_shards == 0 || shard >= n_shards || n_slots == 0)
+  if (!out_dev || !records_dev || !rows_dev || n_shards == 0 || shard >= n_shards || n_slots == 0 || n_win == 0 ||
+      n_win > 65535)
     return fail(ctx, RG_EINVAL, "rg_shard_fixup: bad argument");
+  if (n_win > 1 && (((out_pitch & 3u) != 0) || id_stride < n_slots))
+    return fail(ctx, RG_EINVAL, "rg_shard_fixup_windows: out pitch must be a multiple of 4 words, window_stride >= n_slots");
   RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
   const uint64_t n_words = (n_slots + 31) / 32;
   Layout lout;
   uint64_t need;
   if (int rc = make_layout(ctx, kOutPlanes, n_words, stride_words, &lout, &need, "rg_shard_fixup")) return rc;
+  if (4ull * n_win > ctx->fix_acc_cap) {
+    RG_HIP(ctx, hipDeviceSynchronize());
+    (void)hipFree(ctx->fix_acc);
+    ctx->fix_acc = nullptr;
+    RG_HIP(ctx, hipMalloc(&ctx->fix_acc, 4ull * n_win * sizeof(unsigned long long)));
+    ctx->fix_acc_cap = 4ull * n_win;
+  }
   hipStream_t s = pick_stream(ctx, stream);
-  RG_HIP(ctx, hipMemsetAsync(ctx->fix_acc, 0, 3 * sizeof(unsigned long long), s));
-  RG_HIP(ctx, hipMemsetAsync(ctx->fix_acc + 3, 0xFF, sizeof(unsigned long long), s));
+  // acc [4][n_win]: decided, V1, max V1 id + 1 (0) and min undecided id (all ones)
+  RG_HIP(ctx, hipMemsetAsync(ctx->fix_acc, 0, 3ull * n_win * sizeof(unsigned long long), s));
+  RG_HIP(ctx, hipMemsetAsync(ctx->fix_acc + 3ull * n_win, 0xFF, n_win * sizeof(unsigned long long), s));
   FixParams f;
   f.rec = reinterpret_cast<const unsigned long long*>(records_dev);
   f.rows = reinterpret_cast<const DevResult*>(rows_dev);
@@ -599,16 +611,36 @@ int rg_shard_fixup_async(rg_ctx* ctx, uint32_t* out_dev, uint64_t n_slots, uint6
   f.vq_cap = records_cap;
   f.key = ctx->ref_key;
   f.acc = ctx->fix_acc;
+  f.n_win = n_win;
+  f.out_pitch = out_pitch;
+  f.id_stride = id_stride;
   // one ChaCha12 block per thread per pass; the record count lives on the device,
   // so the grid covers the largest possible count (all slots VQ) and strides
   const uint64_t blocks_max = (records_cap < n_slots ? records_cap : n_slots) / 8 + 2;
   const uint64_t g = (blocks_max + 255) / 256;
   const uint32_t grid = (uint32_t)(g < 1024 ? g : 1024);
-  hipLaunchKernelGGL(shard_fixup_kernel, dim3(grid), dim3(256), 0, s, f);
+  hipLaunchKernelGGL(shard_fixup_kernel, dim3(grid, n_win), dim3(256), 0, s, f);
   hipLaunchKernelGGL(shard_fixup_finish_kernel, dim3(1), dim3(64), 0, s, f, ctx->stage_result + 0,
-                     reinterpret_cast<DevResult*>(row_dev));
+                     reinterpret_cast<DevResult*>(rows_out_dev));
   RG_HIP(ctx, hipGetLastError());
   return RG_OK;
+}
+
+int rg_shard_fixup_async(rg_ctx* ctx, uint32_t* out_dev, uint64_t n_slots, uint64_t stride_words,
+                         uint64_t slot_base, uint64_t max_phase, const uint64_t* records_dev,
+                         uint64_t records_cap, const rg_step_result* rows_dev, uint32_t shard,
+                         uint32_t n_shards, rg_step_result* row_dev, void* stream) {
+  return fixup_impl(ctx, 1, out_dev, 0, n_slots, stride_words, slot_base, n_slots, max_phase, records_dev, records_cap,
+                    rows_dev, shard, n_shards, row_dev, stream);
+}
+
+int rg_shard_fixup_windows_async(rg_ctx* ctx, uint32_t n_windows, uint32_t* out_dev, uint64_t out_pitch_words,
+                                 uint64_t n_slots, uint64_t stride_words, uint64_t slot_base, uint64_t window_stride,
+                                 uint64_t max_phase, const uint64_t* records_dev, uint64_t records_cap,
+                                 const rg_step_result* rows_dev, uint32_t shard, uint32_t n_shards,
+                                 rg_step_result* rows_out_dev, void* stream) {
+  return fixup_impl(ctx, n_windows, out_dev, out_pitch_words, n_slots, stride_words, slot_base, window_stride,
+                    max_phase, records_dev, records_cap, rows_dev, shard, n_shards, rows_out_dev, stream);
 }
 
 int rg_follower_commit_async(rg_ctx* ctx, const uint32_t* out_dev, uint64_t n_slots, uint64_t stride_words,
@@ -650,8 +682,22 @@ int rg_shard_commit_async(rg_ctx* ctx, const rg_step_result* rows_dev, uint32_t 
   if (!rows_dev || n_shards == 0 || window_slots == 0) return fail(ctx, RG_EINVAL, "rg_shard_commit: bad argument");
   RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
   hipLaunchKernelGGL(shard_commit_kernel, dim3(1), dim3(64), 0, pick_stream(ctx, stream),
-                     reinterpret_cast<const DevResult*>(rows_dev), n_shards, window_base, window_slots, ctx->state,
+                     reinterpret_cast<const DevResult*>(rows_dev), n_shards, 1u, window_base, window_slots, ctx->state,
                      ctx->stage_result + 1, reinterpret_cast<DevResult*>(result_dev));
+  RG_HIP(ctx, hipGetLastError());
+  return RG_OK;
+}
+
+int rg_shard_commit_windows_async(rg_ctx* ctx, uint32_t n_windows, const rg_step_result* rows_dev, uint32_t n_shards,
+                                  uint64_t window_base, uint64_t window_slots, rg_step_result* results_dev,
+                                  void* stream) {
+  if (!ctx) return fail(nullptr, RG_EINVAL, "rg_shard_commit_windows: null context");
+  if (!rows_dev || n_shards == 0 || window_slots == 0 || n_windows == 0)
+    return fail(ctx, RG_EINVAL, "rg_shard_commit_windows: bad argument");
+  RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
+  hipLaunchKernelGGL(shard_commit_kernel, dim3(1), dim3(64), 0, pick_stream(ctx, stream),
+                     reinterpret_cast<const DevResult*>(rows_dev), n_shards, n_windows, window_base, window_slots,
+                     ctx->state, ctx->stage_result + 1, reinterpret_cast<DevResult*>(results_dev));
   RG_HIP(ctx, hipGetLastError());
   return RG_OK;
 }
@@ -740,7 +786,28 @@ int rg_decision_bitmap_async(rg_ctx* ctx, const uint32_t* out_dev, uint64_t n_sl
   if (int rc = make_layout(ctx, kOutPlanes, n_words, stride_words, &lout, &need, "rg_decision_bitmap")) return rc;
   RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
   hipLaunchKernelGGL(bitmap_kernel, dim3((uint32_t)((n_words + 255) / 256)), dim3(256), 0,
-                     pick_stream(ctx, stream), out_dev, lout, n_words, committed_dev, v1_dev);
+                     pick_stream(ctx, stream), out_dev, lout, n_words, committed_dev, v1_dev, 0ull, 0ull);
+  RG_HIP(ctx, hipGetLastError());
+  return RG_OK;
+}
+
+int rg_decision_bitmap_windows_async(rg_ctx* ctx, uint32_t n_windows, const uint32_t* out_dev,
+                                     uint64_t out_pitch_words, uint64_t n_slots, uint64_t stride_words,
+                                     uint32_t* committed_dev, uint32_t* v1_dev, uint64_t bitmap_pitch_words,
+                                     void* stream) {
+  if (!ctx || !out_dev || !committed_dev || !v1_dev || n_slots == 0 || n_windows == 0 || n_windows > 65535)
+    return fail(ctx, RG_EINVAL, "rg_decision_bitmap_windows: bad argument");
+  const uint64_t n_words = (n_slots + 31) / 32;
+  if (n_windows > 1 && bitmap_pitch_words < n_words)
+    return fail(ctx, RG_EINVAL, "rg_decision_bitmap_windows: bitmap pitch < ceil(n_slots/32)");
+  Layout lout;
+  uint64_t need;
+  if (int rc = make_layout(ctx, kOutPlanes, n_words, stride_words, &lout, &need, "rg_decision_bitmap_windows"))
+    return rc;
+  RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
+  hipLaunchKernelGGL(bitmap_kernel, dim3((uint32_t)((n_words + 255) / 256), n_windows), dim3(256), 0,
+                     pick_stream(ctx, stream), out_dev, lout, n_words, committed_dev, v1_dev, out_pitch_words,
+                     bitmap_pitch_words);
   RG_HIP(ctx, hipGetLastError());
   return RG_OK;
 }

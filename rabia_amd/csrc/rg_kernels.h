@@ -1709,8 +1709,26 @@ struct FixParams {
   Layout lout;
   uint64_t slot_base, max_phase, vq_cap;
   Key key;
-  unsigned long long* acc;        // [4] decided, V1, max V1 id + 1, min undecided id
+  unsigned long long* acc;        // [4][n_win] decided, V1, max V1 id + 1, min undecided id
+  // n_win windows (grid.y): window w's outputs at out + w * out_pitch, slot ids + w *
+  // id_stride, records + w * vq_cap; rows [n_shards][n_win] (rank-major, as an
+  // all-gather of every shard's n_win rows lays them out)
+  uint32_t n_win;
+  uint64_t out_pitch, id_stride;
 };
+
+// Global stream position of local draw 0 of window w of shard f.shard: the engine
+// position at the first window + every shard's draws of the earlier windows + the
+// lower shards' draws of window w (ascending slot order, engine.rs:567-611).
+__device__ __forceinline__ unsigned long long fix_first_draw(const FixParams& f, uint32_t w) {
+  unsigned long long pre = f.state->rng_next;
+  for (uint32_t r = 0; r < f.n_shards; r++) {
+    const DevResult* rr = f.rows + (uint64_t)r * f.n_win;
+    for (uint32_t v = 0; v < w; v++) pre += rr[v].n_draws;
+    if (r < f.shard) pre += rr[w].n_draws;
+  }
+  return pre;
+}
 
 __device__ __forceinline__ void fix_flush(const FixParams& f, uint64_t w, const uint32_t (&x)[5]) {
   constexpr int kPl[5] = {2, 4, 5, 6, 7};
@@ -1721,10 +1739,14 @@ __device__ __forceinline__ void fix_flush(const FixParams& f, uint64_t w, const 
 }
 
 static __global__ __launch_bounds__(256) void shard_fixup_kernel(FixParams f) {
-  const unsigned long long n = f.rows[f.shard].n_draws;
-  unsigned long long pre = 0;
-  for (uint32_t r = 0; r < f.shard; r++) pre += f.rows[r].n_draws;
-  const unsigned long long g0 = f.state->rng_next + pre;  // global position of local draw 0
+  const uint32_t win = blockIdx.y;
+  const unsigned long long n = f.rows[(uint64_t)f.shard * f.n_win + win].n_draws;
+  const unsigned long long g0 = fix_first_draw(f, win);  // global position of local draw 0
+  if (win) {  // this window's outputs, slot ids, records and accumulators
+    f.out += win * f.out_pitch;
+    f.slot_base += win * f.id_stride;
+    f.rec += win * f.vq_cap;
+  }
   const unsigned long long nn = n < f.vq_cap ? n : f.vq_cap;
   const unsigned long long b_first = g0 >> 3, b_end = nn ? ((g0 + nn - 1) >> 3) + 1 : b_first;
   unsigned long long dec = 0, v1 = 0, mx = 0, mn = ~0ull;
@@ -1788,10 +1810,10 @@ static __global__ __launch_bounds__(256) void shard_fixup_kernel(FixParams f) {
       mx = red[w][2] > mx ? red[w][2] : mx;
       mn = red[w][3] < mn ? red[w][3] : mn;
     }
-    if (dec) atomicAdd(f.acc + 0, dec);
-    if (v1) atomicAdd(f.acc + 1, v1);
-    if (mx) atomicMax(f.acc + 2, mx);
-    if (mn != ~0ull) atomicMin(f.acc + 3, mn);
+    if (dec) atomicAdd(f.acc + win, dec);
+    if (v1) atomicAdd(f.acc + f.n_win + win, v1);
+    if (mx) atomicMax(f.acc + 2 * f.n_win + win, mx);
+    if (mn != ~0ull) atomicMin(f.acc + 3 * f.n_win + win, mn);
   }
 }
 
@@ -1799,58 +1821,67 @@ static __global__ __launch_bounds__(256) void shard_fixup_kernel(FixParams f) {
 // stream position advanced past the whole window's draws (every shard's).
 static __global__ void shard_fixup_finish_kernel(FixParams f, DevResult* row_ctx, DevResult* row_user) {
   if (threadIdx.x != 0) return;
-  DevResult r = f.rows[f.shard];
-  unsigned long long total = 0;
-  for (uint32_t s = 0; s < f.n_shards; s++) total += f.rows[s].n_draws;
-  r.n_decided += f.acc[0];
-  r.n_v1 += f.acc[1];
-  if (f.acc[2] && f.acc[2] - 1 > r.last_committed_max) r.last_committed_max = f.acc[2] - 1;
-  if (f.acc[3] < r.first_undecided) r.first_undecided = f.acc[3];
-  if (r.n_draws > f.vq_cap) r.flags |= 8ull;  // records did not fit: the patch is incomplete
-  // only rng_next: a later window's shard step (shard_draws) may run on another stream
-  r.rng_next = f.state->rng_next + total;
-  r.commit_watermark = 0;
-  f.state->rng_next = r.rng_next;
-  *row_ctx = r;
-  if (row_user) *row_user = r;
+  unsigned long long pos = f.state->rng_next;
+  for (uint32_t w = 0; w < f.n_win; w++) {
+    DevResult r = f.rows[(uint64_t)f.shard * f.n_win + w];
+    unsigned long long total = 0;
+    for (uint32_t s = 0; s < f.n_shards; s++) total += f.rows[(uint64_t)s * f.n_win + w].n_draws;
+    const unsigned long long a0 = f.acc[w], a1 = f.acc[f.n_win + w], a2 = f.acc[2 * f.n_win + w],
+                             a3 = f.acc[3 * f.n_win + w];
+    r.n_decided += a0;
+    r.n_v1 += a1;
+    if (a2 && a2 - 1 > r.last_committed_max) r.last_committed_max = a2 - 1;
+    if (a3 < r.first_undecided) r.first_undecided = a3;
+    if (r.n_draws > f.vq_cap) r.flags |= 8ull;  // records did not fit: the patch is incomplete
+    // only rng_next: a later window's shard step (shard_draws) may run on another stream
+    pos += total;
+    r.rng_next = pos;
+    r.commit_watermark = 0;
+    if (w + 1 == f.n_win) *row_ctx = r;
+    if (row_user) row_user[w] = r;
+  }
+  f.state->rng_next = pos;
 }
 
 // Fold the shards' final rows of one window into the engine state exactly as one
 // evaluator over the whole window: commit_phase max (state.rs:77-99), first
 // undecided = min over shards, contiguous watermark advance.
-static __global__ void shard_commit_kernel(const DevResult* rows, uint32_t n_shards, uint64_t window_base,
-                                    uint64_t window_slots, DevState* state, DevResult* res_ctx,
+static __global__ void shard_commit_kernel(const DevResult* rows_all, uint32_t n_shards, uint32_t n_win,
+                                    uint64_t window_base0, uint64_t window_slots, DevState* state, DevResult* res_ctx,
                                     DevResult* res_user) {
   if (threadIdx.x != 0) return;
-  DevState s = *state;
-  DevResult g;
-  g.n_slots = g.n_decided = g.n_v1 = g.n_pending_r1 = g.n_draws = g.flags = 0;
-  unsigned long long lc = s.last_committed;
-  const unsigned long long end = window_base + window_slots;
-  unsigned long long fu = end;
-  for (uint32_t r = 0; r < n_shards; r++) {
-    const DevResult& x = rows[r];
-    g.n_slots += x.n_slots;
-    g.n_decided += x.n_decided;
-    g.n_v1 += x.n_v1;
-    g.n_pending_r1 += x.n_pending_r1;
-    g.n_draws += x.n_draws;
-    g.flags |= x.flags;
-    if (x.last_committed_max > lc) lc = x.last_committed_max;
-    if (x.n_slots && x.first_undecided < fu) fu = x.first_undecided;
+  for (uint32_t w = 0; w < n_win; w++) {  // consecutive windows, in order (the watermark chains)
+    const uint64_t window_base = window_base0 + w * window_slots;
+    DevState s = *state;
+    DevResult g;
+    g.n_slots = g.n_decided = g.n_v1 = g.n_pending_r1 = g.n_draws = g.flags = 0;
+    unsigned long long lc = s.last_committed;
+    const unsigned long long end = window_base + window_slots;
+    unsigned long long fu = end;
+    for (uint32_t r = 0; r < n_shards; r++) {
+      const DevResult& x = rows_all[(uint64_t)r * n_win + w];
+      g.n_slots += x.n_slots;
+      g.n_decided += x.n_decided;
+      g.n_v1 += x.n_v1;
+      g.n_pending_r1 += x.n_pending_r1;
+      g.n_draws += x.n_draws;
+      g.flags |= x.flags;
+      if (x.last_committed_max > lc) lc = x.last_committed_max;
+      if (x.n_slots && x.first_undecided < fu) fu = x.first_undecided;
+    }
+    if (g.n_slots != window_slots) g.flags |= 16ull;  // the rows do not tile the window
+    unsigned long long wm = s.commit_watermark;
+    if (window_base <= wm && wm < fu) wm = fu;
+    g.last_committed_max = lc;
+    g.first_undecided = fu;
+    g.rng_next = rows_all[w].rng_next;  // the fixed rows carry the position after window w
+    g.commit_watermark = wm;
+    state->last_committed = lc;  // the fields it owns (the shard step and fix-up own the others)
+    state->commit_watermark = wm;
+    state->steps = s.steps + 1;
+    if (w + 1 == n_win) *res_ctx = g;
+    if (res_user) res_user[w] = g;
   }
-  if (g.n_slots != window_slots) g.flags |= 16ull;  // the rows do not tile the window
-  unsigned long long wm = s.commit_watermark;
-  if (window_base <= wm && wm < fu) wm = fu;
-  g.last_committed_max = lc;
-  g.first_undecided = fu;
-  g.rng_next = s.rng_next;
-  g.commit_watermark = wm;
-  state->last_committed = lc;  // the fields it owns (the shard step and fix-up own the others)
-  state->commit_watermark = wm;
-  state->steps = s.steps + 1;
-  *res_ctx = g;
-  if (res_user) *res_user = g;
 }
 
 // ============================================================================
@@ -2198,9 +2229,12 @@ static __global__ void coin_kernel(Key key, uint64_t stream, uint64_t phase, uin
 // Decision bitmaps of a step's output (planes 6 committed, 7 V1/apply) as two
 // contiguous bit arrays: what the multi-GPU exchange all-gathers.
 static __global__ void bitmap_kernel(const uint32_t* out, Layout lout, uint64_t n_words, uint32_t* committed,
-                              uint32_t* v1) {
+                              uint32_t* v1, uint64_t out_pitch, uint64_t bm_pitch) {
   const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= n_words) return;
+  out += blockIdx.y * out_pitch;  // window blockIdx.y of a multi-window call
+  committed += blockIdx.y * bm_pitch;
+  v1 += blockIdx.y * bm_pitch;
   const uint64_t b = lout.base(w);
   committed[w] = out[b + 6 * lout.pstride];
   v1[w] = out[b + 7 * lout.pstride];

@@ -279,6 +279,21 @@ class PhaseEvaluator:
                                               records_cap, rows_ptr, shard, n_shards, row_ptr or None,
                                               stream or None), self.ctx)
 
+    def shard_fixup_windows_async(self, n_windows, out_ptr, out_pitch, n_slots, stride, slot_base, window_stride,
+                                  records_ptr, records_cap, rows_ptr, shard, n_shards, rows_out_ptr=0, max_phase=0,
+                                  stream=0):
+        """Stage 3 for n_windows windows (rows [n_shards][n_windows], rank-major)."""
+        N.check(self.lib.rg_shard_fixup_windows_async(self.ctx, n_windows, out_ptr, out_pitch, n_slots, stride,
+                                                      slot_base, window_stride, max_phase, records_ptr, records_cap,
+                                                      rows_ptr, shard, n_shards, rows_out_ptr or None,
+                                                      stream or None), self.ctx)
+
+    def shard_commit_windows_async(self, n_windows, rows_ptr, n_shards, window_base, window_slots, results_ptr=0,
+                                   stream=0):
+        """Stage 4 for n_windows consecutive windows (rows [n_shards][n_windows])."""
+        N.check(self.lib.rg_shard_commit_windows_async(self.ctx, n_windows, rows_ptr, n_shards, window_base,
+                                                       window_slots, results_ptr or None, stream or None), self.ctx)
+
     def shard_commit_async(self, rows_ptr, n_shards, window_base, window_slots, result_ptr=0, stream=0):
         """Stage 4: fold every shard's final row into this context's engine state."""
         N.check(self.lib.rg_shard_commit_async(self.ctx, rows_ptr, n_shards, window_base, window_slots,
@@ -310,6 +325,12 @@ class PhaseEvaluator:
     def decision_bitmap_async(self, out_ptr, n_slots, stride, committed_ptr, v1_ptr, stream=0):
         N.check(self.lib.rg_decision_bitmap_async(self.ctx, out_ptr, n_slots, stride, committed_ptr, v1_ptr,
                                                   stream or None), self.ctx)
+
+    def decision_bitmap_windows_async(self, n_windows, out_ptr, out_pitch, n_slots, stride, committed_ptr, v1_ptr,
+                                      bitmap_pitch, stream=0):
+        N.check(self.lib.rg_decision_bitmap_windows_async(self.ctx, n_windows, out_ptr, out_pitch, n_slots, stride,
+                                                          committed_ptr, v1_ptr, bitmap_pitch, stream or None),
+                self.ctx)
 
     def ref_draws_async(self, first, count, out_ptr, stream=0):
         N.check(self.lib.rg_ref_draws_async(self.ctx, first, count, out_ptr, stream or None), self.ctx)

@@ -103,9 +103,11 @@ def run_sharded(n, world, window_sizes, votes, out, stride, seed=42, self_lane=N
     return [rows_of(result[w]) for w in range(len(window_sizes))], states, rows_of(rows[0]), rows_of(fixed[0])
 
 
-def run_sharded_windows(n, world, K, S, votes, out, stride, seed=42, self_lane=None, state=None, max_phase=0):
+def run_sharded_windows(n, world, K, S, votes, out, stride, seed=42, self_lane=None, state=None, max_phase=0,
+                        batched_stages=False):
     """As run_sharded over K equal windows, but stage 1 of each shard runs as ONE
-    multi-window launch (rg_phase_step_shard_windows_async) over its K windows."""
+    multi-window launch (rg_phase_step_shard_windows_async) over its K windows;
+    batched_stages: the fix-ups and commits too (one call each for the K windows)."""
     torch = torch_cuda()
     self_lane = n // 2 if self_lane is None else self_lane
     Sp = ((S + 127) // 128) * 128
@@ -129,7 +131,23 @@ def run_sharded_windows(n, world, K, S, votes, out, stride, seed=42, self_lane=N
         torch.cuda.synchronize()
         for r in range(world):
             rows[:, r] = rows_r[r]
-        for w in range(K):
+        if batched_stages:  # rank-major rows [world][K], as an all-gather of each rank's K rows
+            g = torch.stack(rows_r).contiguous()
+            fixed_r = [torch.zeros((K, 10), dtype=torch.int64, device="cuda") for _ in range(world)]
+            for r, (start, cnt) in enumerate(parts):
+                w0 = start // 32
+                ctxs[r].shard_fixup_windows_async(K, out.data_ptr() + 4 * w0, Sp // 32, cnt, stride, 1 + start, S,
+                                                  recs[r].data_ptr(), cnt, g.data_ptr(), r, world,
+                                                  fixed_r[r].data_ptr(), max_phase=max_phase)
+            torch.cuda.synchronize()
+            fg = torch.stack(fixed_r).contiguous()
+            res_r = [torch.zeros((K, 10), dtype=torch.int64, device="cuda") for _ in range(world)]
+            for r in range(world):
+                ctxs[r].shard_commit_windows_async(K, fg.data_ptr(), world, 1, S, res_r[r].data_ptr())
+            torch.cuda.synchronize()
+            for r in range(world):
+                result[:, r] = res_r[r]
+        for w in range(K if not batched_stages else 0):
             base, off = 1 + w * S, w * Sp
             g = rows[w].contiguous()
             for r, (start, cnt) in enumerate(parts):
@@ -232,17 +250,20 @@ def test_sharded_equals_one_engine(oracle, n, world, sizes, kind):
     (7, 1, 5, 262_144, 2),
     (3, 4, 2, 100_096, 0),
 ])
-def test_shard_windows_launch_equals_per_window(n, world, K, S, kind):
+@pytest.mark.parametrize("batched", [False, True])
+def test_shard_windows_launch_equals_per_window(n, world, K, S, kind, batched):
     """K windows of one shard in ONE launch (rg_phase_step_shard_windows_async) ==
     K per-window shard launches: identical fixed outputs, per-window shard rows
-    (counts, extremes, n_draws), global results (rng_next, watermarks) and engine state."""
+    (counts, extremes, n_draws), global results (rng_next, watermarks) and engine state;
+    batched: the fix-ups and commits of the K windows as one call each as well."""
     torch = torch_cuda()
     votes, stride, total = make_votes(n, [S] * K, kind)
     out_m = torch.zeros(8 * stride, dtype=torch.int32, device="cuda")
     out_w = torch.zeros(8 * stride, dtype=torch.int32, device="cuda")
     state = {"rng_next": 99, "last_committed": 5, "commit_watermark": 1, "steps": 0}
     mp = K * S * 3 // 4
-    res_m, st_m, rows_m = run_sharded_windows(n, world, K, S, votes, out_m, stride, state=state, max_phase=mp)
+    res_m, st_m, rows_m = run_sharded_windows(n, world, K, S, votes, out_m, stride, state=state, max_phase=mp,
+                                              batched_stages=batched)
     res_w, st_w, _, _ = run_sharded(n, world, [S] * K, votes, out_w, stride, state=state, max_phase=mp)
     assert torch.equal(out_m, out_w)
     for w in range(K):
