@@ -1169,8 +1169,8 @@ __device__ __forceinline__ uint32_t take_ticket(Record* rec) {
   return atomicAdd(reinterpret_cast<unsigned int*>(&rec->ticket.v) + zero, 1u);
 }
 
-template <int N, int W, int BLOCK, bool SHARD>
-__global__ __launch_bounds__(BLOCK, 4) void ref_lag_kernel(StepParams p) {  // 4 waves/SIMD: 2 x 512 or 1 x 1024 per CU
+template <int N, int W, int BLOCK, bool SHARD, int OCC = 4>
+__global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  // OCC waves/SIMD: 2 x 512 or 1 x 1024 per CU
   constexpr int B = ctr_bits(N);
   constexpr int WAVES = BLOCK / 64;
   constexpr int kRows = BLOCK / 4;  // ChaCha12 blocks per pass, one per quad of lanes

@@ -4,7 +4,8 @@ per-launch HBM bytes of the REF step kernel -> profiles/pmc_c2.json.
 gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports exactly half the
 bytes of a wide (16 B/lane) coalesced streaming read, so it is doubled; WRITE_SIZE
 is exact for 16 B/lane streaming stores. Both counters are in KB.
-usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> <replicas> <slots_per_launch> <out.json>
+usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> <replicas> <slots_per_launch> <out.json> [kernel_substring]
+(kernel_substring default "ref_": the REF step kernel, tiled or lag)
 """
 import csv
 import glob
@@ -13,7 +14,7 @@ import statistics
 import sys
 
 
-def per_dispatch(d, counter, kernel_sub="ref_step_kernel"):
+def per_dispatch(d, counter, kernel_sub="ref_"):
     """Counter value per dispatch of the headline launch: the step kernel dispatches
     with the largest grid (bench.py also times single-window launches)."""
     rows = []
@@ -36,12 +37,13 @@ def per_dispatch(d, counter, kernel_sub="ref_step_kernel"):
 
 def main():
     fdir, wdir, n, slots, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), sys.argv[5]
-    f = per_dispatch(fdir, "FETCH_SIZE")
-    w = per_dispatch(wdir, "WRITE_SIZE")
+    ks = sys.argv[6] if len(sys.argv) > 6 else "ref_"
+    f = per_dispatch(fdir, "FETCH_SIZE", ks)
+    w = per_dispatch(wdir, "WRITE_SIZE", ks)
     if not f or not w:
-        raise SystemExit(f"no ref_step_kernel rows (fetch {len(f)}, write {len(w)})")
+        raise SystemExit(f"no {ks} rows (fetch {len(f)}, write {len(w)})")
     fk, wk = statistics.median(f), statistics.median(w)
-    res = {"replicas": n, "slots_per_launch": slots, "dispatches": [len(f), len(w)],
+    res = {"replicas": n, "slots_per_launch": slots, "kernel": ks, "dispatches": [len(f), len(w)],
            "fetch_size_kb_median": fk, "write_size_kb_median": wk,
            "hbm_read_bytes_per_launch": 2 * fk * 1024, "hbm_write_bytes_per_launch": wk * 1024,
            "hbm_bytes_per_launch": 2 * fk * 1024 + wk * 1024,
