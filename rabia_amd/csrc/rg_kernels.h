@@ -1192,22 +1192,26 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
   //   the round-2 wait), 4 draws of the parked tile, 5 its stores, 6 loop end->record, 7 iterations,
   //   [8] look-back completion inside the draws, [9] continued look-backs, [10] start, [11] end (absolute),
   //   inside the draws (thread 0): [12] ChaCha blocks, [13] the barrier after them, [14] the selection loop
-  const bool stamps = (p.diag & 4u) != 0;
-  unsigned long long st_acc[13] = {};  // [8] look-back completion, [9] continued, [10-12] draws split
-  unsigned long long st_t = stamps ? __builtin_amdgcn_s_memrealtime() : 0;
-  const unsigned long long st_begin = st_t;
+  // (thread 0 keeps them in LDS: 13 live 64-bit accumulators would cost the loop SGPRs)
+  const bool stamps = (p.diag & 4u) != 0 && tid == 0;
+  __shared__ unsigned long long s_st[16];  // [0-12] accumulators, [13] last stamp, [14] start
+  if (stamps) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (int k = 0; k < 13; k++) s_st[k] = 0;
+    s_st[13] = s_st[14] = t0;
+  }
   auto lap = [&](int k) {
     if (stamps) {
       const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-      st_acc[k] += t - st_t;
-      st_t = t;
+      s_st[k] += t - s_st[13];
+      s_st[13] = t;
     }
   };
 
   // this thread's byte offsets inside a tile's planes; plane strides in bytes
   const uint32_t in_lane = (uint32_t)p.lin.base((uint64_t)tid * W) * 4u;
   const uint32_t out_lane = (uint32_t)p.lout.base((uint64_t)tid * W) * 4u;
-  const uint32_t in_pb = (uint32_t)p.lin.pstride * 4u, out_pb = (uint32_t)p.lout.pstride * 4u;
+  uint32_t in_pb = (uint32_t)p.lin.pstride * 4u, out_pb = (uint32_t)p.lout.pstride * 4u;
   auto in_rsrc = [&](uint32_t t) { return plane_rsrc(p.votes + p.lin.base((uint64_t)t * kTW)); };
   auto out_rsrc = [&](uint32_t t) { return plane_rsrc(p.out + p.lout.base((uint64_t)t * kTW)); };
   auto active = [&](uint32_t t) { return (uint64_t)t * kTW + (uint64_t)tid * W < p.n_words; };
@@ -1323,7 +1327,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
       lds_barrier();
       excl = s_bcast[pk][1];
     }
-    if (stamps) st_acc[9] += lb_done ? 0 : 1;
+    if (stamps) s_st[9] += lb_done ? 0 : 1;
     lap(8);
     if (tid == 0)
       atomic_store_agent(p.lookback + park_tile, ((unsigned long long)tag_inc << 32) | (excl + park_total));
@@ -1489,6 +1493,9 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
   }
   lap(0);
   while (c < p.n_tiles) {
+    // opaque per iteration: the 28 plane offsets (k * stride) are recomputed by SALU
+    // next to their loads and stores instead of living in SGPRs across the loop
+    asm volatile("" : "+s"(in_pb), "+s"(out_pb));
     const bool have_park = park_tile >= 0;
     uint32_t(&pc)[kParkFields][BLOCK][W] = s_park[pk];
     // (1) round 1 of tile c: count_votes + |votes| >= quorum fallback (engine.rs:495-505);
@@ -1600,7 +1607,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
     lap(4);
     store_parked(own, have_park);
     lap(5);
-    st_acc[7]++;
+    if (stamps) s_st[7]++;
     a_draws += vq_count;
     park_tile = (int32_t)c;  // tile c is parked; its look-back poll (prev_tile: the tile just finished)
     park_total = total;
@@ -1627,13 +1634,12 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
     const uint32_t mx = wave_max32(a_max1), mn = wave_min32(a_min);
     if (lane == 0) { red[wave][0] = s0; red[wave][1] = s1; red[wave][2] = mx; red[wave][3] = mn; }
     lds_barrier();
-    if (stamps && tid == 0) {
+    if (stamps) {
       lap(6);
-#pragma unroll
-      for (int k = 0; k < 10; k++) p.dbg[(uint64_t)blockIdx.x * 16 + k] = st_acc[k];
-      p.dbg[(uint64_t)blockIdx.x * 16 + 10] = st_begin;
-      p.dbg[(uint64_t)blockIdx.x * 16 + 11] = st_t;
-      for (int k = 10; k < 13; k++) p.dbg[(uint64_t)blockIdx.x * 16 + k + 2] = st_acc[k];
+      for (int k = 0; k < 10; k++) p.dbg[(uint64_t)blockIdx.x * 16 + k] = s_st[k];
+      p.dbg[(uint64_t)blockIdx.x * 16 + 10] = s_st[14];
+      p.dbg[(uint64_t)blockIdx.x * 16 + 11] = s_st[13];
+      for (int k = 10; k < 13; k++) p.dbg[(uint64_t)blockIdx.x * 16 + k + 2] = s_st[k];
     }
     if (tid == 0) {
       unsigned long long t[kLagStatGranules] = {0, 0, 0, 0, 0, 0xFFFFFFFFull};
