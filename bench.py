@@ -57,19 +57,22 @@ def c3_roofline(r, bytes_slot):
     """C3 is VALU-issue bound (per phase 2n keyed scheduler hashes per slot + the coin),
     not HBM bound. achieved = VALU wave-instructions per launch (per-slot count from the
     SQ_INSTS_VALU pass committed in profiles/r02_pmc_c3.json, tools/pmc_c3.sh) / the live
-    kernel time; peak = 256 CUs x 4 SIMDs x 1/2 wave-instruction per cycle at the 2.4 GHz
-    peak engine clock (MI355X_MICROARCH.md). The HBM fraction is kept beside it."""
+    kernel time; peak = 256 CUs x 4 SIMDs x 1/4 wave64 instruction per cycle (a SIMD issues
+    one wave64 VALU instruction per 4 cycles, MI355X_MICROARCH.md 'vector-instruction ISSUE
+    cost'; the pure-VALU trace kernel reaches 98 % of it, profiles/r03_pmc_c2_sq_*) at the
+    2.4 GHz peak engine clock. The HBM fraction is kept beside it."""
     kern_s = r["kern_ms"] / 1000.0
     hbm = r["S"] * bytes_slot / kern_s / 1e9
-    out = {"bound": "valu", "achieved": None, "peak": 512 * 2.4, "unit": "G VALU wave-instr/s", "frac": None,
+    out = {"bound": "valu", "achieved": None, "peak": 256 * 2.4, "unit": "G VALU wave-instr/s", "frac": None,
            "traffic": None, "kernel_avg_us": r["kern_ms"] * 1000.0, "hbm_gbs": hbm, "hbm_frac": hbm / HBM_PEAK_GBS}
     path = os.path.join(ROOT, "profiles", "r02_pmc_c3.json")
     if os.path.exists(path):
         pmc = json.load(open(path))
         achieved = pmc["valu_wave_instr_per_slot"] * r["S"] / kern_s / 1e9
-        out.update(achieved=achieved, frac=achieved / out["peak"],
-                   counter_issue_util=pmc["valu_issue_util"],
-                   note="counter_issue_util = SQ_INSTS_VALU / (512 x GRBM_GUI_ACTIVE/8 cycles): the same "
+        pd = pmc["per_dispatch"]
+        util = sum(x["SQ_INSTS_VALU"] / (256.0 * x["active_cycles"]) for x in pd) / len(pd)
+        out.update(achieved=achieved, frac=achieved / out["peak"], counter_issue_util=util,
+                   note="counter_issue_util = SQ_INSTS_VALU / (256 x GRBM_GUI_ACTIVE/8 cycles): the same "
                         "ratio at the clock the chip actually ran (DVFS)")
     return out
 

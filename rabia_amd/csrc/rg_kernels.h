@@ -99,17 +99,67 @@ RG_HD void ctr_add(Ctr<B>& c, uint32_t m) {
   }
 }
 
-// Per-slot mask of (count >= q) for a wave-uniform q < 2^B.
+// Per-slot mask of (count >= q) for a wave-uniform 1 <= q < 2^B: the carry out of
+// count + (2^B - q), one majority per bit whose addend bit is a uniform 0 / ~0 (one
+// v_bitop3 per bit on gfx950).
 template <int B>
 RG_HD uint32_t ctr_ge(const Ctr<B>& c, uint32_t q) {
-  uint32_t gt = 0, eq = ~0u;
+  const uint32_t k = (1u << B) - q;
+  uint32_t cy = 0;
 #pragma unroll
-  for (int i = B - 1; i >= 0; i--) {
-    uint32_t qb = ((q >> i) & 1u) ? ~0u : 0u;
-    gt |= eq & c.b[i] & ~qb;
-    eq &= ~(c.b[i] ^ qb);
+  for (int i = 0; i < B; i++) {
+    const uint32_t kb = ((k >> i) & 1u) ? ~0u : 0u;
+    cy = (c.b[i] & kb) | (cy & (c.b[i] | kb));
   }
-  return gt | eq;
+  return cy;
+}
+
+// Bit-sliced population count of N masks (count of set bits per slot position) as a
+// carry-save (Wallace) tree: full adders (xor3, majority: one v_bitop3 each on
+// gfx950) over triples, then the weight-1 sums and weight-2 carries counted the same
+// way and added. n = 5: 6 operations (sequential ctr_add: ~17); n = 9: 14 (~45).
+template <int N>
+struct Csa {
+  static RG_HD void count(const uint32_t* m, uint32_t* out) {
+    if constexpr (N == 1) {
+      out[0] = m[0];
+    } else if constexpr (N == 2) {
+      out[0] = m[0] ^ m[1];
+      out[1] = m[0] & m[1];
+    } else if constexpr (N == 3) {
+      out[0] = m[0] ^ m[1] ^ m[2];
+      out[1] = (m[0] & m[1]) | (m[2] & (m[0] ^ m[1]));
+    } else if constexpr (N >= 4) {
+      constexpr int G = N / 3, R = N % 3, S = G + R;
+      uint32_t sums[S], carries[G];
+#pragma unroll
+      for (int g = 0; g < G; g++) {
+        const uint32_t a = m[3 * g], b = m[3 * g + 1], c = m[3 * g + 2];
+        sums[g] = a ^ b ^ c;
+        carries[g] = (a & b) | (c & (a ^ b));
+      }
+#pragma unroll
+      for (int r = 0; r < R; r++) sums[G + r] = m[3 * G + r];
+      constexpr int BS = ctr_bits(S), BC = ctr_bits(G), B = ctr_bits(N);
+      uint32_t a[BS], b[BC];
+      Csa<S>::count(sums, a);
+      Csa<G>::count(carries, b);
+      out[0] = a[0];  // a + 2b, ripple
+      uint32_t k = 0;
+#pragma unroll
+      for (int i = 1; i < B; i++) {
+        const uint32_t x = i < BS ? a[i] : 0u, y = i - 1 < BC ? b[i - 1] : 0u;
+        out[i] = x ^ y ^ k;
+        k = (x & y) | (k & (x ^ y));
+      }
+    }
+  }
+};
+template <int N>
+RG_HD Ctr<ctr_bits(N)> ctr_count(const uint32_t (&m)[N]) {
+  Ctr<ctr_bits(N)> c;
+  Csa<N>::count(m, c.b);
+  return c;
 }
 
 template <int B>
@@ -661,20 +711,19 @@ __device__ __forceinline__ void r2_decision_ab(const uint32_t (&lo)[N][W], const
                                                uint32_t q, int self, uint32_t v1, uint32_t vq, uint32_t pend,
                                                uint32_t& alo, uint32_t& ahi, uint32_t& blo, uint32_t& bhi) {
   constexpr int B = ctr_bits(N);
-  Ctr<B> c0, c1, cq;
-  ctr_zero(c0); ctr_zero(c1); ctr_zero(cq);
+  uint32_t m0[N], m1[N], mq[N];
   uint32_t sl = 0, sh = 0;
 #pragma unroll
   for (int j = 0; j < N; j++) {
-    const bool me = j == self;
+    const uint32_t keep = j == self ? 0u : ~0u;  // wave-uniform: the self lane counts as absent here
     const uint32_t l = lo[j][i], h = hi[j][i];
-    sl |= me ? l : 0u;
-    sh |= me ? h : 0u;
-    const uint32_t ol = me ? ~0u : l, oh = me ? ~0u : h;  // the self lane counts as absent here
-    ctr_add(c0, ~ol & ~oh);
-    ctr_add(c1, ol & ~oh);
-    ctr_add(cq, ~ol & oh);
+    sl |= l & ~keep;
+    sh |= h & ~keep;
+    m0[j] = ~l & ~h & keep;
+    m1[j] = l & ~h & keep;
+    mq[j] = ~l & h & keep;
   }
+  const Ctr<B> c0 = ctr_count<N>(m0), c1 = ctr_count<N>(m1), cq = ctr_count<N>(mq);
   const bool has_self = (unsigned)self < (unsigned)N;  // self_lane -1: no own vote joins R2
 #pragma unroll
   for (int v = 0; v < 2; v++) {
@@ -741,16 +790,16 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p_arg) {
 #pragma unroll
   for (int i = 0; i < W; i++) {
     const uint32_t vm = valid_mask(w0 + i, p.n_words, p.n_slots);
-    Ctr<B> c0, c1, cp;
-    ctr_zero(c0); ctr_zero(c1); ctr_zero(cp);
-    c0.b[0] = c1.b[0] = cp.b[0] = seq0;  // (the words tally one after another: no 4-word ILP)
+    uint32_t m0[N], m1[N], mp[N];
 #pragma unroll
     for (int j = 0; j < N; j++) {
       const uint32_t lo = r1lo[j][i], hi = r1hi[j][i];
-      ctr_add(c0, ~lo & ~hi);
-      ctr_add(c1, lo & ~hi);
-      ctr_add(cp, ~(lo & hi));
+      m0[j] = ~lo & ~hi;
+      m1[j] = lo & ~hi;
+      mp[j] = ~(lo & hi);
     }
+    m0[0] |= seq0; m1[0] |= seq0; mp[0] |= seq0;  // (the words tally one after another: no 4-word ILP)
+    const Ctr<B> c0 = ctr_count<N>(m0), c1 = ctr_count<N>(m1), cp = ctr_count<N>(mp);
     const uint32_t g0 = ctr_ge(c0, p.q), g1 = ctr_ge(c1, p.q), gp = ctr_ge(cp, p.q);
     const uint32_t v0 = g0 & vm;
     r1v1[i] = ~g0 & g1 & vm;
@@ -1508,16 +1557,16 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
 #pragma unroll
       for (int i = 0; i < W; i++) {
         const uint32_t vm = valid_mask(w0 + i, p.n_words, p.n_slots);
-        Ctr<B> c0, c1, cp;
-        ctr_zero(c0); ctr_zero(c1); ctr_zero(cp);
-        c0.b[0] = c1.b[0] = cp.b[0] = seq0;
+        uint32_t m0[N], m1[N], mp[N];
 #pragma unroll
         for (int j = 0; j < N; j++) {
           const uint32_t lo = r1lo[j][i], hi = r1hi[j][i];
-          ctr_add(c0, ~lo & ~hi);
-          ctr_add(c1, lo & ~hi);
-          ctr_add(cp, ~(lo & hi));
+          m0[j] = ~lo & ~hi;
+          m1[j] = lo & ~hi;
+          mp[j] = ~(lo & hi);
         }
+        m0[0] |= seq0; m1[0] |= seq0; mp[0] |= seq0;  // (a zero: the words tally one after another)
+        const Ctr<B> c0 = ctr_count<N>(m0), c1 = ctr_count<N>(m1), cp = ctr_count<N>(mp);
         const uint32_t g0 = ctr_ge(c0, p.q), g1 = ctr_ge(c1, p.q), gp = ctr_ge(cp, p.q);
         const uint32_t x0 = g0 & vm;
         v1[i] = ~g0 & g1 & vm;
