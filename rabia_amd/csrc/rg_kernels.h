@@ -2545,6 +2545,8 @@ __device__ __forceinline__ uint64_t cluster_key(uint64_t seed, uint32_t phase, u
 
 // The receiver's heard set from its (phase, round, replica) key (cluster_key, which
 // does not depend on the slot: the lane-compacted kernel keeps a table of them).
+// The k-th lowest set bit of avail is picked branch-free (every lane steps through
+// span - 1 clears and keeps the k-th; a loop of k clears diverged across the wave).
 template <int N>
 __device__ __forceinline__ uint32_t heard_mask_k(uint64_t ckey, uint64_t slot, int r, uint32_t q) {
   const uint64_t h = mix64(ckey + slot);
@@ -2555,29 +2557,13 @@ __device__ __forceinline__ uint32_t heard_mask_k(uint64_t ckey, uint64_t slot, i
     if (i + 1 >= q) break;
     const uint32_t span = N - 1 - i;
     const uint32_t k = (uint32_t)((h >> (6 * i)) & 63u) % span;
-    uint32_t a = avail;
-    for (uint32_t t = 0; t < k; t++) a &= a - 1;
-    const uint32_t pick = a & (~a + 1u);
-    mask |= pick;
-    avail &= ~pick;
-  }
-  return mask;
-}
-
-template <int N>
-__device__ __forceinline__ uint32_t heard_mask(uint64_t dseed, uint64_t slot, uint32_t phase, uint32_t round,
-                                               int r, uint32_t q) {
-  const uint64_t h = mix64(cluster_key(dseed, phase, round, r) + slot);
-  uint32_t avail = ((1u << N) - 1u) & ~(1u << r);
-  uint32_t mask = 1u << r;
+    uint32_t a = avail, sel = avail;
 #pragma unroll
-  for (uint32_t i = 0; i + 1 < (uint32_t)N; i++) {  // unrolled: span is a constant, % is a mul-shift
-    if (i + 1 >= q) break;
-    const uint32_t span = N - 1 - i;
-    const uint32_t k = (uint32_t)((h >> (6 * i)) & 63u) % span;
-    uint32_t a = avail;
-    for (uint32_t t = 0; t < k; t++) a &= a - 1;
-    const uint32_t pick = a & (~a + 1u);
+    for (uint32_t t = 1; t < span; t++) {
+      a &= a - 1;
+      sel = t == k ? a : sel;
+    }
+    const uint32_t pick = sel & (~sel + 1u);
     mask |= pick;
     avail &= ~pick;
   }
