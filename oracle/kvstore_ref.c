@@ -21,6 +21,9 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 enum { K_SET = 0, K_GET = 1, K_DELETE = 2, K_EXISTS = 3 };
 enum { R_OK = 0, R_NOT_FOUND, R_KEY_EMPTY, R_KEY_LONG, R_VALUE_LARGE, R_FULL, R_DECODE, R_NOT_APPLIED };
@@ -238,4 +241,66 @@ int or_kv_dump(const or_kv* kv, uint64_t* key_off, uint8_t* keys, uint64_t* val_
     val_off[j] = vp;
   }
   return 0;
+}
+
+/* All-core CPU baseline of the same apply (BASELINE INFRASTRUCTURE ONLY,
+ * tools/bench_c4.py): the commands are partitioned by key hash over `parts`
+ * independent stores, each replayed in total order by one thread. Exact when the
+ * store's only cross-key dependency (StoreFull, store.rs:153-158) cannot fire, i.e.
+ * when live keys + keys created stay below max_keys (every partition gets the whole
+ * max_keys); a command that does not decode goes to partition 0 (it touches no
+ * store). threads <= 0: the OpenMP default. Results are per command, in command order; out[0..2] = live keys,
+ * KVStore.version and total_operations summed over the partitions. */
+static uint64_t part_of(const uint8_t* d, uint64_t len, uint32_t parts) {
+  if (len < 12) return 0;
+  const uint64_t klen = rd64(d + 4);
+  if (klen > len - 12 || klen == 0 || klen > 256) return 0;
+  return fnv1a(d + 12, klen) % parts;
+}
+
+int or_kv_apply_partitioned(uint32_t parts, int threads, uint64_t max_keys, uint64_t max_value_size,
+                            int enable_notifications, const uint8_t* data, const uint64_t* off, uint64_t n,
+                            const uint8_t* mask, uint8_t* results, uint64_t out[3]) {
+  if (!parts || (n && (!data || !off || !results))) return -1;
+#ifdef _OPENMP
+  if (threads <= 0) threads = omp_get_max_threads();
+#else
+  threads = 1;
+#endif
+  uint32_t* pc = (uint32_t*)malloc(n * sizeof(uint32_t) + 1);
+  uint64_t* cnt = (uint64_t*)calloc((size_t)parts + 1, sizeof(uint64_t));
+  uint64_t* idx = (uint64_t*)malloc(n * sizeof(uint64_t) + 8);
+  uint64_t* tot = (uint64_t*)calloc((size_t)parts * 3, sizeof(uint64_t));
+  if (!pc || !cnt || !idx || !tot) { free(pc); free(cnt); free(idx); free(tot); return -1; }
+  int64_t nn = (int64_t)n;
+#pragma omp parallel for schedule(static) num_threads(threads)
+  for (int64_t c = 0; c < nn; c++) {
+    if (mask && !mask[c]) { results[c] = R_NOT_APPLIED; pc[c] = parts; continue; }
+    pc[c] = (uint32_t)part_of(data + off[c], off[c + 1] - off[c], parts);
+  }
+  for (uint64_t c = 0; c < n; c++) if (pc[c] < parts) cnt[pc[c] + 1]++;
+  for (uint32_t p = 0; p < parts; p++) cnt[p + 1] += cnt[p];
+  {
+    uint64_t* cur = (uint64_t*)malloc((size_t)parts * sizeof(uint64_t));
+    if (!cur) { free(pc); free(cnt); free(idx); free(tot); return -1; }
+    memcpy(cur, cnt, (size_t)parts * sizeof(uint64_t));
+    for (uint64_t c = 0; c < n; c++) if (pc[c] < parts) idx[cur[pc[c]]++] = c;  /* ascending within a part */
+    free(cur);
+  }
+  int err = 0;
+#pragma omp parallel for schedule(dynamic, 1) reduction(| : err) num_threads(threads)
+  for (int64_t p = 0; p < (int64_t)parts; p++) {
+    or_kv* kv = or_kv_create(max_keys, max_value_size, enable_notifications);
+    if (!kv) { err |= 1; continue; }
+    for (uint64_t k = cnt[p]; k < cnt[p + 1]; k++) {
+      const uint64_t c = idx[k];
+      results[c] = (uint8_t)apply_one(kv, data + off[c], off[c + 1] - off[c]);
+    }
+    tot[3 * p] = kv->live; tot[3 * p + 1] = kv->version; tot[3 * p + 2] = kv->total_ops;
+    or_kv_destroy(kv);
+  }
+  out[0] = out[1] = out[2] = 0;
+  for (uint32_t p = 0; p < parts; p++) { out[0] += tot[3 * p]; out[1] += tot[3 * p + 1]; out[2] += tot[3 * p + 2]; }
+  free(pc); free(cnt); free(idx); free(tot);
+  return err ? -1 : 0;
 }

@@ -71,6 +71,7 @@ def load():
     lib.or_kv_destroy.argtypes = [ctypes.c_void_p]
     lib.or_kv_apply.argtypes = [ctypes.c_void_p, u8p, u64p, u64, u8p, u8p]
     lib.or_kv_stats.argtypes = [ctypes.c_void_p, u64p]
+    lib.or_kv_apply_partitioned.argtypes = [ctypes.c_uint32, i, u64, u64, i, u8p, u64p, u64, u8p, u8p, u64p]
     lib.or_kv_dump.argtypes = [ctypes.c_void_p, u64p, u8p, u64p, u8p, u32p]
     lib.or_unpack_planes.argtypes = [u32p, i, u64, u64, u8p]
     _lib = lib
@@ -230,6 +231,24 @@ def cluster_trace(n, seed, slot_base, S):
     st = np.zeros((S, n), np.uint8)
     lib.or_cluster_trace(n, seed, slot_base, S, _p(st, u8p))
     return st
+
+
+def kv_apply_partitioned(data, offs, mask=None, parts=16, max_keys=0, max_value_size=0, notify=True, threads=0):
+    """oracle/kvstore_ref.c:or_kv_apply_partitioned — the all-core CPU baseline of the
+    apply (key-hash partitions, one store and one thread each; exact while StoreFull
+    cannot fire). -> (results[n], {live_keys, version, total_operations})."""
+    lib = load()
+    data = np.ascontiguousarray(data, np.uint8)
+    offs = np.ascontiguousarray(offs, np.uint64)
+    n = offs.size - 1
+    res = np.zeros(max(n, 1), np.uint8)
+    out = np.zeros(3, np.uint64)
+    m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+    rc = lib.or_kv_apply_partitioned(parts, threads, max_keys, max_value_size, 1 if notify else 0,
+                                     _p(data if data.size else np.zeros(1, np.uint8), u8p), _p(offs, u64p), n,
+                                     _p(m, u8p) if m is not None else None, _p(res, u8p), _p(out, u64p))
+    assert rc == 0
+    return res[:n], {"live_keys": int(out[0]), "version": int(out[1]), "total_operations": int(out[2])}
 
 
 class KVStoreC:

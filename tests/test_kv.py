@@ -506,3 +506,32 @@ def test_gpu_decode_fast_path_edges(seed):
             got = [int(x) for x in dev.apply_commands(blobs)]
             assert got == ref.apply_commands(blobs)
         _check_state(dev, ref)
+
+
+def test_partitioned_cpu_baseline_equals_sequential():
+    """The all-core C baseline of the apply (key-hash partitions, oracle/kvstore_ref.c:
+    or_kv_apply_partitioned) gives the sequential restatement's results and counters
+    when StoreFull cannot fire (CPU only)."""
+    import oracle_lib as O
+    rng = np.random.default_rng(5)
+    cmds = []
+    for _ in range(20000):
+        k = f"key{int(rng.integers(0, 700))}".encode()
+        op = int(rng.choice([0, 0, 0, 1, 2, 3]))
+        body = op.to_bytes(4, "little") + len(k).to_bytes(8, "little") + k
+        if op == 0:
+            v = bytes(rng.integers(97, 123, int(rng.integers(0, 40))).astype(np.uint8))
+            body += len(v).to_bytes(8, "little") + v
+        cmds.append(body)
+    cmds.append(b"\x05\x00")  # undecodable
+    data = np.frombuffer(b"".join(cmds), np.uint8)
+    offs = np.zeros(len(cmds) + 1, np.uint64)
+    offs[1:] = np.cumsum([len(c) for c in cmds])
+    mask = (rng.random(len(cmds)) < 0.8).astype(np.uint8)
+    seq = O.KVStoreC(max_keys=10_000)
+    exp = seq.apply(data, offs, mask)
+    st = seq.stats()
+    for parts in (1, 3, 16):
+        got, tot = O.kv_apply_partitioned(data, offs, mask, parts=parts, max_keys=10_000)
+        np.testing.assert_array_equal(got, exp)
+        assert tot == {k: st[k] for k in ("live_keys", "version", "total_operations")}
