@@ -75,7 +75,11 @@ typedef struct rg_kv_stats {
   uint64_t ordered_batches;  /* batches applied on the exact in-order path (StoreFull
                                 reachable or a hash collision group too large)          */
   uint64_t flags;            /* nonzero: a capacity fault (1 table slots, 2 heap bytes)
-                                refused a batch; that batch changed nothing              */
+                                refused a batch; that batch changed nothing. Bit 4: a
+                                capacity fault inside the commit pass (the pre-check
+                                should make it impossible): that batch is PARTIALLY
+                                written and its results do not describe the store —
+                                treat the store as lost                               */
   uint64_t last_path;        /* the last batch: 0 keyed replay, 1 ordered replay,
                                 2 refused (capacity fault, results RG_KV_E_CAPACITY)     */
 } rg_kv_stats;

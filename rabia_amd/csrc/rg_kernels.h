@@ -1420,7 +1420,11 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
           }
         }
         lap(12);
+#ifdef RG_EXP_NO_TRAIL
+        if (cb + kRows <= b_last) lds_barrier();  // experiment: the next scan barrier guards s_blk's reuse
+#else
         lds_barrier();
+#endif
       }
     }
     if constexpr (SHARD) {  // draw records, indexed by local draw number (ascending slot order)

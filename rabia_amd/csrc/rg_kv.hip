@@ -58,7 +58,9 @@ constexpr int kBlock = 256;
 constexpr int kMaxRunKeys = 8;             // distinct keys per hash run on the keyed path
 constexpr uint8_t kPending = 0xFF;
 
-enum : uint64_t { kFaultTable = 1, kFaultHeap = 2 };
+// kFaultPartial: a capacity fault raised inside the commit pass (the whole-batch
+// pre-check should make it impossible): that batch is partially written.
+enum : uint64_t { kFaultTable = 1, kFaultHeap = 2, kFaultPartial = 4 };
 
 // Value allocations come in size classes (0, then powers of two >= 16): a SET whose
 // value's class is not above the class of the slot's current value length
@@ -770,7 +772,7 @@ __global__ __launch_bounds__(kBlock) void kv_commit_kernel(BatchView b, StoreVie
         const uint64_t koff = heap_pos, voff = heap_pos + r.key_len;
         heap_pos += r.key_len + val_class(r.val_len);
         if (s < 0 || heap_pos > st.heap_cap) {
-          atomicOr(&st.ctr->flags, s < 0 ? kFaultTable : kFaultHeap);
+          atomicOr(&st.ctr->flags, (s < 0 ? kFaultTable : kFaultHeap) | kFaultPartial);
         } else {
           if (r.key_len >= 8 && r.key_len <= 16 && r.val_len >= 8 && r.val_len <= 64) {
             Span<2> ks;  // key and value words all in flight before the stores
@@ -796,7 +798,7 @@ __global__ __launch_bounds__(kBlock) void kv_commit_kernel(BatchView b, StoreVie
           heap_pos += val_class(r.val_len);
         }
         if (dst + r.val_len > st.heap_cap) {
-          atomicOr(&st.ctr->flags, kFaultHeap);
+          atomicOr(&st.ctr->flags, kFaultHeap | kFaultPartial);
         } else {
           copy_fast(st.heap + dst, b.data + r.val_src, r.val_len);
           st.ent[s].val_off = dst;

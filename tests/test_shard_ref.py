@@ -389,3 +389,77 @@ def test_two_process_gloo(oracle):
         dec = decode_outputs(np.frombuffer(raw, np.uint32).reshape(8, stride), cnt)
         for k in exp:
             np.testing.assert_array_equal(dec[k], exp[k][start:start + cnt], err_msg=f"rank {rank} {k}")
+
+
+def test_pipelined_two_streams_equals_one_engine():
+    """The C5 schedule on two shards (two contexts): each step's K-window shard launch
+    runs on a compute stream while the previous step's fix-ups and commits run on a
+    second stream per context (events only, no host synchronisation between steps),
+    as bench.py pipelines it. Final outputs, per-window results and engine states ==
+    one evaluator over all windows."""
+    torch = torch_cuda()
+    n, world, K, steps, S = 5, 2, 3, 4, 262_144
+    W = K * steps
+    votes, stride, total = make_votes(n, [S] * W, 1, seed=21)
+    Sp = ((S + 127) // 128) * 128
+    out = torch.zeros(8 * stride, dtype=torch.int32, device="cuda")
+    parts = [shard.shard_range(S, world, r, align=128) for r in range(world)]
+    i64 = dict(dtype=torch.int64, device="cuda")
+    rows = torch.zeros((steps, world, K, 10), **i64)
+    g_rows = torch.zeros((steps, world, world, K, 10), **i64)
+    fixed = torch.zeros((steps, world, K, 10), **i64)
+    g_fixed = torch.zeros((steps, world, world, K, 10), **i64)
+    result = torch.zeros((steps, world, K, 10), **i64)
+    recs = [[torch.zeros(K * cnt, **i64) for _, cnt in parts] for _ in range(steps)]
+    ctxs = [PhaseEvaluator(n, self_lane=2, seed=42) for _ in range(world)]
+    comp = [torch.cuda.Stream() for _ in range(world)]
+    fix = [torch.cuda.Stream() for _ in range(world)]
+    torch.cuda.synchronize()
+    try:
+        for t in range(steps):
+            e_main = []
+            for r, (start, cnt) in enumerate(parts):
+                w0 = (t * K * Sp + start) // 32
+                ctxs[r].phase_step_shard_windows_async(K, votes.data_ptr() + 4 * w0, Sp // 32, out.data_ptr() + 4 * w0,
+                                                       Sp // 32, cnt, stride, 1 + t * K * S + start, S,
+                                                       recs[t][r].data_ptr(), cnt, rows[t, r].data_ptr(),
+                                                       stream=comp[r].cuda_stream)
+                e = torch.cuda.Event()
+                e.record(comp[r])
+                e_main.append(e)
+            e_fix = []
+            for r, (start, cnt) in enumerate(parts):  # the row all-gather, then the fix-up
+                with torch.cuda.stream(fix[r]):
+                    for e in e_main:
+                        fix[r].wait_event(e)
+                    g_rows[t, r].copy_(rows[t])
+                    w0 = (t * K * Sp + start) // 32
+                    ctxs[r].shard_fixup_windows_async(K, out.data_ptr() + 4 * w0, Sp // 32, cnt, stride,
+                                                      1 + t * K * S + start, S, recs[t][r].data_ptr(), cnt,
+                                                      g_rows[t, r].data_ptr(), r, world, fixed[t, r].data_ptr(),
+                                                      stream=fix[r].cuda_stream)
+                    e = torch.cuda.Event()
+                    e.record(fix[r])
+                    e_fix.append(e)
+            for r in range(world):  # the final-row all-gather, then the commit
+                with torch.cuda.stream(fix[r]):
+                    for e in e_fix:
+                        fix[r].wait_event(e)
+                    g_fixed[t, r].copy_(fixed[t])
+                    ctxs[r].shard_commit_windows_async(K, g_fixed[t, r].data_ptr(), world, 1 + t * K * S, S,
+                                                       result[t, r].data_ptr(), stream=fix[r].cuda_stream)
+        torch.cuda.synchronize()
+        states = [ev.get_state() for ev in ctxs]
+    finally:
+        for ev in ctxs:
+            ev.close()
+    out_1 = torch.zeros(8 * stride, dtype=torch.int32, device="cuda")
+    res_1, st_1 = run_single(n, [S] * W, votes, out_1, stride, self_lane=2)
+    assert torch.equal(out, out_1)
+    got = result.cpu().numpy().view(np.uint64)
+    for t in range(steps):
+        for r in range(world):
+            for k in range(K):
+                g = shard.row_result(got[t, r, k].tolist())
+                assert {f: g[f] for f in RES_CMP} == {f: res_1[t * K + k][f] for f in RES_CMP}, (t, r, k)
+    assert all(st == st_1 for st in states)
