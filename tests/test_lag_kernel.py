@@ -99,14 +99,14 @@ def test_lag_small_grid_large_launch():
     assert torch.equal(o1, o2) and (r1 == r2).all() and s1 == s2
 
 
-@pytest.mark.parametrize("S", [1 << 26, 1 << 23])
+@pytest.mark.parametrize("S", [1 << 29, 1 << 26, 1 << 23])
 def test_lag_concurrent_contexts_two_streams(S):
-    """Two contexts on one GPU launch REF steps on two streams at once. At 2^26 slots
-    the lag kernel takes tiles by ticket, so neither launch can wait on a workgroup
-    that the other holds off the GPU (the tiled kernel's cross-kernel look-back
-    cycle); at 2^23 slots the tiled kernel runs and the C ABI chains the two contexts'
-    launches through its per-device event. Both finish with flags 0 and outputs equal
-    to serial runs."""
+    """Two contexts on one GPU launch REF steps on two streams at once. At 2^29 slots
+    the lag kernel runs (>= 32 tiles per CU) and takes tiles by ticket, so neither
+    launch can wait on a workgroup that the other holds off the GPU (the tiled
+    kernel's cross-kernel look-back cycle); at 2^26 and 2^23 slots the tiled kernel
+    runs and the C ABI chains the two contexts' launches through its per-device event.
+    Both finish with flags 0 and outputs equal to serial runs."""
     torch = torch_cuda()
     n = 5
     stride = ((S + 127) // 128) * 4
