@@ -1420,11 +1420,10 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
           }
         }
         lap(12);
-#ifdef RG_EXP_NO_TRAIL
-        if (cb + kRows <= b_last) lds_barrier();  // experiment: the next scan barrier guards s_blk's reuse
-#else
-        lds_barrier();
-#endif
+        // only between passes: after the last one the next iteration's scan barrier
+        // orders these reads before the next writes of s_blk (686.5 -> 670.9 us per
+        // 2^30 slots, interleaved A/B)
+        if (cb + kRows <= b_last) lds_barrier();
       }
     }
     if constexpr (SHARD) {  // draw records, indexed by local draw number (ascending slot order)
@@ -1537,17 +1536,12 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
     uint32_t voff0 = any ? in_off(c) : 0u;
     LAG_CHK_IN(any ? c : 0u, voff0, 2 * N);
     buf_ld_planes<N, W>(in_rsrc(any ? c : 0u), voff0, in_pb, 0, r1lo, r1hi);
-#ifndef RG_EXP_R2_LATE
     buf_ld_planes<N, W>(in_rsrc(any ? c : 0u), voff0, in_pb, 2 * N, r2lo, r2hi);
-#endif
     const uint32_t z[W] = {};
     const __amdgpu_buffer_rsrc_t orr = out_rsrc(0u);
 #pragma unroll
     for (int k = 0; k < 5; k++) buf_st<W>(orr, kOffNone, (uint32_t)k * 4u, z);
     lbg = lb_poll(park_tile);  // no parked tile yet: a harmless poll
-#ifdef RG_EXP_R2_LATE
-    buf_ld_planes<N, W>(in_rsrc(any ? c : 0u), voff0, in_pb, 2 * N, r2lo, r2hi);
-#endif
   }
   lap(0);
   while (c < p.n_tiles) {
@@ -1652,9 +1646,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
         const uint32_t vm = valid_mask(w0 + i, p.n_words, p.n_slots);
         alo[i] &= vm; ahi[i] &= vm; blo[i] &= vm; bhi[i] &= vm;
       }
-#ifndef RG_EXP_R2_LATE
       buf_ld_planes<N, W>(nrr, noff, in_pb, 2 * N, r2lo, r2hi);
-#endif
       lds_st<W>(pc[4][tid], alo);
       lds_st<W>(pc[5][tid], ahi);
       lds_st<W>(pc[6][tid], blo);
@@ -1674,9 +1666,6 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
     park_thr = wave_off + incl - vq_count;
     lbg = lb_poll(park_tile);  // (issued ahead of the next round-2 loads instead: 877 vs 705 us per 2^30
                                // slots, its predecessors not yet published: continued look-backs)
-#ifdef RG_EXP_R2_LATE  // experiment: the next round-2 planes behind the poll (the poll's wait no longer covers them)
-    buf_ld_planes<N, W>(nrr, noff, in_pb, 2 * N, r2lo, r2hi);
-#endif
     pk ^= 1u;
     c = nx;
   }
