@@ -137,10 +137,6 @@ struct Disp {
     if constexpr (N <= 10)
       hipLaunchKernelGGL((ref_lag_kernel<N, lag_words(N), kLagBlock, false>), dim3(grid), dim3(kLagBlock), 0, s, p);
   }
-  static void ref_lag_w4(uint32_t grid, hipStream_t s, const StepParams& p) {  // A/B shape (diag bit 23)
-    if constexpr (N == 5)
-      hipLaunchKernelGGL((ref_lag_kernel<N, 4, 512, false, 2>), dim3(grid), dim3(512), 0, s, p);
-  }
   static void ref_lag512(uint32_t grid, hipStream_t s, const StepParams& p) {
     if constexpr (N <= 10)
       hipLaunchKernelGGL((ref_lag_kernel<N, lag_words(N), kLagBlockSmall, false>), dim3(grid), dim3(kLagBlockSmall),
@@ -179,7 +175,6 @@ const StepLaunch kRefLaunch[17] = RG_TABLE(ref);
 using LagLaunch = void (*)(uint32_t, hipStream_t, const StepParams&);
 const LagLaunch kRefLagLaunch[17] = RG_TABLE(ref_lag);
 const LagLaunch kRefLag512Launch[17] = RG_TABLE(ref_lag512);
-const LagLaunch kRefLagW4Launch[17] = RG_TABLE(ref_lag_w4);
 const StepLaunch kWmvcLaunch[17] = RG_TABLE(wmvc);
 const DigestLaunch kDigestLaunch[17] = RG_TABLE(digest);
 using ClusterLcLaunch = void (*)(uint32_t, hipStream_t, const uint32_t*, uint64_t, uint64_t, uint64_t, uint32_t,
@@ -456,8 +451,6 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
                    ((ctx->diag & 0x200000u) ? !wmvc : (lag_ok && lag_big && !(ctx->diag & 0x100000u)));
   const bool lag1024 = lag && !(ctx->diag & 0x400000u) &&
                        n_words >= 2ull * ctx->n_cu * kLagBlock * (uint64_t)lag_words(n);
-  // A/B (diag bit 23, n = 5): 512 threads x 4 words (16-B plane loads), 2 waves per SIMD
-  const bool lag_w4 = lag1024 && n == 5 && !shard && (ctx->diag & 0x800000u);
   const uint64_t lag_block = lag1024 ? kLagBlock : kLagBlockSmall;
   uint64_t tile_words = lag ? lag_block * lag_words(n) : (uint64_t)cfg_block(cfg) * cfg_words(cfg, n);
   uint64_t n_tiles = (n_words + tile_words - 1) / tile_words;
@@ -528,7 +521,6 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
   if (shard)
     launch_ref_shard(n, lag ? (lag1024 ? -1 : 0) : cfg_block(cfg), cfg_words(cfg, n),
                      lag ? lag_grid : (uint32_t)n_tiles, s, p);
-  else if (lag_w4) kRefLagW4Launch[n](lag_grid, s, p);
   else if (lag1024) kRefLagLaunch[n](lag_grid, s, p);
   else if (lag) kRefLag512Launch[n](lag_grid, s, p);
   else (wmvc ? kWmvcLaunch : kRefLaunch)[n](cfg, (uint32_t)n_tiles, s, p);

@@ -1055,24 +1055,11 @@ __global__ void kv_trace_fill_kernel(uint64_t seed, uint64_t n, uint64_t key_spa
   }
 }
 
-// Stable (bucket, index) sort. RG_KV_SORT_BITS (experiment builds): rocprim onesweep
-// with that many bits per pass and RG_KV_SORT_BLOCK x RG_KV_SORT_IPT tiles instead of
-// hipCUB's tuned default (8 bits per pass).
-#ifndef RG_KV_SORT_BITS
-#define RG_KV_SORT_BITS 0
-#endif
+// Stable (bucket, index) sort: hipCUB's onesweep radix sort (8-bit digits). Measured
+// alternatives (11-bit digits, narrower bucket keys) were slower: DESIGN.md §4b.
 hipError_t kv_sort(void* tmp, size_t& tb, uint32_t* ka, uint32_t* kb, uint32_t* ia, uint32_t* ib, int n,
                    int bits, hipStream_t s) {
-#if RG_KV_SORT_BITS
-  using cfg = rocprim::radix_sort_config<
-      rocprim::default_config, rocprim::default_config,
-      rocprim::radix_sort_onesweep_config<rocprim::kernel_config<RG_KV_SORT_BLOCK, RG_KV_SORT_IPT>,
-                                          rocprim::kernel_config<RG_KV_SORT_BLOCK, RG_KV_SORT_IPT>, RG_KV_SORT_BITS,
-                                          rocprim::block_radix_rank_algorithm::RG_KV_SORT_RANK>>;
-  return rocprim::radix_sort_pairs<cfg>(tmp, tb, ka, kb, ia, ib, n, 0u, (unsigned)bits, s);
-#else
   return hipcub::DeviceRadixSort::SortPairs(tmp, tb, ka, kb, ia, ib, n, 0, bits, s);
-#endif
 }
 
 }  // namespace
