@@ -79,7 +79,9 @@ def c3_roofline(r, bytes_slot):
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) of the run; without an external launcher (no WORLD_SIZE) N > 1 starts N "
+                         "rank processes itself; under torch.distributed.run it must equal WORLD_SIZE")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--windows", type=int, default=1024)
@@ -200,7 +202,13 @@ def cpu_baseline_c3(a, gpu_info) -> dict:
                       f"per-slot info words equal the GPU's: {agree}"}
 
 
-def cpu_baseline(a, n: int, ev: PhaseEvaluator, stream, windows: int = 256) -> dict:
+def cpu_baseline(a, n: int, r: dict) -> dict:
+    """CPU legs on the GPU box's host cores, rank 0, N = 1. The reported value is the
+    SoA all-core path (oracle/rabia_cpu_soa.c) over the input planes of the bench's own
+    set 0, and its outputs are checked bit for bit against the GPU's output of the last
+    TIMED step that read set 0 (the kernel the headline times: the persistent lag
+    kernel at the C2 shape), from that step's engine position (StdRng draw index,
+    last_committed, watermark: the previous step's result)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
     th = cpu_threads(a)
@@ -228,40 +236,52 @@ def cpu_baseline(a, n: int, ev: PhaseEvaluator, stream, windows: int = 256) -> d
         t.join()
     dtp = time.perf_counter() - t0
     sfp = sum(x[0] for x in out) / dtp
-    # (3) SoA all cores on the GPU's own planar planes (same trace kind/seed)
-    S3 = windows * WINDOW  # 256 windows at n=5: 704 MB of planes, past the host's L3
-    stride = ((S3 + 127) // 128) * 4
-    planar = PhaseEvaluator(n, self_lane=lane, seed=SEED, tile_words=0)
-    votes = torch.empty((4 * n + 1) * stride, dtype=torch.int32, device="cuda")
-    planar.trace_generate_async(N.RG_TRACE_AGREE90, SEED, 1, S3, stride, votes.data_ptr(), stream.cuda_stream)
-    outp = torch.empty(8 * stride, dtype=torch.int32, device="cuda")
-    resd = torch.zeros(10, dtype=torch.int64, device="cuda")
-    planar.phase_step_async(votes.data_ptr(), outp.data_ptr(), S3, stride, 1, result_ptr=resd.data_ptr(),
-                            stream=stream.cuda_stream)
+    # (3) SoA all cores over set 0's planes (planar copy of the slot-tiled buffer)
+    S, T, P = r["S"], r["T"], 4 * n + 1
+    nw = (S + 31) // 32
+    votes, gout = r["sets"][0]
+    res_all = r["res"]
+    t_last = ((a.warmup + a.steps - 1) // a.sets) * a.sets  # the last step that read set 0
+    prev = res_all[t_last - 1] if t_last else None
+    rng0 = int(prev[7]) if prev is not None else 0
+    lc0 = int(prev[5]) if prev is not None else 0
+    wm0 = int(prev[8]) if prev is not None else 1
+    base = 1 + t_last * S
     torch.cuda.synchronize()
-    host = votes.view(4 * n + 1, stride).cpu().numpy().view(np.uint32)
-    gpu_res = resd.cpu().numpy().view(np.uint64)
-    planar.close()
-    del votes, outp
+    if T:
+        tiles = (nw + T - 1) // T
+        host = votes.view(tiles, P, T).permute(1, 0, 2).reshape(P, tiles * T).cpu().numpy().view(np.uint32)
+        g_out = gout.view(tiles, 8, T).permute(1, 0, 2).reshape(8, tiles * T).cpu().numpy().view(np.uint32)
+        stride = tiles * T
+    else:
+        stride = r["stride"]
+        host = votes.view(P, stride).cpu().numpy().view(np.uint32)
+        g_out = gout.view(8, stride).cpu().numpy().view(np.uint32)
     times = []
     for _ in range(5):
         t0 = time.perf_counter()
-        _, sres = O.ref_step_soa(n, q, lane, SEED, 0, 1, host, stride, S3, threads=th)
+        s_out, sres = O.ref_step_soa(n, q, lane, SEED, rng0, base, host, stride, S, 0, lc0, wm0, threads=th)
         times.append(time.perf_counter() - t0)
     dt3 = float(np.median(times))
     soa = sres["n_decided"] / dt3
-    # the CPU fast path and the GPU agree on the same planes (decided count, draws)
-    agree = int(gpu_res[1]) == sres["n_decided"] and int(gpu_res[4]) == sres["n_draws"]
+    gres = dict(zip(N.RESULT_FIELDS, [int(x) for x in res_all[t_last]]))
+    keys = ("n_slots", "n_decided", "n_v1", "n_pending_r1", "n_draws", "last_committed_max", "first_undecided",
+            "rng_next", "commit_watermark")
+    agree_res = all(sres[k] == gres[k] for k in keys)
+    agree_out = bool(np.array_equal(s_out[:, :nw], g_out[:, :nw]))
     g = granted_cpus()
     return {"value": soa, "unit": "slots decided/s", "cores": th, "kind": "port",
             "cpu_model": cpu_model(), "host_cpus": g["host_cpus"], "granted_cpus": g["granted"],
             "affinity_cpus": g["affinity"], "cgroup_quota_cpus": g["cgroup_quota"],
-            "sample": f"SoA all-core path (oracle/rabia_cpu_soa.c, {th} OpenMP threads) over {S3} slots "
-                      f"({windows} x 2^20, agree90, n={n}, the GPU's planar planes), median of 5 = {dt3:.3f} s; "
-                      f"agrees with the GPU step on decided/draws: {agree}",
+            "sample": f"SoA all-core path (oracle/rabia_cpu_soa.c, {th} OpenMP threads) over the bench's set-0 "
+                      f"input ({S} slots, n={n}, agree90), median of 5 = {dt3:.3f} s, from the engine position of "
+                      f"timed step {t_last}; its 8 output planes equal that GPU step's bit for bit: {agree_out}; "
+                      f"step results equal: {agree_res}",
+            "gpu_agrees": agree_out and agree_res,
             "structure_faithful_1t": {"value": sf1, "slots": S1, "seconds": dt1},
             "structure_faithful_per_core": {"value": sfp, "instances": th, "slots_each": S1, "seconds": dtp},
-            "soa_all_cores": {"value": soa, "threads": th, "slots": S3, "seconds": dt3, "gpu_agrees": agree}}
+            "soa_all_cores": {"value": soa, "threads": th, "slots": S, "seconds": dt3, "gpu_step": t_last,
+                              "outputs_equal": agree_out, "results_equal": agree_res}}
 
 
 def load_pmc(path: str, n: int, slots: int):
@@ -332,19 +352,21 @@ def run_single(a, n, S, label):
     timed = res[a.warmup:]
     assert (timed[:, 0] == S).all(), "a timed step did not complete"
     decided = int(timed[:, 1].sum())
+    launch = ev.last_launch()  # the timed steps' kernel shape
     sweep_us = None
     if label == "c2":  # single-window (C2 one sweep) latency, outside the headline
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         reps = 20
+        w_out = torch.empty(layout(n, WINDOW, T)[2], dtype=torch.int32, device="cuda")  # the sets' outputs stay
         e0.record(stream)
         for i in range(reps):
-            ev.phase_step_async(sets[i % a.sets][0].data_ptr(), sets[i % a.sets][1].data_ptr(), WINDOW,
-                                stride, slot_base=1, stream=sp)
+            ev.phase_step_async(sets[i % a.sets][0].data_ptr(), w_out.data_ptr(), WINDOW, stride, slot_base=1,
+                                stream=sp)
         e1.record(stream)
         torch.cuda.synchronize()
         sweep_us = e0.elapsed_time(e1) * 1000.0 / reps
     return {"total_ms": total_ms, "kern_ms": kern_ms, "decided": decided, "sweep_us": sweep_us, "ev": ev,
-            "stream": stream}
+            "stream": stream, "sets": sets, "res": res, "S": S, "T": T, "stride": stride, "launch": launch}
 
 
 # ---------------------------------------------------------------------------
@@ -372,7 +394,7 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, bitmaps):
     (C5) the committed/V1 bitmaps all-gathered, on a second stream. world = 1 runs the
     same pipeline with one shard (the 1-GPU measurement of a shard-size step)."""
     T = a.tile_words
-    K = max(1, a.c5_batch)
+    K = max(1, a.c5_batch) if a.config == "c5" else 1  # C2: one 2^30-slot shard per rank, as at N = 1
     gather = make_gather(dist, a.backend) if world > 1 else (lambda out, inp: out.copy_(inp.unsqueeze(0)))
     stride, in_words, out_words = layout(n, S, T)
     comp = torch.cuda.Stream()
@@ -494,7 +516,7 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, bitmaps):
         dist.all_reduce(tm, op=dist.ReduceOp.MAX)
         total_ms, kern_ms = float(tm[0]), float(tm[1])
     return {"total_ms": total_ms, "kern_ms": kern_ms, "decided": decided, "sweep_us": None, "ev": ev,
-            "stream": comp, "windows_per_launch": K}
+            "stream": comp, "windows_per_launch": K, "launch": ev.last_launch()}
 
 
 # ---------------------------------------------------------------------------
@@ -572,9 +594,45 @@ def run_c3(a, world, rank, dist):
             "info": info}
 
 
+def spawn_ranks(a) -> int:
+    """--gpus N > 1 without an external launcher: start N rank processes of this script
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set as torch.distributed.run sets them,
+    rendezvous on 127.0.0.1) before this process touches the GPU; returns the worst
+    exit code. A rank that fails ends the others (they would wait in a collective)."""
+    import socket
+    import subprocess
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus), LOCAL_WORLD_SIZE=str(a.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0:
+                rc = rc or (code if code > 0 else 128 - code)
+                for o in live:
+                    o.kill()
+        time.sleep(0.2)
+    return rc
+
+
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and (a.gpus or 1) > 1:
+        sys.exit(spawn_ranks(a))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.gpus is not None and a.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.backend == "gloo":  # rehearsal: ranks may share the box's one GPU
@@ -634,11 +692,12 @@ def main():
         value = r["decided"] / (r["total_ms"] / 1000.0)
         alg_bytes = K * S * bytes_per_slot_ref(n)
         achieved = alg_bytes / (r["kern_ms"] / 1000.0) / 1e9
-        cpu = None if (a.no_cpu_baseline or world > 1) else cpu_baseline(
-            a, n, r["ev"], r["stream"], windows=256 if a.config == "c2" else a.c5_windows)
+        cpu = None if (a.no_cpu_baseline or world > 1 or "sets" not in r) else cpu_baseline(a, n, r)
         sharded = "windows_per_launch" in r
-        par = f"slot-shard x{world}" + (f", one engine: sharded draws + fix-up, {K} C5 windows per shard launch"
-                                        if sharded else "")
+        par = f"slot-shard x{world}" + (
+            (f", one engine: sharded draws + fix-up, {K} C5 windows per shard launch" if a.config == "c5" else
+             ", one engine: each rank's 2^30-slot shard at provisional draws, shard rows all-gathered, VQ slots "
+             "re-drawn at their global positions, final rows all-gathered and folded") if sharded else "")
         if a.config == "c5":
             metric = "consensus slots decided/sec (9 replicas, 2^26 slots per step, bitmap all-gather)"
             workload = (f"C5: {n} replicas x {window_slots}-slot windows, {K} per step (one engine), REF sweep "
@@ -669,7 +728,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": load_pmc(a.pmc_file, n, S) if world == 1 else None,
-                         "alg_bytes_per_launch": alg_bytes, "kernel_avg_us": r["kern_ms"] * 1000.0},
+                         "alg_bytes_per_launch": alg_bytes, "kernel_avg_us": r["kern_ms"] * 1000.0,
+                         "kernel": r["launch"]},
             "cpu_baseline": cpu,
             "sweep_1m_us": r["sweep_us"],
         }

@@ -155,6 +155,11 @@ int rg_phase_step(rg_ctx* ctx, const uint32_t* votes_host, uint32_t* out_host,
                   uint64_t n_slots, uint64_t stride_words, uint64_t slot_base,
                   uint64_t phase, uint64_t max_phase, rg_step_result* result_host);
 int rg_last_result(rg_ctx* ctx, rg_step_result* out_host);
+/* The latest result of a later stage, synchronising the device: stage 0 = the shard
+ * fix-up's final row (rg_shard_fixup*_async), 1 = the shard commit's global result
+ * (rg_shard_commit*_async; of the last window), 2 = the follower commit's result
+ * (rg_follower_commit_async). For callers that pass NULL row/result pointers. */
+int rg_last_stage_result(rg_ctx* ctx, int stage, rg_step_result* out_host);
 
 /* ---- Sharded REF: ONE engine (one StdRng stream, engine.rs:59-62) over a window
  * split into contiguous shards, one per GPU. Draw k of shard r is
@@ -178,7 +183,9 @@ int rg_last_result(rg_ctx* ctx, rg_step_result* out_host);
  * fields it owns (shard_draws; rng_next; last_committed / watermark / steps) and its
  * own context-internal scratch. Each stage's calls must be stream-ordered among
  * themselves, and (3)/(4) of a window after (3)/(4) of the window before it.
- * row_dev / result_dev may be NULL. */
+ * row_dev / result_dev may be NULL: the context then keeps the latest fix-up's and
+ * commit's result for rg_last_stage_result (rg_last_result returns phase steps'
+ * results only — a fix-up may run on another stream than the next window's step). */
 int rg_phase_step_shard_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev,
                               uint64_t n_slots, uint64_t stride_words, uint64_t slot_base,
                               uint64_t max_phase, uint64_t* records_dev, uint64_t records_cap,
@@ -194,7 +201,9 @@ int rg_phase_step_shard_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* 
  * fix-up re-draws every VQ slot at its global position, so the fixed outputs, rows
  * and engine state are the same). Stages (2)-(4) then run per window as above, with
  * that window's out buffer, records and rows. The context's last result is the last
- * window's row. */
+ * window's row. For n_windows > 1 the pitches must cover one window's planes (planar:
+ * >= ceil(n_slots/32) words; slot-tiled: >= the window's tiles x planes x tile_words),
+ * else RG_EINVAL: overlapping windows would be patched twice by the fix-up. */
 int rg_phase_step_shard_windows_async(rg_ctx* ctx, uint32_t n_windows, const uint32_t* votes_dev,
                                       uint64_t votes_pitch_words, uint32_t* out_dev, uint64_t out_pitch_words,
                                       uint64_t n_slots, uint64_t stride_words, uint64_t slot_base,
@@ -211,7 +220,9 @@ int rg_shard_fixup_async(rg_ctx* ctx, uint32_t* out_dev, uint64_t n_slots, uint6
  * records at records_dev + w * records_cap; rows_out_dev[w] = its final row. The
  * commit folds [n_shards][n_windows] final rows window by window (window w =
  * [window_base + w * window_slots, + window_slots)) into results_dev[w]. Equivalent
- * to the per-window calls in window order. */
+ * to the per-window calls in window order. window_slots of the commit must equal the
+ * window_stride the step and the fix-up were given (window w's slot ids), and
+ * out_pitch_words obeys the step's pitch rule. */
 int rg_shard_fixup_windows_async(rg_ctx* ctx, uint32_t n_windows, uint32_t* out_dev, uint64_t out_pitch_words,
                                  uint64_t n_slots, uint64_t stride_words, uint64_t slot_base, uint64_t window_stride,
                                  uint64_t max_phase, const uint64_t* records_dev, uint64_t records_cap,

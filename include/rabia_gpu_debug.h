@@ -18,6 +18,11 @@ extern "C" {
  *         1024-thread tiles per CU; A/B on large ones);
  * bits 24-31: lag-kernel grid (0 = one workgroup per CU, two in the 512-thread shape). */
 int rg_debug_set(rg_ctx* ctx, uint32_t diag);
+/* The phase-step launch the context issued last (what step_impl picked), 6 words:
+ * kind (0 tiled REF kernel, 1 persistent lag REF kernel, 2 tiled WMVC kernel), shard (0/1),
+ * threads per workgroup, words per thread, grid (tiled: tiles per window; lag: workgroups),
+ * windows (grid.y of a multi-window shard launch). */
+int rg_debug_last_launch(const rg_ctx* ctx, uint32_t* out6);
 int rg_debug_stamps(rg_ctx* ctx, uint64_t* host_out, uint64_t n_words);
 /* REF kernel memory pattern (20 in-planes, 8 out-planes, 16 B/lane) without protocol.
  * tile_words = 0: planar planes `stride` words apart; > 0: slot-tiled layout

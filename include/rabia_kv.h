@@ -79,7 +79,8 @@ typedef struct rg_kv_stats {
                                 capacity fault inside the commit pass (the pre-check
                                 should make it impossible): that batch is PARTIALLY
                                 written and its results do not describe the store —
-                                treat the store as lost                               */
+                                treat the store as lost; the bit stays set and every
+                                later batch is refused (results RG_KV_E_CAPACITY)      */
   uint64_t last_path;        /* the last batch: 0 keyed replay, 1 ordered replay,
                                 2 refused (capacity fault, results RG_KV_E_CAPACITY)     */
 } rg_kv_stats;

@@ -95,6 +95,7 @@ _SIGS = {
     "rg_decision_bitmap_windows_async": (ctypes.c_int, [vp, u32, vp, u64, u64, u64, vp, vp, u64, vp]),
     "rg_shard_commit_async": (ctypes.c_int, [vp, vp, u32, u64, u64, vp, vp]),
     "rg_last_result": (ctypes.c_int, [vp, ctypes.POINTER(RgStepResult)]),
+    "rg_last_stage_result": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(RgStepResult)]),
     "rg_digest_majority_async": (ctypes.c_int, [vp, vp, u64, vp, u64, vp]),
     "rg_coin_async": (ctypes.c_int, [vp, u64, u64, u64, vp, vp]),
     "rg_ref_draws_async": (ctypes.c_int, [vp, u64, u64, vp, vp]),
@@ -130,6 +131,7 @@ _SIGS = {
     # diagnostics (include/rabia_gpu_debug.h)
     "rg_debug_set": (ctypes.c_int, [vp, u32]),
     "rg_debug_stamps": (ctypes.c_int, [vp, vp, u64]),
+    "rg_debug_last_launch": (ctypes.c_int, [vp, vp]),
     "rg_debug_stream_probe": (ctypes.c_int, [vp, vp, u64, u64, u32, u32, vp]),
 }
 

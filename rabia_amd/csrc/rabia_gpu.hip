@@ -61,6 +61,7 @@ struct rg_ctx {
   DevResult* stage_result = nullptr;            // [3]
   uint32_t n_cu = 256;                          // compute units (persistent lag-kernel grid)
   bool chained = false;                         // counted in g_chain[device].live
+  uint32_t last_launch[6] = {};                 // rg_debug_last_launch: kind, shard, block, words, grid, windows
   std::string err;
 };
 
@@ -327,6 +328,7 @@ int rg_create(rg_ctx** out, const rg_config* cfg) {
   if ((e = hipMemcpy(ctx->rec, recs, sizeof recs, hipMemcpyHostToDevice)) != hipSuccess) return bail(e, "init rec");
   if ((e = hipMemcpy(ctx->state, &st, sizeof st, hipMemcpyHostToDevice)) != hipSuccess) return bail(e, "init state");
   if ((e = hipMemcpy(ctx->result, &res, sizeof res, hipMemcpyHostToDevice)) != hipSuccess) return bail(e, "init result");
+  if ((e = hipMemset(ctx->stage_result, 0, 3 * sizeof(DevResult))) != hipSuccess) return bail(e, "init stage results");
   if ((e = hipDeviceSynchronize()) != hipSuccess) return bail(e, "init sync");
   if (ensure_tiles(ctx, 4096, true) != RG_OK) {
     g_err = ctx->err;
@@ -429,6 +431,12 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
   uint64_t need_in, need_out;
   if (int rc = make_layout(ctx, 4 * n + 1, n_words, stride_words, &lin, &need_in, "rg_phase_step")) return rc;
   if (int rc = make_layout(ctx, kOutPlanes, n_words, stride_words, &lout, &need_out, "rg_phase_step")) return rc;
+  if (win.n > 1) {  // window w's planes must not overlap window w + 1's (the fix-up patches them by XOR)
+    const uint64_t min_in = ctx->cfg.tile_words ? need_in : n_words, min_out = ctx->cfg.tile_words ? need_out : n_words;
+    if (win.in_pitch < min_in || win.out_pitch < min_out)
+      return fail(ctx, RG_EINVAL, "rg_phase_step_shard_windows: a pitch is smaller than one window's planes "
+                                  "(planar: ceil(n_slots/32) words; slot-tiled: the window's tiles)");
+  }
   uint32_t force = (ctx->diag >> 8) & 7u;  // diagnostics: force a tile shape of the tiled kernel
   if (force > 3) force = 0;
   int cfg = force ? (int)force - 1 : pick_cfg(n, n_words);
@@ -511,6 +519,12 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
     p.dbg = ctx->dbg;
   }
   hipStream_t s = pick_stream(ctx, stream);
+  ctx->last_launch[0] = lag ? 1u : (wmvc ? 2u : 0u);
+  ctx->last_launch[1] = shard ? 1u : 0u;
+  ctx->last_launch[2] = lag ? (uint32_t)lag_block : (uint32_t)cfg_block(cfg);
+  ctx->last_launch[3] = lag ? (uint32_t)lag_words(n) : (uint32_t)cfg_words(cfg, n);
+  ctx->last_launch[4] = lag ? lag_grid : (uint32_t)n_tiles;
+  ctx->last_launch[5] = win.n;
   std::unique_lock<std::mutex> chain_lk;
   DevChain* dc = (!lag && ctx->chained) ? &g_chain[ctx->cfg.device] : nullptr;
   if (dc) {
@@ -587,6 +601,8 @@ static int fixup_impl(rg_ctx* ctx, uint32_t n_win, uint32_t* out_dev, uint64_t o
   Layout lout;
   uint64_t need;
   if (int rc = make_layout(ctx, kOutPlanes, n_words, stride_words, &lout, &need, "rg_shard_fixup")) return rc;
+  if (n_win > 1 && out_pitch < (ctx->cfg.tile_words ? need : n_words))
+    return fail(ctx, RG_EINVAL, "rg_shard_fixup_windows: out pitch is smaller than one window's output planes");
   if (4ull * n_win > ctx->fix_acc_cap) {
     RG_HIP(ctx, hipDeviceSynchronize());
     (void)hipFree(ctx->fix_acc);
@@ -708,6 +724,15 @@ int rg_last_result(rg_ctx* ctx, rg_step_result* out_host) {
   RG_HIP(ctx, hipDeviceSynchronize());
   RG_HIP(ctx, hipMemcpy(out_host, ctx->result, sizeof(DevResult), hipMemcpyDeviceToHost));
   if (out_host->flags) return fail(ctx, RG_ESTATE, "device-side protocol fault (look-back timeout)");
+  return RG_OK;
+}
+
+int rg_last_stage_result(rg_ctx* ctx, int stage, rg_step_result* out_host) {
+  if (!ctx || !out_host) return fail(ctx, RG_EINVAL, "rg_last_stage_result: null argument");
+  if (stage < 0 || stage > 2) return fail(ctx, RG_EINVAL, "rg_last_stage_result: stage must be 0..2");
+  RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
+  RG_HIP(ctx, hipDeviceSynchronize());
+  RG_HIP(ctx, hipMemcpy(out_host, ctx->stage_result + stage, sizeof(DevResult), hipMemcpyDeviceToHost));
   return RG_OK;
 }
 
@@ -1046,6 +1071,12 @@ int rg_tiled_to_planar(const uint32_t* tiled, uint32_t n_planes, uint64_t n_word
 int rg_debug_set(rg_ctx* ctx, uint32_t diag) {
   if (!ctx) return fail(nullptr, RG_EINVAL, "rg_debug_set: null context");
   ctx->diag = diag;
+  return RG_OK;
+}
+
+int rg_debug_last_launch(const rg_ctx* ctx, uint32_t* out6) {
+  if (!ctx || !out6) return fail(nullptr, RG_EINVAL, "rg_debug_last_launch: null argument");
+  std::memcpy(out6, ctx->last_launch, sizeof ctx->last_launch);
   return RG_OK;
 }
 

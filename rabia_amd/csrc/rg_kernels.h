@@ -291,6 +291,23 @@ __device__ __forceinline__ void atomic_store_agent(unsigned long long* p, unsign
 // Workgroup barrier for LDS hand-offs only. __syncthreads() also drains every
 // outstanding global load and store (its workgroup-scope release waits on
 // vmcnt), which would serialise the tile's HBM traffic behind each barrier.
+// Bounded spins: a wait that lasts longer than kSpinTicks of the constant 100 MHz
+// s_memrealtime clock is a protocol fault, not a wait (the caller raises an error
+// flag instead of hanging). Elapsed time, not an iteration count: other processes'
+// kernels on the same GPU may legitimately delay a ticket holder for a while.
+constexpr unsigned long long kSpinTicks = 400000000ull;  // 4 s
+struct SpinBound {
+  unsigned long long t0 = 0;
+  __device__ __forceinline__ bool expired() {
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    if (t0 == 0) {
+      t0 = t | 1ull;
+      return false;
+    }
+    return t - t0 > kSpinTicks;
+  }
+};
+
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
@@ -315,7 +332,7 @@ __device__ __forceinline__ uint32_t lookback_exclusive(unsigned long long* statu
   if (lane == 0) atomic_store_agent(status + tile, ((unsigned long long)tag_agg << 32) | agg);
   uint32_t excl = 0;
   int64_t pos = (int64_t)tile - 1;
-  uint32_t spins = 0;
+  SpinBound spin;
   for (;;) {
     const int64_t pidx = pos - lane;
     unsigned long long g = pidx >= 0 ? atomic_load_agent(status + pidx)
@@ -328,7 +345,7 @@ __device__ __forceinline__ uint32_t lookback_exclusive(unsigned long long* statu
     const int first = incl_mask ? __builtin_ctzll(incl_mask) : 64;
     const unsigned long long need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);
     if (notready & need) {
-      if (++spins > (1u << 22)) {  // ~seconds: a protocol fault, not a wait
+      if (spin.expired()) {
         if (lane == 0) {
           atomicOr(err, 1ull);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -364,7 +381,7 @@ __device__ __forceinline__ uint32_t lookback_exclusive_wide(unsigned long long* 
   if (lane == 0) atomic_store_agent(status + tile, ((unsigned long long)tag_agg << 32) | agg);
   uint32_t excl = 0;
   int64_t pos = (int64_t)tile - 1;  // distance 0 = tile - 1
-  uint32_t spins = 0;
+  SpinBound spin;
   int K = kfirst;
   for (;;) {
     unsigned long long g[KMAX];
@@ -391,7 +408,7 @@ __device__ __forceinline__ uint32_t lookback_exclusive_wide(unsigned long long* 
       }
     }
     if (blocked) {
-      if (++spins > (1u << 22)) {
+      if (spin.expired()) {
         if (lane == 0) {
           atomicOr(err, 1ull);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -428,7 +445,6 @@ constexpr int kLBWide = 8;  // granules per lane in a first-generation tile's po
 // thread's tiles in flight at once). No per-tile atomics on shared words:
 // thousands of same-address atomics per launch serialise at the memory side.
 constexpr int kStatGranules = 2;
-constexpr uint32_t kSpinLimit = 1u << 24;
 constexpr uint32_t kStatNone = 0x1FFFFu;
 
 struct TileStats {
@@ -549,13 +565,13 @@ __device__ __forceinline__ void finish_tile(const StepParams& p, Record* rec, Ti
       g[k][0] = i < p.n_tiles ? atomic_load_agent(const_cast<unsigned long long*>(gp)) : tag;
       g[k][1] = i < p.n_tiles ? atomic_load_agent(const_cast<unsigned long long*>(gp) + 1) : tag;
     }
-    uint32_t spins = 0;
+    SpinBound spin;
     for (;;) {
       bool ready = true;
 #pragma unroll
       for (int k = 0; k < kBatch; k++) ready &= ((g[k][0] & kTagMask) == tag) & ((g[k][1] & kTagMask) == tag);
       if (ready) break;
-      if (++spins > kSpinLimit) { v[6] = 2; break; }
+      if (spin.expired()) { v[6] = 2; break; }
       __builtin_amdgcn_s_sleep(2);
 #pragma unroll
       for (int k = 0; k < kBatch; k++) {
@@ -1057,10 +1073,10 @@ __device__ __forceinline__ bool lag_eval(const unsigned long long (&g)[kLagPoll]
 __device__ __forceinline__ uint32_t lag_finish(const unsigned long long* status, int32_t pos, int32_t pp,
                                                uint32_t incl_pp, uint32_t seq, int lane, uint32_t excl,
                                                bool blocked, unsigned long long* err) {
-  uint32_t spins = 0;
+  SpinBound spin;
   for (;;) {
     if (blocked) {
-      if (++spins > (1u << 22)) {  // ~seconds: a protocol fault, not a wait
+      if (spin.expired()) {
         if (lane == 0) {
           atomicOr(err, 1ull);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1721,13 +1737,13 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
     unsigned long long x[kLagStatGranules];
 #pragma unroll
     for (int k = 0; k < kLagStatGranules; k++) x[k] = atomic_load_agent(const_cast<unsigned long long*>(gr) + k);
-    uint32_t spins = 0;
+    SpinBound spin;
     for (;;) {  // visible already (arrival counter): a guard, not a wait
       bool ok = true;
 #pragma unroll
       for (int k = 0; k < kLagStatGranules; k++) ok &= (x[k] & kTagMask) == tag;
       if (ok) break;
-      if (++spins > kSpinLimit) { v[6] = 2; break; }
+      if (spin.expired()) { v[6] = 2; break; }
       __builtin_amdgcn_s_sleep(1);
 #pragma unroll
       for (int k = 0; k < kLagStatGranules; k++) x[k] = atomic_load_agent(const_cast<unsigned long long*>(gr) + k);

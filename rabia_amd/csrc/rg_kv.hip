@@ -7,8 +7,9 @@
 //               and key/value validation (store.rs:463-478), 64-bit key hash, a u32
 //               sort key (hash bucket; "not applied" sorts last), per-block worst-case
 //               growth for the capacity refusal; short commands in one load round trip
-//   2 sort      stable radix sort of (bucket, command index): each key's commands
-//               become one contiguous run, still in total order
+//   2 sort      stable sort of the applied commands by bucket (two levels of 8-bit
+//               counting passes, hand-written): each key's commands become one
+//               contiguous run, still in total order; the rest sort last
 //   3 plan      wave per 1024 sorted positions, decoded fields staged in LDS; run
 //               heads compacted per wave, each lane replays one key's commands in
 //               order (one table lookup per key), writes the result bytes and a
@@ -30,7 +31,6 @@
 #include "rabia_kv.h"
 
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <cstring>
 #include <new>
@@ -45,8 +45,8 @@ constexpr uint64_t kInvalidKey = ~0ull;    // full hash of commands that are not
 // invalid bucket and sort last. A bucket run may hold several hashes: the walkers
 // already split runs into keys by comparing key bytes, and look each key up with
 // its own full hash.
-// (The bucket width is chosen per batch: valid buckets take sbits - 1 bits and the
-// invalid bucket is 1 << (sbits - 1), so a radix sort over sbits bits orders them.)
+// (The bucket width vbits is chosen per batch; the invalid bucket is 1 << vbits, and
+// the sort drops those commands: they need no plan.)
 // Command bytes sit at arbitrary byte offsets: multi-byte fields, key compares and
 // copies go through 1-byte-aligned types (gfx950 global memory takes unaligned
 // dword accesses; little-endian like bincode's fixint encoding).
@@ -284,7 +284,7 @@ constexpr uint32_t kFastKey = 16, kFastVal = 64;  // decode fast path: key <= 16
 __global__ __launch_bounds__(kBlock) void kv_decode_kernel(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ off, uint64_t n, const uint8_t* __restrict__ mask,
     uint64_t max_value, uint64_t hmask, uint64_t bmask, uint32_t invalid_bucket, KvOp* __restrict__ ops,
-    uint32_t* __restrict__ sort_key, uint32_t* __restrict__ sort_idx, uint8_t* __restrict__ results,
+    uint32_t* __restrict__ sort_key, uint8_t* __restrict__ results,
     unsigned long long* __restrict__ set_part, uint8_t* __restrict__ done) {
   const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long sets = 0, set_bytes = 0;  // worst-case growth of the batch (the refusal check)
@@ -366,7 +366,6 @@ __global__ __launch_bounds__(kBlock) void kv_decode_kernel(
   op.hash = key;
   ops[c] = op;
   sort_key[c] = key == kInvalidKey ? invalid_bucket : (uint32_t)hash_bucket(key, bmask);
-  sort_idx[c] = (uint32_t)c;
   done[c] = 0;  // the plan's per-sorted-position marks (multi-key runs), cleared here: no memset launch
   if (op.status != kPending) results[c] = (uint8_t)op.status;
   if (op.status == kPending && op.kind == 0) {
@@ -890,19 +889,23 @@ __global__ __launch_bounds__(kFoldBlock) void kv_decide_kernel(StoreView st, con
   unsigned long long mode = 0;
   // StoreFull unreachable iff live + created <= max_keys (size never exceeds it).
   if (ov || k->live + c > st.max_keys) mode = 1;
+  // an earlier commit pass faulted and left a batch partially written: the store is
+  // lost, and every later batch is refused (the fault bit stays set)
   // capacities: at most 7/8 of the table occupied; heap bytes available. The ordered
   // replay is checked against its worst case (every pending SET a new key and a new
   // value allocation), so a batch either fits whole or is refused before any write.
   const uint64_t cap = st.mask + 1, slot_cap = cap - cap / 8;
   if (mode == 0 && (k->occupied + ns > slot_cap || k->heap_top + bytes > st.heap_cap)) mode = 2;
   if (mode == 1 && (k->occupied + sets > slot_cap || k->heap_top + set_bytes > st.heap_cap)) mode = 2;
+  const bool lost = (k->flags & kFaultPartial) != 0;
+  if (lost) mode = 2;
   k->mode = mode;
   k->batches += 1;
   if (mode == 0) {
     k->occupied += ns;
     k->batch_base = k->heap_top;  // commit writes [batch_base + block_base[b] + ..., ...)
     k->heap_top += bytes;
-  } else if (mode == 2) {
+  } else if (mode == 2 && !lost) {
     const bool table = mode == 2 && (k->occupied + (ov || k->live + c > st.max_keys ? sets : ns) > slot_cap);
     k->flags |= table ? kFaultTable : kFaultHeap;
   }
@@ -1055,11 +1058,389 @@ __global__ void kv_trace_fill_kernel(uint64_t seed, uint64_t n, uint64_t key_spa
   }
 }
 
-// Stable (bucket, index) sort: hipCUB's onesweep radix sort (8-bit digits). Measured
-// alternatives (11-bit digits, narrower bucket keys) were slower: DESIGN.md §4b.
-hipError_t kv_sort(void* tmp, size_t& tb, uint32_t* ka, uint32_t* kb, uint32_t* ia, uint32_t* ib, int n,
-                   int bits, hipStream_t s) {
-  return hipcub::DeviceRadixSort::SortPairs(tmp, tb, ka, kb, ia, ib, n, 0, bits, s);
+// ---- 2 sort: stable (bucket, command index) over the applied commands only --------
+// Two levels, every pass a stable counting sort by an 8-bit digit (so equal buckets
+// keep the total order of their commands):
+//   L1  over the whole batch, grid-wide: the top 8 bits of the bucket. Each block
+//       ranks a 4096-command chunk (kv_l1_hist_kernel counts, kv_l1_scan_kernel turns
+//       the [chunk][digit] counts into global offsets, digit-major, kv_l1_scatter_kernel
+//       writes); commands that are not applied are dropped, so only the applied ones
+//       (about half of a C4 batch) are sorted, and their count lands on the device.
+//   L2  one workgroup per top-digit bin (kv_l2_sort_kernel): LSD over the remaining
+//       bucket bits (<= 23: up to 3 digit passes), in LDS when the bin fits one chunk,
+//       else streamed through global memory chunk by chunk (a hot key's bin). It also
+//       fills the sorted tail [n_applied, n) with the invalid bucket.
+// Chunk ranking (rank_chunk): a wave owns 64 x PER consecutive commands; per round
+// the lanes with equal digits find each other with 8 ballots, the lowest one adds the
+// round's count to the wave's digit counter in LDS, and per-wave counters become
+// per-wave offsets (waves in order): the chunk's commands sorted by digit, stably.
+constexpr int kRadix = 256;
+
+template <int BLOCK, int PER>
+struct SortLds {
+  static constexpr int kWaves = BLOCK / 64, kChunk = BLOCK * PER;
+  uint32_t wcnt[kWaves][kRadix];  // per-wave digit counts -> exclusive offsets over the waves
+  uint32_t dstart[kRadix + 1];    // chunk-local exclusive scan of the digit totals
+  uint32_t scan[kWaves];
+  uint32_t key[kChunk];           // the chunk, sorted by digit
+  uint32_t idx[kChunk];
+};
+
+// Exclusive scan of one value per thread of the first kRadix threads (BLOCK >= kRadix);
+// every thread of the block must call it.
+template <int BLOCK, int PER>
+__device__ __forceinline__ uint32_t radix_excl_scan(SortLds<BLOCK, PER>& s, uint32_t v, uint32_t* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63 && wave < kRadix / 64) s.scan[wave] = incl;
+  __syncthreads();
+  uint32_t before = 0, all = 0;
+#pragma unroll
+  for (int w = 0; w < kRadix / 64; w++) {
+    const uint32_t x = s.scan[w];
+    before += w < wave ? x : 0u;
+    all += x;
+  }
+  __syncthreads();
+  *total = all;
+  return before + incl - v;
+}
+
+// Stable rank of the chunk's commands by digit (key >> shift) & 255; valid[r] marks the
+// commands of round r that take part. Returns each one's chunk-local sorted position;
+// s.dstart holds the digit starts, s.dstart[256] the number of valid commands.
+template <int BLOCK, int PER>
+__device__ __forceinline__ void rank_chunk(SortLds<BLOCK, PER>& s, const uint32_t (&key)[PER], uint32_t valid,
+                                           uint32_t shift, uint32_t (&pos)[PER]) {
+  constexpr int kWaves = BLOCK / 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < kWaves * kRadix; i += BLOCK) (&s.wcnt[0][0])[i] = 0u;
+  __syncthreads();
+  const unsigned long long lt = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int r = 0; r < PER; r++) {
+    const bool v = (valid >> r) & 1u;
+    const uint32_t d = (key[r] >> shift) & 255u;
+    unsigned long long peers = __ballot(v);
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+      const bool bit = (d >> b) & 1u;
+      const unsigned long long m = __ballot(bit);
+      peers &= bit ? m : ~m;
+    }
+    const uint32_t below = (uint32_t)__builtin_popcountll(peers & lt);
+    // one wave's LDS accesses complete in issue order: this round's reads return the
+    // counters before the leaders' writes below, the next round's reads after them
+    const uint32_t base = v ? s.wcnt[wave][d] : 0u;
+    pos[r] = base + below;
+    if (v && below == 0) s.wcnt[wave][d] = base + (uint32_t)__builtin_popcountll(peers);
+  }
+  __syncthreads();
+  uint32_t tot = 0;
+  if (threadIdx.x < kRadix) {
+    const int d = threadIdx.x;
+#pragma unroll
+    for (int w = 0; w < kWaves; w++) {
+      const uint32_t c = s.wcnt[w][d];
+      s.wcnt[w][d] = tot;
+      tot += c;
+    }
+  }
+  uint32_t all;
+  const uint32_t ex = radix_excl_scan(s, threadIdx.x < kRadix ? tot : 0u, &all);
+  if (threadIdx.x < kRadix) s.dstart[threadIdx.x] = ex;
+  if (threadIdx.x == 0) s.dstart[kRadix] = all;
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < PER; r++) {
+    if (!((valid >> r) & 1u)) continue;
+    const uint32_t d = (key[r] >> shift) & 255u;
+    pos[r] += s.dstart[d] + s.wcnt[wave][d];
+  }
+}
+
+// chunk position of thread's round-r command: a wave owns 64 x PER consecutive ones
+template <int BLOCK, int PER>
+__device__ __forceinline__ uint32_t chunk_pos(int r) {
+  return (uint32_t)(threadIdx.x >> 6) * (64u * PER) + (uint32_t)r * 64u + (threadIdx.x & 63);
+}
+
+constexpr int kL1Block = 256, kL1Per = 32, kL1Chunk = kL1Block * kL1Per;   // 8192 commands per L1 chunk
+constexpr int kL2Block = 1024, kL2Per = 16, kL2Chunk = kL2Block * kL2Per;  // 16384 per L2 chunk (in LDS)
+
+struct SortArgs {
+  const uint32_t* key_in;   // decode's buckets, all n commands (invalid_bucket: not applied)
+  uint64_t n;
+  uint32_t invalid_bucket;
+  uint32_t shift1;          // L1 digit = key >> shift1 (the top <= 8 bucket bits)
+  uint32_t passes2;         // L2 digit passes over bits [0, shift1)
+  uint32_t chunks;          // L1 chunks
+  uint32_t* hist;           // [chunks][256] L1 counts, then each digit's count in the chunks before
+  uint32_t* bin_tot;        // [256] L1 bin sizes (applied commands per top digit)
+  uint32_t *a_key, *a_idx;  // L2 ping-pong buffers
+  uint32_t *b_key, *b_idx;  // (L1 writes b; pass p reads b/a and writes a/b; the last writes the final pair)
+};
+
+__global__ __launch_bounds__(kL1Block) void kv_l1_hist_kernel(SortArgs a) {
+  __shared__ uint32_t h[kRadix];
+  for (int d = threadIdx.x; d < kRadix; d += kL1Block) h[d] = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x * kL1Chunk;
+#pragma unroll
+  for (int r = 0; r < kL1Per; r++) {
+    const uint64_t i = base + chunk_pos<kL1Block, kL1Per>(r);
+    if (i < a.n) {
+      const uint32_t k = a.key_in[i];
+      if (k != a.invalid_bucket) atomicAdd(&h[(k >> a.shift1) & 255u], 1u);
+    }
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < kRadix; d += kL1Block) a.hist[(uint64_t)blockIdx.x * kRadix + d] = h[d];
+}
+
+// One workgroup per digit: column d of [chunks][256] -> its exclusive prefix over the
+// chunks (in place) and the digit's total.
+constexpr int kColBlock = 256;
+__global__ __launch_bounds__(kColBlock) void kv_l1_colscan_kernel(SortArgs a) {
+  __shared__ uint32_t w_sum[kColBlock / 64];
+  const uint32_t d = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t carry = 0;
+  for (uint32_t c0 = 0; c0 < a.chunks; c0 += kColBlock) {
+    const uint32_t c = c0 + threadIdx.x;
+    const uint32_t v = c < a.chunks ? a.hist[(uint64_t)c * kRadix + d] : 0u;
+    uint32_t incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
+    }
+    if (lane == 63) w_sum[wave] = incl;
+    __syncthreads();
+    uint32_t before = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < kColBlock / 64; w++) {
+      before += w < wave ? w_sum[w] : 0u;
+      all += w_sum[w];
+    }
+    __syncthreads();
+    if (c < a.chunks) a.hist[(uint64_t)c * kRadix + d] = carry + before + incl - v;
+    carry += all;
+  }
+  if (threadIdx.x == 0) a.bin_tot[d] = carry;
+}
+
+// The L1 bin starts: exclusive scan of the 256 bin totals into s_lo[0..256]
+// (every thread of the block calls it; BLOCK >= 256).
+template <int BLOCK, int PER>
+__device__ __forceinline__ void bin_starts(SortLds<BLOCK, PER>& s, const SortArgs& a, uint32_t* s_lo) {
+  uint32_t all;
+  const uint32_t t = threadIdx.x < kRadix ? a.bin_tot[threadIdx.x] : 0u;
+  const uint32_t ex = radix_excl_scan(s, t, &all);
+  if (threadIdx.x < kRadix) s_lo[threadIdx.x] = ex;
+  if (threadIdx.x == 0) s_lo[kRadix] = all;
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kL1Block) void kv_l1_scatter_kernel(SortArgs a) {
+  __shared__ SortLds<kL1Block, kL1Per> s;
+  __shared__ uint32_t goff[kRadix + 1];
+  const uint64_t base = (uint64_t)blockIdx.x * kL1Chunk;
+  bin_starts(s, a, goff);
+  for (int d = threadIdx.x; d < kRadix; d += kL1Block) goff[d] += a.hist[(uint64_t)blockIdx.x * kRadix + d];
+  uint32_t key[kL1Per], pos[kL1Per], valid = 0;
+#pragma unroll
+  for (int r = 0; r < kL1Per; r++) {
+    const uint64_t i = base + chunk_pos<kL1Block, kL1Per>(r);
+    key[r] = i < a.n ? a.key_in[i] : a.invalid_bucket;
+    valid |= (key[r] != a.invalid_bucket ? 1u : 0u) << r;
+  }
+  rank_chunk(s, key, valid, a.shift1, pos);
+#pragma unroll
+  for (int r = 0; r < kL1Per; r++) {
+    if (!((valid >> r) & 1u)) continue;
+    s.key[pos[r]] = key[r];
+    s.idx[pos[r]] = (uint32_t)(base + chunk_pos<kL1Block, kL1Per>(r));
+  }
+  __syncthreads();
+  const uint32_t nv = s.dstart[kRadix];
+  for (uint32_t p = threadIdx.x; p < nv; p += kL1Block) {  // runs of one digit go to consecutive addresses
+    const uint32_t k = s.key[p], d = (k >> a.shift1) & 255u;
+    const uint32_t dst = goff[d] + (p - s.dstart[d]);
+    a.b_key[dst] = k;
+    a.b_idx[dst] = s.idx[p];
+  }
+}
+
+// L2: one workgroup per L1 bin [lo, hi); pass p sorts by bits [8p, 8p + 8) of the
+// bucket (below shift1). Pass p reads (p even ? b : a) and writes (p even ? a : b);
+// the in-LDS path of a bin that fits one chunk reads b once and writes the final pair
+// once (final = a when the pass count is odd, else b: the same place).
+__global__ __launch_bounds__(kL2Block) void kv_l2_sort_kernel(SortArgs a) {
+  __shared__ SortLds<kL2Block, kL2Per> s;
+  __shared__ uint32_t s_hist[kRadix], s_run[kRadix], s_lo[kRadix + 1];
+  bin_starts(s, a, s_lo);
+  const uint32_t lo = s_lo[blockIdx.x], hi = s_lo[blockIdx.x + 1];
+  const uint32_t n_app = s_lo[kRadix];
+  // the sorted tail: commands that are not applied (the plan's walks stop there)
+  uint32_t* const fin_key = (a.passes2 & 1u) ? a.a_key : a.b_key;
+  for (uint64_t i = n_app + (uint64_t)blockIdx.x * kL2Block + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * kL2Block)
+    fin_key[i] = a.invalid_bucket;
+  const uint32_t cnt = hi - lo;
+  if (a.passes2 == 0 || cnt <= 1) {
+    if (cnt == 1 && (a.passes2 & 1u) && threadIdx.x == 0) {  // a single command: just move it
+      a.a_key[lo] = a.b_key[lo];
+      a.a_idx[lo] = a.b_idx[lo];
+    }
+    return;
+  }
+  uint32_t key[kL2Per], pos[kL2Per];
+  if (cnt <= (uint32_t)kL2Chunk) {  // in LDS: load once, every pass, write once
+    uint32_t valid = 0, idx[kL2Per];
+#pragma unroll
+    for (int r = 0; r < kL2Per; r++) {
+      const uint32_t q = chunk_pos<kL2Block, kL2Per>(r);
+      valid |= (q < cnt ? 1u : 0u) << r;
+      key[r] = q < cnt ? a.b_key[lo + q] : 0u;
+      idx[r] = q < cnt ? a.b_idx[lo + q] : 0u;
+    }
+    for (uint32_t p = 0; p < a.passes2; p++) {
+      rank_chunk(s, key, valid, 8 * p, pos);
+#pragma unroll
+      for (int r = 0; r < kL2Per; r++) {
+        if (!((valid >> r) & 1u)) continue;
+        s.key[pos[r]] = key[r];
+        s.idx[pos[r]] = idx[r];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < kL2Per; r++) {  // the next pass reads the digit-sorted order
+        const uint32_t q = chunk_pos<kL2Block, kL2Per>(r);
+        if (q < cnt) {
+          key[r] = s.key[q];
+          idx[r] = s.idx[q];
+        }
+      }
+      __syncthreads();
+    }
+    uint32_t* const fk = fin_key;
+    uint32_t* const fi = (a.passes2 & 1u) ? a.a_idx : a.b_idx;
+#pragma unroll
+    for (int r = 0; r < kL2Per; r++) {
+      const uint32_t q = chunk_pos<kL2Block, kL2Per>(r);
+      if (q < cnt) {
+        fk[lo + q] = key[r];
+        fi[lo + q] = idx[r];
+      }
+    }
+    return;
+  }
+  // streamed (a bin larger than one chunk: a hot key's): per pass a digit histogram
+  // over the bin, then the chunks in order
+  for (uint32_t p = 0; p < a.passes2; p++) {
+    const uint32_t* sk = (p & 1u) ? a.a_key : a.b_key;
+    const uint32_t* si = (p & 1u) ? a.a_idx : a.b_idx;
+    uint32_t* dk = (p & 1u) ? a.b_key : a.a_key;
+    uint32_t* di = (p & 1u) ? a.b_idx : a.a_idx;
+    const uint32_t shift = 8 * p;
+    for (int d = threadIdx.x; d < kRadix; d += kL2Block) s_hist[d] = 0;
+    __syncthreads();
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += kL2Block) atomicAdd(&s_hist[(sk[i] >> shift) & 255u], 1u);
+    __syncthreads();
+    uint32_t all;
+    const uint32_t ex = radix_excl_scan(s, threadIdx.x < kRadix ? s_hist[threadIdx.x] : 0u, &all);
+    if (threadIdx.x < kRadix) s_run[threadIdx.x] = lo + ex;
+    __syncthreads();
+    for (uint32_t c = lo; c < hi; c += kL2Chunk) {
+      uint32_t valid = 0;
+#pragma unroll
+      for (int r = 0; r < kL2Per; r++) {
+        const uint32_t i = c + chunk_pos<kL2Block, kL2Per>(r);
+        valid |= (i < hi ? 1u : 0u) << r;
+        key[r] = i < hi ? sk[i] : 0u;
+      }
+      rank_chunk(s, key, valid, shift, pos);
+#pragma unroll
+      for (int r = 0; r < kL2Per; r++) {
+        if (!((valid >> r) & 1u)) continue;
+        s.key[pos[r]] = key[r];
+        s.idx[pos[r]] = si[c + chunk_pos<kL2Block, kL2Per>(r)];
+      }
+      __syncthreads();
+      const uint32_t nv = s.dstart[kRadix];
+      for (uint32_t q = threadIdx.x; q < nv; q += kL2Block) {
+        const uint32_t k = s.key[q], d = (k >> shift) & 255u;
+        const uint32_t dst = s_run[d] + (q - s.dstart[d]);
+        dk[dst] = k;
+        di[dst] = s.idx[q];
+      }
+      __syncthreads();
+      if (threadIdx.x < kRadix) s_run[threadIdx.x] += s.dstart[threadIdx.x + 1] - s.dstart[threadIdx.x];
+      __syncthreads();
+    }
+  }
+}
+
+// ---- exclusive scan of u64 (the synthetic trace's command offsets) ----------------
+constexpr int kScanBlock = 1024, kScanPer = 4, kScanChunk = kScanBlock * kScanPer;
+__device__ __forceinline__ unsigned long long block_excl_scan64(unsigned long long v, unsigned long long* total) {
+  __shared__ unsigned long long w_sum[kScanBlock / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  unsigned long long incl = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63) w_sum[wave] = incl;
+  __syncthreads();
+  unsigned long long before = 0, all = 0;
+  for (int w = 0; w < kScanBlock / 64; w++) {
+    before += w < wave ? w_sum[w] : 0ull;
+    all += w_sum[w];
+  }
+  __syncthreads();
+  *total = all;
+  return before + incl - v;
+}
+__global__ __launch_bounds__(kScanBlock) void scan_sums_kernel(const uint64_t* in, uint64_t n, uint64_t* sums) {
+  const uint64_t b = (uint64_t)blockIdx.x * kScanChunk + (uint64_t)threadIdx.x * kScanPer;
+  unsigned long long v = 0;
+  for (int k = 0; k < kScanPer; k++) v += b + k < n ? in[b + k] : 0ull;
+  unsigned long long all;
+  (void)block_excl_scan64(v, &all);
+  if (threadIdx.x == 0) sums[blockIdx.x] = all;
+}
+// one block: the chunk sums scanned in place (sequential over pieces of kScanBlock)
+__global__ __launch_bounds__(kScanBlock) void scan_top_kernel(uint64_t* sums, uint64_t chunks) {
+  unsigned long long carry = 0;
+  for (uint64_t c0 = 0; c0 < chunks; c0 += kScanBlock) {
+    const uint64_t c = c0 + threadIdx.x;
+    const unsigned long long v = c < chunks ? sums[c] : 0ull;
+    unsigned long long all;
+    const unsigned long long ex = block_excl_scan64(v, &all);
+    if (c < chunks) sums[c] = carry + ex;
+    carry += all;
+  }
+}
+__global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(const uint64_t* in, uint64_t n, const uint64_t* sums,
+                                                               uint64_t* out) {
+  const uint64_t b = (uint64_t)blockIdx.x * kScanChunk + (uint64_t)threadIdx.x * kScanPer;
+  unsigned long long x[kScanPer], v = 0;
+  for (int k = 0; k < kScanPer; k++) {
+    x[k] = b + k < n ? in[b + k] : 0ull;
+    v += x[k];
+  }
+  unsigned long long all;
+  unsigned long long run = sums[blockIdx.x] + block_excl_scan64(v, &all);
+  for (int k = 0; k < kScanPer; k++) {
+    if (b + k < n) out[b + k] = run;
+    run += x[k];
+  }
 }
 
 }  // namespace
@@ -1078,12 +1459,13 @@ struct rg_kv {
   KvOp* ops = nullptr;
   uint64_t *need = nullptr, *block_base = nullptr;
   uint32_t *key_a = nullptr, *key_b = nullptr, *idx_a = nullptr, *idx_b = nullptr;
+  uint32_t* sort_hist = nullptr;           // [L1 chunks][256] digit counts -> offsets
+  uint32_t* bin_lo = nullptr;              // [256] L1 bin sizes
+  uint64_t* scan_sums = nullptr;           // trace generator's offset scan: per-chunk sums
   KeyRec* recs = nullptr;
   uint8_t* done = nullptr;
   unsigned long long* part = nullptr;
   unsigned long long* set_part = nullptr;  // [blocks][2] decode partials: pending SETs, worst-case bytes
-  void* tmp = nullptr;
-  size_t tmp_bytes = 0;
   std::string err;
 };
 
@@ -1110,12 +1492,14 @@ StoreView view(rg_kv* kv) {
 void free_scratch(rg_kv* kv) {
   (void)hipFree(kv->ops); (void)hipFree(kv->key_a); (void)hipFree(kv->key_b);
   (void)hipFree(kv->need); (void)hipFree(kv->block_base); (void)hipFree(kv->idx_a);
-  (void)hipFree(kv->idx_b); (void)hipFree(kv->done); (void)hipFree(kv->part); (void)hipFree(kv->tmp);
+  (void)hipFree(kv->idx_b); (void)hipFree(kv->done); (void)hipFree(kv->part);
   (void)hipFree(kv->set_part); (void)hipFree(kv->recs);
+  (void)hipFree(kv->sort_hist); (void)hipFree(kv->bin_lo); (void)hipFree(kv->scan_sums);
   kv->set_part = nullptr; kv->recs = nullptr;
+  kv->sort_hist = kv->bin_lo = nullptr; kv->scan_sums = nullptr;
   kv->ops = nullptr; kv->need = kv->block_base = nullptr;
-  kv->key_a = kv->key_b = kv->idx_a = kv->idx_b = nullptr; kv->done = nullptr; kv->part = nullptr; kv->tmp = nullptr;
-  kv->cap_cmds = 0; kv->tmp_bytes = 0;
+  kv->key_a = kv->key_b = kv->idx_a = kv->idx_b = nullptr; kv->done = nullptr; kv->part = nullptr;
+  kv->cap_cmds = 0;
 }
 
 int ensure_scratch(rg_kv* kv, uint64_t n) {
@@ -1136,11 +1520,9 @@ int ensure_scratch(rg_kv* kv, uint64_t n) {
   KV_HIP(kv, hipMalloc(&kv->done, cap));
   KV_HIP(kv, hipMalloc(&kv->part, blocks * kPCount * 8));
   KV_HIP(kv, hipMalloc(&kv->set_part, blocks * 2 * 8));
-  size_t t1 = 0, t2 = 0;
-  KV_HIP(kv, kv_sort(nullptr, t1, kv->key_a, kv->key_b, kv->idx_a, kv->idx_b, (int)cap, 32, kv->stream));
-  KV_HIP(kv, hipcub::DeviceScan::ExclusiveSum(nullptr, t2, kv->need, kv->need, (int)cap, kv->stream));
-  kv->tmp_bytes = t1 > t2 ? t1 : t2;
-  KV_HIP(kv, hipMalloc(&kv->tmp, kv->tmp_bytes));
+  KV_HIP(kv, hipMalloc(&kv->sort_hist, (cap / kL1Chunk + 1) * kRadix * 4));
+  KV_HIP(kv, hipMalloc(&kv->bin_lo, (kRadix + 1) * 4));
+  KV_HIP(kv, hipMalloc(&kv->scan_sums, (cap / kScanChunk + 2) * 8));
   kv->cap_cmds = cap;
   return 0;
 }
@@ -1245,18 +1627,36 @@ int rg_kv_apply_async(rg_kv* kv, const uint8_t* data_dev, const uint64_t* cmd_of
   int vbits = 14;
   while (vbits < 31 && (1ull << (vbits - 8)) < n_cmds) vbits++;
   if (kv->cfg.bucket_bits && (int)kv->cfg.bucket_bits < vbits) vbits = (int)kv->cfg.bucket_bits;
-  const int sbits = vbits + 1;
   const uint32_t invalid_bucket = 1u << vbits;
   hipLaunchKernelGGL(kv_decode_kernel, dim3(blocks), dim3(kBlock), 0, s, data_dev, cmd_off_dev, n_cmds,
                      apply_mask_dev, kv->cfg.max_value_size,
                      kv->cfg.hash_bits && kv->cfg.hash_bits < 64 ? (1ull << kv->cfg.hash_bits) - 1 : ~0ull,
-                     (uint64_t)invalid_bucket - 1, invalid_bucket, kv->ops, kv->key_a, kv->idx_a,
-                     results_dev, kv->set_part, kv->done);
+                     (uint64_t)invalid_bucket - 1, invalid_bucket, kv->ops, kv->key_a, results_dev, kv->set_part,
+                     kv->done);
   KV_HIP(kv, hipGetLastError());
-  size_t tb = kv->tmp_bytes;
-  KV_HIP(kv, kv_sort(kv->tmp, tb, kv->key_a, kv->key_b, kv->idx_a, kv->idx_b, (int)n_cmds, sbits, s));
-  BatchView b{data_dev, kv->ops, kv->key_b, kv->idx_b, n_cmds, results_dev, kv->done, kv->need,
-              kv->block_base, kv->recs, invalid_bucket, kv->part};
+  // stable (bucket, index) sort of the applied commands (two levels of 8-bit digits)
+  SortArgs sa;
+  sa.key_in = kv->key_a;
+  sa.n = n_cmds;
+  sa.invalid_bucket = invalid_bucket;
+  sa.shift1 = (uint32_t)(vbits > 8 ? vbits - 8 : 0);
+  sa.passes2 = (sa.shift1 + 7) / 8;
+  sa.hist = kv->sort_hist;
+  sa.bin_tot = kv->bin_lo;
+  sa.a_key = kv->key_a;
+  sa.a_idx = kv->idx_a;
+  sa.b_key = kv->key_b;
+  sa.b_idx = kv->idx_b;
+  const uint32_t chunks = (uint32_t)((n_cmds + kL1Chunk - 1) / kL1Chunk);
+  sa.chunks = chunks;
+  hipLaunchKernelGGL(kv_l1_hist_kernel, dim3(chunks), dim3(kL1Block), 0, s, sa);
+  hipLaunchKernelGGL(kv_l1_colscan_kernel, dim3(kRadix), dim3(kColBlock), 0, s, sa);
+  hipLaunchKernelGGL(kv_l1_scatter_kernel, dim3(chunks), dim3(kL1Block), 0, s, sa);
+  hipLaunchKernelGGL(kv_l2_sort_kernel, dim3(kRadix), dim3(kL2Block), 0, s, sa);
+  KV_HIP(kv, hipGetLastError());
+  const bool fin_a = (sa.passes2 & 1u) != 0;
+  BatchView b{data_dev, kv->ops, fin_a ? kv->key_a : kv->key_b, fin_a ? kv->idx_a : kv->idx_b, n_cmds, results_dev,
+              kv->done, kv->need, kv->block_base, kv->recs, invalid_bucket, kv->part};
   const StoreView st = view(kv);
   const uint32_t walk_blocks = (uint32_t)((n_cmds + kWalkBlockSpan - 1) / kWalkBlockSpan);
   hipLaunchKernelGGL(kv_plan_kernel, dim3(walk_blocks), dim3(kBlock), 0, s, b, st);
@@ -1317,8 +1717,11 @@ int rg_kv_trace_async(rg_kv* kv, uint64_t seed, uint64_t n_cmds, uint64_t key_sp
   hipStream_t s = stream ? (hipStream_t)stream : kv->stream;
   const uint32_t blocks = (uint32_t)((n_cmds + 1 + kBlock - 1) / kBlock);
   hipLaunchKernelGGL(kv_trace_size_kernel, dim3(blocks), dim3(kBlock), 0, s, seed, n_cmds, kv->need);
-  size_t tb = kv->tmp_bytes;
-  KV_HIP(kv, hipcub::DeviceScan::ExclusiveSum(kv->tmp, tb, kv->need, cmd_off_dev, (int)(n_cmds + 1), s));
+  const uint64_t m = n_cmds + 1, sc = (m + kScanChunk - 1) / kScanChunk;  // exclusive scan of the sizes
+  hipLaunchKernelGGL(scan_sums_kernel, dim3((uint32_t)sc), dim3(kScanBlock), 0, s, kv->need, m, kv->scan_sums);
+  hipLaunchKernelGGL(scan_top_kernel, dim3(1), dim3(kScanBlock), 0, s, kv->scan_sums, sc);
+  hipLaunchKernelGGL(scan_apply_kernel, dim3((uint32_t)sc), dim3(kScanBlock), 0, s, kv->need, m, kv->scan_sums,
+                     cmd_off_dev);
   hipLaunchKernelGGL(kv_trace_fill_kernel, dim3(blocks), dim3(kBlock), 0, s, seed, n_cmds, key_space, data_dev,
                      cmd_off_dev);
   KV_HIP(kv, hipGetLastError());

@@ -223,6 +223,12 @@ class PhaseEvaluator:
         N.check(self.lib.rg_last_result(self.ctx, ctypes.byref(r)), self.ctx)
         return r.as_dict()
 
+    def last_stage_result(self, stage: int) -> dict:
+        """The latest shard fix-up (0), shard commit (1) or follower commit (2) result."""
+        r = N.RgStepResult()
+        N.check(self.lib.rg_last_stage_result(self.ctx, stage, ctypes.byref(r)), self.ctx)
+        return r.as_dict()
+
     # -- steps ---------------------------------------------------------------
     def phase_step_host(self, window: PhaseWindow, phase: int = 1, max_phase: int = 0):
         """Synchronous step over host planes: returns (out planes, result dict)."""
@@ -355,6 +361,18 @@ class PhaseEvaluator:
     def cluster_trace_async(self, seed, slot_base, n_slots, stride, states_ptr, stream=0):
         N.check(self.lib.rg_cluster_trace_async(self.ctx, seed, slot_base, n_slots, stride, states_ptr,
                                                 stream or None), self.ctx)
+
+    # -- diagnostics (include/rabia_gpu_debug.h) --------------------------------
+    def debug_set(self, diag: int):
+        N.check(self.lib.rg_debug_set(self.ctx, diag), self.ctx)
+
+    def last_launch(self) -> dict:
+        """The kernel shape the last phase step launched (step_impl's pick)."""
+        buf = (ctypes.c_uint32 * 6)()
+        N.check(self.lib.rg_debug_last_launch(self.ctx, buf), self.ctx)
+        kind = ("tiled", "lag", "wmvc")[buf[0]]
+        return {"kernel": kind, "shard": bool(buf[1]), "block": buf[2], "words": buf[3], "grid": buf[4],
+                "windows": buf[5]}
 
     def sync(self, stream=0):
         N.check(self.lib.rg_stream_sync(self.ctx, stream or None), self.ctx)

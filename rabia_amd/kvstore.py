@@ -163,7 +163,7 @@ class DeviceKVStore:
                          r.data_ptr(), None)
         self.sync()
         st = self.stats()
-        if (st["flags"] & ~flags0) & 4:  # a fault inside the commit pass (include/rabia_kv.h)
+        if st["flags"] & 4:  # a fault inside a commit pass, this batch's or an earlier one (include/rabia_kv.h)
             raise N.RabiaGpuError(N.RG_ESTATE, f"kvstore capacity fault during the commit (flags {st['flags']}): "
                                                f"the batch of {n} commands is partially written; the store is lost")
         if st["last_path"] == 2 or st["flags"] != flags0:

@@ -186,6 +186,43 @@ def test_gpu_hash_collision_runs(hash_bits):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n,hot_frac,warm,key_space", [(60000, 0.4, 10, 5000), (30000, 1.0, 0, 1),
+                                                       (50000, 0.2, 200, 20000)])
+def test_gpu_hot_keys_sort_bins(n, hot_frac, warm, key_space):
+    """Skewed batches: a hot key (and warm keys) put far more commands into one
+    top-digit bin of the sort than an LDS chunk holds, so the bin is sorted streamed
+    through global memory (rg_kv.hip kv_l2_sort_kernel); every result and the final
+    store equal the sequential restatement."""
+    rng = random.Random(n + warm)
+    blobs = []
+    for _ in range(n):
+        r = rng.random()
+        if r < hot_frac:
+            key = b"hot"
+        elif r < hot_frac + 0.3 and warm:
+            key = f"warm{rng.randrange(warm)}".encode()
+        else:
+            key = f"key{rng.randrange(key_space)}".encode()
+        x = rng.random()
+        if x < 0.6:
+            blobs.append(R.encode_op(R.SET, key, f"v{rng.randrange(1 << 20)}".encode()))
+        elif x < 0.8:
+            blobs.append(R.encode_op(R.GET, key))
+        elif x < 0.9:
+            blobs.append(R.encode_op(R.DELETE, key))
+        else:
+            blobs.append(R.encode_op(R.EXISTS, key))
+    mask = [1 if rng.random() < 0.7 else 0 for _ in range(n)]
+    with _store(max_value_size=64) as dev:
+        ref = R.KVStoreRef(max_value_size=64)
+        for _ in range(2):
+            got = [int(x) for x in dev.apply_commands(blobs, mask=mask)]
+            exp = [R.NOT_APPLIED if not m else ref.apply_data(b) for b, m in zip(blobs, mask)]
+            assert got == exp
+        _check_state(dev, ref)
+
+
+@pytest.mark.gpu
 def test_gpu_mask_not_applied():
     blobs = [R.encode_op(R.SET, b"a", b"1"), R.encode_op(R.SET, b"a", b"2"), R.encode_op(R.GET, b"b")]
     with _store() as dev:

@@ -38,9 +38,11 @@ def rows_of(t):
 
 
 def run_sharded(n, world, window_sizes, votes, out, stride, seed=42, self_lane=None, state=None, max_phase=0,
-                cap=None, aligned=128, keep=None):
+                cap=None, aligned=128, keep=None, diag=0, launches=None):
     """Every window's stage 1 on every shard first (provisional positions pile up,
-    as in the pipelined bench), then fix-ups and commits window by window."""
+    as in the pipelined bench), then fix-ups and commits window by window.
+    diag: rg_debug_set switches of every context (e.g. the lag kernel forced);
+    launches: gets each stage-1 launch's shape (rg_debug_last_launch)."""
     torch = torch_cuda()
     self_lane = n // 2 if self_lane is None else self_lane
     ctxs = [PhaseEvaluator(n, self_lane=self_lane, seed=seed) for _ in range(world)]
@@ -48,6 +50,8 @@ def run_sharded(n, world, window_sizes, votes, out, stride, seed=42, self_lane=N
         for ev in ctxs:
             if state:
                 ev.set_state(**state)
+            if diag:
+                ev.debug_set(diag)
         W = len(window_sizes)
         rows = torch.zeros((W, world, 10), dtype=torch.int64, device="cuda")
         fixed = torch.zeros((W, world, 10), dtype=torch.int64, device="cuda")
@@ -72,6 +76,8 @@ def run_sharded(n, world, window_sizes, votes, out, stride, seed=42, self_lane=N
                     ctxs[r].phase_step_shard_async(votes.data_ptr() + 4 * w0, out.data_ptr() + 4 * w0, cnt, stride,
                                                    base + start, rec.data_ptr(), c, rows[w, r].data_ptr(),
                                                    max_phase=max_phase)
+                    if launches is not None:
+                        launches.append(ctxs[r].last_launch())
                 else:  # an empty shard still reports a row
                     rows[w, r, 6] = base + S
                     torch.cuda.synchronize()
@@ -104,7 +110,7 @@ def run_sharded(n, world, window_sizes, votes, out, stride, seed=42, self_lane=N
 
 
 def run_sharded_windows(n, world, K, S, votes, out, stride, seed=42, self_lane=None, state=None, max_phase=0,
-                        batched_stages=False):
+                        batched_stages=False, diag=0, launches=None):
     """As run_sharded over K equal windows, but stage 1 of each shard runs as ONE
     multi-window launch (rg_phase_step_shard_windows_async) over its K windows;
     batched_stages: the fix-ups and commits too (one call each for the K windows)."""
@@ -116,6 +122,8 @@ def run_sharded_windows(n, world, K, S, votes, out, stride, seed=42, self_lane=N
         for ev in ctxs:
             if state:
                 ev.set_state(**state)
+            if diag:
+                ev.debug_set(diag)
         rows = torch.zeros((K, world, 10), dtype=torch.int64, device="cuda")
         fixed = torch.zeros((K, world, 10), dtype=torch.int64, device="cuda")
         result = torch.zeros((K, world, 10), dtype=torch.int64, device="cuda")
@@ -128,6 +136,8 @@ def run_sharded_windows(n, world, K, S, votes, out, stride, seed=42, self_lane=N
             ctxs[r].phase_step_shard_windows_async(K, votes.data_ptr() + 4 * w0, Sp // 32, out.data_ptr() + 4 * w0,
                                                    Sp // 32, cnt, stride, 1 + start, S, recs[r].data_ptr(), cnt,
                                                    rows_r[r].data_ptr(), max_phase=max_phase)
+            if launches is not None:
+                launches.append(ctxs[r].last_launch())
         torch.cuda.synchronize()
         for r in range(world):
             rows[:, r] = rows_r[r]
