@@ -501,16 +501,28 @@ static uint64_t cluster_key(uint64_t seed, uint32_t phase, uint32_t round, int r
 }
 
 /* Bit mask (bit j = sender j heard) of receiver r's round `round` in `phase`:
- * itself plus q-1 of the other senders; pick i takes the k-th (ascending) still
- * available sender, k = 6-bit chunk i of one mix64 modulo the number left. */
+ * itself plus q-1 of the other senders (scheduler hash version 2):
+ * h = fmix32(low word of cluster_key ^ slot folded to 32 bits); pick i takes the
+ * k-th (ascending) still available sender, k = (6-bit chunk i % 5 of word i / 5)
+ * * span >> 6, word j + 1 = fmix32(word j + 0x9E3779B9). */
+static uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
 uint32_t or_heard(uint64_t delivery_seed, uint64_t slot, uint32_t phase, uint32_t round,
                   int r, int n, int q) {
-  uint64_t h = mix64(cluster_key(delivery_seed, phase, round, r) + slot);
+  uint32_t s32 = (uint32_t)slot ^ ((uint32_t)(slot >> 32) * 0x9E3779B9u);
+  uint32_t h = fmix32((uint32_t)cluster_key(delivery_seed, phase, round, r) ^ s32);
   uint32_t avail = ((1u << n) - 1u) & ~(1u << r);
   uint32_t mask = 1u << r;
   for (int i = 0; i < q - 1; i++) {
+    if (i && i % 5 == 0) h = fmix32(h + 0x9E3779B9u);
     int span = n - 1 - i;
-    int k = (int)((h >> (6 * i)) & 63u) % span;
+    int k = (int)((((h >> (6 * (i % 5))) & 63u) * (uint32_t)span) >> 6);
     uint32_t a = avail;
     for (int t = 0; t < k; t++) a &= a - 1;
     uint32_t pick = a & (~a + 1u);  /* lowest remaining set bit */

@@ -343,14 +343,27 @@ def _cluster_key(seed, phase, rnd, r):
     return _mix64(seed ^ ((((phase << 32) | (rnd << 16) | r) * 0x9E6C63D0676A9A99) & MASK64))
 
 
+def _fmix32(h):
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & MASK32
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & MASK32
+    return h ^ (h >> 16)
+
+
 def heard(delivery_seed, slot, phase, rnd, r, n, q):
-    """Receiver r hears itself and q-1 others (cluster view)."""
-    h = _mix64((_cluster_key(delivery_seed, phase, rnd, r) + slot) & MASK64)
+    """Receiver r hears itself and q-1 others (scheduler hash version 2):
+    h = fmix32(low word of the receiver key ^ the slot folded to 32 bits); pick i takes
+    the k-th remaining sender, k = (6-bit chunk i % 5 of word i // 5) * span >> 6."""
+    s32 = (slot & MASK32) ^ (((slot >> 32) * 0x9E3779B9) & MASK32)
+    h = _fmix32((_cluster_key(delivery_seed, phase, rnd, r) & MASK32) ^ s32)
     avail = [j for j in range(n) if j != r]
     mask = 1 << r
     for i in range(q - 1):
+        if i and i % 5 == 0:
+            h = _fmix32((h + 0x9E3779B9) & MASK32)
         span = n - 1 - i
-        k = ((h >> (6 * i)) & 63) % span
+        k = (((h >> (6 * (i % 5))) & 63) * span) >> 6
         pick = avail.pop(k)
         mask |= 1 << pick
     return mask

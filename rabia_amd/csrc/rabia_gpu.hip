@@ -51,6 +51,7 @@ struct rg_ctx {
   uint32_t* cluster_coins = nullptr;            // [phases][n_words] common-coin table
   uint64_t cluster_coins_cap = 0;               // words
   unsigned long long* cluster_part = nullptr;  // [blocks][kClusterStats]
+  uint64_t cluster_part_cap = 0;                // blocks
   unsigned long long* cluster_stats = nullptr;  // [kClusterStats]
   unsigned long long* fix_acc = nullptr;        // sharded REF fix-up accumulators [4][windows]
   uint64_t fix_acc_cap = 4;
@@ -946,13 +947,23 @@ int rg_wmvc_cluster_async(rg_ctx* ctx, const uint32_t* states_dev, uint64_t stri
   if (max_phases < 1 || max_phases > 255) return fail(ctx, RG_EINVAL, "rg_wmvc_cluster: max_phases must be 1..255");
   if (slot_base + n_slots > (1ull << 49)) return fail(ctx, RG_EINVAL, "rg_wmvc_cluster: slot ids must be < 2^49");
   RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
+  // one slot per lane to start with, at most 2048 workgroups, unless that leaves a
+  // workgroup more than kClusterChunk slots (its initial states are staged in LDS)
   constexpr uint32_t kGrid = 2048;
   const uint64_t need = (n_slots + 255) / 256;
-  const uint32_t grid = (uint32_t)(need < kGrid ? need : kGrid);
-  if (!ctx->cluster_part) {
-    RG_HIP(ctx, hipMalloc(&ctx->cluster_part, (uint64_t)kGrid * kClusterStats * 8));
-    RG_HIP(ctx, hipMalloc(&ctx->cluster_stats, kClusterStats * 8));
+  const uint64_t by_chunk = (n_slots + kClusterChunk - 1) / kClusterChunk;
+  uint64_t g64 = need < kGrid ? need : kGrid;
+  if (g64 < by_chunk) g64 = by_chunk;
+  const uint32_t grid = (uint32_t)g64;
+  if (grid > ctx->cluster_part_cap) {
+    RG_HIP(ctx, hipDeviceSynchronize());
+    (void)hipFree(ctx->cluster_part);
+    ctx->cluster_part = nullptr;
+    ctx->cluster_part_cap = 0;
+    RG_HIP(ctx, hipMalloc(&ctx->cluster_part, (uint64_t)grid * kClusterStats * 8));
+    ctx->cluster_part_cap = grid;
   }
+  if (!ctx->cluster_stats) RG_HIP(ctx, hipMalloc(&ctx->cluster_stats, kClusterStats * 8));
   hipStream_t s = pick_stream(ctx, stream);
   // coin bits of the first phases precomputed (one ChaCha12 block per 512 slots and
   // phase instead of one per lane and phase); later phases (rare) compute inline
@@ -974,7 +985,7 @@ int rg_wmvc_cluster_async(rg_ctx* ctx, const uint32_t* states_dev, uint64_t stri
                                         ctx->coin_key, ctx->coin_stream, delivery_seed, max_phases, info_dev,
                                         ctx->cluster_part, ctx->cluster_coins, coin_phases, chunk);
   unsigned long long* dst = stats_dev ? reinterpret_cast<unsigned long long*>(stats_dev) : ctx->cluster_stats;
-  hipLaunchKernelGGL(cluster_stats_kernel, dim3(1), dim3(64), 0, s, ctx->cluster_part, grid, dst);
+  hipLaunchKernelGGL(cluster_stats_kernel, dim3(1), dim3(256), 0, s, ctx->cluster_part, grid, dst);
   RG_HIP(ctx, hipGetLastError());
   return RG_OK;
 }

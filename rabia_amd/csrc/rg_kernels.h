@@ -2562,20 +2562,38 @@ __device__ __forceinline__ uint64_t cluster_key(uint64_t seed, uint32_t phase, u
                           0x9E6C63D0676A9A99ull);
 }
 
-// The receiver's heard set from its (phase, round, replica) key (cluster_key, which
-// does not depend on the slot: the lane-compacted kernel keeps a table of them).
-// The k-th lowest set bit of avail is picked branch-free (every lane steps through
-// span - 1 clears and keeps the k-th; a loop of k clears diverged across the wave).
+// Scheduler hash (the build's own definition; version 2, round 4):
+// 32-bit arithmetic. The receiver's key is the low word of cluster_key (a table per
+// workgroup: it does not depend on the slot); the slot id enters folded to 32 bits
+// (once per slot); h = fmix32(key ^ slot) (murmur3's finaliser: two 32-bit multiplies
+// instead of mix64's two 64-bit ones, i.e. 2 instead of 8 quarter-rate multiplies);
+// pick i uses 6-bit chunk i % 5 of word i / 5 (word j + 1 = fmix32(word j + golden))
+// and maps it to [0, span) by a multiply-shift (a full-rate 24-bit multiply) instead
+// of a modulo. Restated in oracle/rabia_oracle.c:or_heard and oracle/rabia_ref.py:heard.
+RG_HD uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+RG_HD uint32_t slot_fold32(uint64_t slot) { return (uint32_t)slot ^ ((uint32_t)(slot >> 32) * 0x9E3779B9u); }
+
+// The receiver's heard set: itself + q - 1 others, pick i the k-th lowest still
+// available sender, picked branch-free (every lane steps through span - 1 clears and
+// keeps the k-th; a loop of k clears diverged across the wave).
 template <int N>
-__device__ __forceinline__ uint32_t heard_mask_k(uint64_t ckey, uint64_t slot, int r, uint32_t q) {
-  const uint64_t h = mix64(ckey + slot);
+__device__ __forceinline__ uint32_t heard_mask_k(uint32_t ck, uint32_t s32, int r, uint32_t q) {
+  uint32_t h = fmix32(ck ^ s32);
   uint32_t avail = ((1u << N) - 1u) & ~(1u << r);
   uint32_t mask = 1u << r;
 #pragma unroll
   for (uint32_t i = 0; i + 1 < (uint32_t)N; i++) {
     if (i + 1 >= q) break;
+    if (i && i % 5 == 0) h = fmix32(h + 0x9E3779B9u);
     const uint32_t span = N - 1 - i;
-    const uint32_t k = (uint32_t)((h >> (6 * i)) & 63u) % span;
+    const uint32_t k = (((h >> (6 * (i % 5))) & 63u) * span) >> 6;  // (a 24-bit product)
     uint32_t a = avail, sel = avail;
 #pragma unroll
     for (uint32_t t = 1; t < span; t++) {
@@ -2623,7 +2641,10 @@ static __global__ void coin_table_kernel(Key key, uint64_t stream, uint64_t slot
 // Lane-compacted cluster kernel: each workgroup owns a contiguous chunk of slots;
 // a lane whose slot terminated takes the next slot of the chunk (wave-aggregated
 // LDS counter), so a wave never idles on its slowest slot (phases per slot vary
-// 1..max). Coins come from coin_table_kernel for phases <= coin_phases.
+// 1..max). Coins come from coin_table_kernel for phases <= coin_phases. The chunk's
+// initial-state words are staged in LDS first (<= kClusterChunk slots: the host sizes
+// the grid for it), so a refill reads LDS instead of waiting on global loads.
+constexpr uint32_t kClusterChunk = 8192;
 template <int N>
 __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* states, uint64_t stride,
                                                               uint64_t n_slots, uint64_t slot_base, uint32_t q,
@@ -2633,22 +2654,32 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
                                                               uint32_t coin_phases, uint64_t chunk) {
   constexpr uint32_t kAll = (1u << N) - 1u;
   constexpr uint32_t kKeyPhases = 32;  // cluster_key table: phases 1..32 (later phases compute theirs)
+  constexpr uint32_t kStageWords = kClusterChunk / 32 + 1;
   __shared__ unsigned long long s_next;
-  __shared__ uint64_t s_ck[kKeyPhases][2][N];
+  __shared__ uint32_t s_ck[kKeyPhases][2][N];
+  __shared__ uint32_t s_st[N][kStageWords];  // the chunk's initial-state words
   const uint64_t n_words = (n_slots + 31) / 32;
   const uint64_t c0 = (uint64_t)blockIdx.x * chunk;
   const uint64_t c1 = c0 + chunk < n_slots ? c0 + chunk : n_slots;
+  const uint64_t w0 = c0 / 32;
   if (threadIdx.x == 0) s_next = c0;
   for (uint32_t e = threadIdx.x; e < kKeyPhases * 2 * N; e += blockDim.x) {
     const uint32_t ph = e / (2 * N), rd = (e / N) % 2, rr = e % N;
-    s_ck[ph][rd][rr] = cluster_key(dseed, ph + 1, rd + 1, (int)rr);
+    s_ck[ph][rd][rr] = (uint32_t)cluster_key(dseed, ph + 1, rd + 1, (int)rr);
+  }
+  if (c1 > c0) {
+    const uint32_t nw = (uint32_t)((c1 - 1) / 32 - w0 + 1);  // <= kStageWords (chunk <= kClusterChunk)
+    for (uint32_t e = threadIdx.x; e < N * nw; e += blockDim.x) {
+      const uint32_t r = e / nw, w = e % nw;
+      s_st[r][w] = states[(uint64_t)r * stride + w0 + w];
+    }
   }
   __syncthreads();
   const int lane = threadIdx.x & 63;
-  unsigned long long acc[kClusterStats] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t acc[kClusterStats] = {0, 0, 0, 0, 0, 0, 0, 0};  // per lane: <= chunk slots, sums < 2^32
   bool active = false;
   uint64_t s = 0, id = 0;
-  uint32_t st = 0, decided = 0, decv = 0, p = 0, first = 0, coins = 0;
+  uint32_t s32 = 0, st = 0, decided = 0, decv = 0, p = 0, first = 0, coins = 0;
   for (;;) {
     const unsigned long long idle = __ballot(!active);
     if (idle) {
@@ -2663,9 +2694,11 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
         if (ns < c1) {
           s = ns;
           id = slot_base + s;
+          s32 = slot_fold32(id);
           st = 0;
+          const uint32_t wl = (uint32_t)(s / 32 - w0);
 #pragma unroll
-          for (int r = 0; r < N; r++) st |= ((states[(uint64_t)r * stride + s / 32] >> (s & 31)) & 1u) << r;
+          for (int r = 0; r < N; r++) st |= ((s_st[r][wl] >> (s & 31)) & 1u) << r;
           decided = decv = first = coins = 0;
           p = 1;
           active = true;
@@ -2679,8 +2712,8 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
     const bool tab = p <= kKeyPhases;
 #pragma unroll
     for (int r = 0; r < N; r++) {
-      const uint64_t ck = tab ? s_ck[p - 1][0][r] : cluster_key(dseed, p, 1, r);
-      const uint32_t h = heard_mask_k<N>(ck, id, r, q);
+      const uint32_t ck = tab ? s_ck[p - 1][0][r] : (uint32_t)cluster_key(dseed, p, 1, r);
+      const uint32_t h = heard_mask_k<N>(ck, s32, r, q);
       const uint32_t c1r = __builtin_popcount(h & st), c0r = __builtin_popcount(h & ~st);
       if (c1r >= q) v1 |= 1u << r;
       else if (c0r < q) vq |= 1u << r;
@@ -2689,8 +2722,8 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
     int coin = -1;
 #pragma unroll
     for (int r = 0; r < N; r++) {
-      const uint64_t ck = tab ? s_ck[p - 1][1][r] : cluster_key(dseed, p, 2, r);
-      const uint32_t h = heard_mask_k<N>(ck, id, r, q);
+      const uint32_t ck = tab ? s_ck[p - 1][1][r] : (uint32_t)cluster_key(dseed, p, 2, r);
+      const uint32_t h = heard_mask_k<N>(ck, s32, r, q);
       const uint32_t c1r = __builtin_popcount(h & v1), cq = __builtin_popcount(h & vq);
       const uint32_t c0r = q - c1r - cq;
       int nv = c0r >= fp1 ? 0 : (c1r >= fp1 ? 1 : -1);
@@ -2740,10 +2773,10 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
   __shared__ unsigned long long red[4][kClusterStats];
   const int wave = threadIdx.x >> 6;
 #pragma unroll
-  for (int k = 0; k < kClusterStats; k++) acc[k] = k == 3 ? wave_max64(acc[k]) : wave_sum64(acc[k]);
-  if (lane == 0)
-#pragma unroll
-    for (int k = 0; k < kClusterStats; k++) red[wave][k] = acc[k];
+  for (int k = 0; k < kClusterStats; k++) {
+    const unsigned long long x = k == 3 ? wave_max64(acc[k]) : wave_sum64(acc[k]);
+    if (lane == 0) red[wave][k] = x;
+  }
   __syncthreads();
   if (threadIdx.x < kClusterStats) {
     const int k = threadIdx.x;
@@ -2767,14 +2800,22 @@ static __global__ __launch_bounds__(256) void cluster_bitmap_kernel(const uint32
   if (lane == 32 && w + 1 < n_words) { decided[w + 1] = (uint32_t)(bd >> 32); v1[w + 1] = (uint32_t)(b1 >> 32); }
 }
 
-static __global__ void cluster_stats_kernel(const unsigned long long* partials, uint32_t nblocks, unsigned long long* out) {
-  const int k = threadIdx.x;
-  if (k >= kClusterStats) return;
+// One 256-thread block: thread t folds field t % 8 of blocks t / 8, t / 8 + 32, ...
+// (every load of a thread in flight together), then the 32 partial folds per field.
+static __global__ __launch_bounds__(256) void cluster_stats_kernel(const unsigned long long* partials,
+                                                                  uint32_t nblocks, unsigned long long* out) {
+  __shared__ unsigned long long red[256];
+  const int t = threadIdx.x, k = t % kClusterStats;
   unsigned long long v = 0;
-  for (uint32_t b = 0; b < nblocks; b++) {
+  for (uint32_t b = t / kClusterStats; b < nblocks; b += 256 / kClusterStats) {
     const unsigned long long x = partials[(uint64_t)b * kClusterStats + k];
     v = k == 3 ? (x > v ? x : v) : v + x;
   }
+  red[t] = v;
+  __syncthreads();
+  if (t >= kClusterStats) return;
+  v = 0;
+  for (int i = t; i < 256; i += kClusterStats) v = k == 3 ? (red[i] > v ? red[i] : v) : v + red[i];
   out[k] = v;
 }
 

@@ -1076,20 +1076,18 @@ __global__ void kv_trace_fill_kernel(uint64_t seed, uint64_t n, uint64_t key_spa
 // per-wave offsets (waves in order): the chunk's commands sorted by digit, stably.
 constexpr int kRadix = 256;
 
-template <int BLOCK, int PER>
-struct SortLds {
-  static constexpr int kWaves = BLOCK / 64, kChunk = BLOCK * PER;
+template <int BLOCK>
+struct RankLds {
+  static constexpr int kWaves = BLOCK / 64;
   uint32_t wcnt[kWaves][kRadix];  // per-wave digit counts -> exclusive offsets over the waves
   uint32_t dstart[kRadix + 1];    // chunk-local exclusive scan of the digit totals
   uint32_t scan[kWaves];
-  uint32_t key[kChunk];           // the chunk, sorted by digit
-  uint32_t idx[kChunk];
 };
 
 // Exclusive scan of one value per thread of the first kRadix threads (BLOCK >= kRadix);
 // every thread of the block must call it.
-template <int BLOCK, int PER>
-__device__ __forceinline__ uint32_t radix_excl_scan(SortLds<BLOCK, PER>& s, uint32_t v, uint32_t* total) {
+template <int BLOCK>
+__device__ __forceinline__ uint32_t radix_excl_scan(RankLds<BLOCK>& s, uint32_t v, uint32_t* total) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t incl = v;
 #pragma unroll
@@ -1115,7 +1113,7 @@ __device__ __forceinline__ uint32_t radix_excl_scan(SortLds<BLOCK, PER>& s, uint
 // commands of round r that take part. Returns each one's chunk-local sorted position;
 // s.dstart holds the digit starts, s.dstart[256] the number of valid commands.
 template <int BLOCK, int PER>
-__device__ __forceinline__ void rank_chunk(SortLds<BLOCK, PER>& s, const uint32_t (&key)[PER], uint32_t valid,
+__device__ __forceinline__ void rank_chunk(RankLds<BLOCK>& s, const uint32_t (&key)[PER], uint32_t valid,
                                            uint32_t shift, uint32_t (&pos)[PER]) {
   constexpr int kWaves = BLOCK / 64;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1170,7 +1168,7 @@ __device__ __forceinline__ uint32_t chunk_pos(int r) {
   return (uint32_t)(threadIdx.x >> 6) * (64u * PER) + (uint32_t)r * 64u + (threadIdx.x & 63);
 }
 
-constexpr int kL1Block = 256, kL1Per = 32, kL1Chunk = kL1Block * kL1Per;   // 8192 commands per L1 chunk
+constexpr int kL1Block = 256, kL1Per = 16, kL1Chunk = kL1Block * kL1Per;   // 4096 commands per L1 chunk
 constexpr int kL2Block = 1024, kL2Per = 16, kL2Chunk = kL2Block * kL2Per;  // 16384 per L2 chunk (in LDS)
 
 struct SortArgs {
@@ -1237,8 +1235,8 @@ __global__ __launch_bounds__(kColBlock) void kv_l1_colscan_kernel(SortArgs a) {
 
 // The L1 bin starts: exclusive scan of the 256 bin totals into s_lo[0..256]
 // (every thread of the block calls it; BLOCK >= 256).
-template <int BLOCK, int PER>
-__device__ __forceinline__ void bin_starts(SortLds<BLOCK, PER>& s, const SortArgs& a, uint32_t* s_lo) {
+template <int BLOCK>
+__device__ __forceinline__ void bin_starts(RankLds<BLOCK>& s, const SortArgs& a, uint32_t* s_lo) {
   uint32_t all;
   const uint32_t t = threadIdx.x < kRadix ? a.bin_tot[threadIdx.x] : 0u;
   const uint32_t ex = radix_excl_scan(s, t, &all);
@@ -1247,11 +1245,17 @@ __device__ __forceinline__ void bin_starts(SortLds<BLOCK, PER>& s, const SortArg
   __syncthreads();
 }
 
+struct L1Lds {
+  RankLds<kL1Block> r;
+  uint32_t key[kL1Chunk];  // the chunk, sorted by digit
+  uint32_t idx[kL1Chunk];
+};
+
 __global__ __launch_bounds__(kL1Block) void kv_l1_scatter_kernel(SortArgs a) {
-  __shared__ SortLds<kL1Block, kL1Per> s;
+  __shared__ L1Lds s;
   __shared__ uint32_t goff[kRadix + 1];
   const uint64_t base = (uint64_t)blockIdx.x * kL1Chunk;
-  bin_starts(s, a, goff);
+  bin_starts(s.r, a, goff);
   for (int d = threadIdx.x; d < kRadix; d += kL1Block) goff[d] += a.hist[(uint64_t)blockIdx.x * kRadix + d];
   uint32_t key[kL1Per], pos[kL1Per], valid = 0;
 #pragma unroll
@@ -1260,7 +1264,7 @@ __global__ __launch_bounds__(kL1Block) void kv_l1_scatter_kernel(SortArgs a) {
     key[r] = i < a.n ? a.key_in[i] : a.invalid_bucket;
     valid |= (key[r] != a.invalid_bucket ? 1u : 0u) << r;
   }
-  rank_chunk(s, key, valid, a.shift1, pos);
+  rank_chunk(s.r, key, valid, a.shift1, pos);
 #pragma unroll
   for (int r = 0; r < kL1Per; r++) {
     if (!((valid >> r) & 1u)) continue;
@@ -1268,27 +1272,37 @@ __global__ __launch_bounds__(kL1Block) void kv_l1_scatter_kernel(SortArgs a) {
     s.idx[pos[r]] = (uint32_t)(base + chunk_pos<kL1Block, kL1Per>(r));
   }
   __syncthreads();
-  const uint32_t nv = s.dstart[kRadix];
+  const uint32_t nv = s.r.dstart[kRadix];
   for (uint32_t p = threadIdx.x; p < nv; p += kL1Block) {  // runs of one digit go to consecutive addresses
     const uint32_t k = s.key[p], d = (k >> a.shift1) & 255u;
-    const uint32_t dst = goff[d] + (p - s.dstart[d]);
+    const uint32_t dst = goff[d] + (p - s.r.dstart[d]);
     a.b_key[dst] = k;
     a.b_idx[dst] = s.idx[p];
   }
 }
 
 // L2: one workgroup per L1 bin [lo, hi); pass p sorts by bits [8p, 8p + 8) of the
-// bucket (below shift1). Pass p reads (p even ? b : a) and writes (p even ? a : b);
-// the in-LDS path of a bin that fits one chunk reads b once and writes the final pair
-// once (final = a when the pass count is odd, else b: the same place).
+// bucket (below shift1). A bin that fits one chunk (the common case) is sorted in LDS:
+// its keys are loaded once and the passes permute a 16-bit index array (two buffers),
+// so neither the keys nor the command indices move until the final gather (a command
+// index is read from global memory, L2-resident, once). A larger bin (a hot key's) is
+// streamed: pass p reads (p even ? b : a) and writes (p even ? a : b), chunk by chunk.
+// Final pair: a when the pass count is odd, else b.
+struct L2Lds {
+  RankLds<kL2Block> r;
+  uint32_t key[kL2Chunk];
+  uint16_t perm[2][kL2Chunk];  // sorted position -> bin-local command
+};
+
 __global__ __launch_bounds__(kL2Block) void kv_l2_sort_kernel(SortArgs a) {
-  __shared__ SortLds<kL2Block, kL2Per> s;
+  __shared__ L2Lds s;
   __shared__ uint32_t s_hist[kRadix], s_run[kRadix], s_lo[kRadix + 1];
-  bin_starts(s, a, s_lo);
+  bin_starts(s.r, a, s_lo);
   const uint32_t lo = s_lo[blockIdx.x], hi = s_lo[blockIdx.x + 1];
   const uint32_t n_app = s_lo[kRadix];
   // the sorted tail: commands that are not applied (the plan's walks stop there)
   uint32_t* const fin_key = (a.passes2 & 1u) ? a.a_key : a.b_key;
+  uint32_t* const fin_idx = (a.passes2 & 1u) ? a.a_idx : a.b_idx;
   for (uint64_t i = n_app + (uint64_t)blockIdx.x * kL2Block + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * kL2Block)
     fin_key[i] = a.invalid_bucket;
   const uint32_t cnt = hi - lo;
@@ -1300,42 +1314,46 @@ __global__ __launch_bounds__(kL2Block) void kv_l2_sort_kernel(SortArgs a) {
     return;
   }
   uint32_t key[kL2Per], pos[kL2Per];
-  if (cnt <= (uint32_t)kL2Chunk) {  // in LDS: load once, every pass, write once
-    uint32_t valid = 0, idx[kL2Per];
-#pragma unroll
-    for (int r = 0; r < kL2Per; r++) {
-      const uint32_t q = chunk_pos<kL2Block, kL2Per>(r);
-      valid |= (q < cnt ? 1u : 0u) << r;
-      key[r] = q < cnt ? a.b_key[lo + q] : 0u;
-      idx[r] = q < cnt ? a.b_idx[lo + q] : 0u;
+  if (cnt <= (uint32_t)kL2Chunk) {
+    for (uint32_t q = threadIdx.x; q < cnt; q += kL2Block) {
+      s.key[q] = a.b_key[lo + q];
+      s.perm[0][q] = (uint16_t)q;
     }
-    for (uint32_t p = 0; p < a.passes2; p++) {
-      rank_chunk(s, key, valid, 8 * p, pos);
+    __syncthreads();
+    uint32_t valid = 0;
+#pragma unroll
+    for (int r = 0; r < kL2Per; r++) valid |= (chunk_pos<kL2Block, kL2Per>(r) < cnt ? 1u : 0u) << r;
+    uint32_t cur = 0;
+    for (uint32_t p = 0; p < a.passes2; p++, cur ^= 1u) {
+      uint32_t j[kL2Per];
 #pragma unroll
       for (int r = 0; r < kL2Per; r++) {
-        if (!((valid >> r) & 1u)) continue;
-        s.key[pos[r]] = key[r];
-        s.idx[pos[r]] = idx[r];
-      }
-      __syncthreads();
-#pragma unroll
-      for (int r = 0; r < kL2Per; r++) {  // the next pass reads the digit-sorted order
         const uint32_t q = chunk_pos<kL2Block, kL2Per>(r);
-        if (q < cnt) {
-          key[r] = s.key[q];
-          idx[r] = s.idx[q];
-        }
+        j[r] = q < cnt ? s.perm[cur][q] : 0u;
+        key[r] = s.key[j[r]];
       }
+      rank_chunk(s.r, key, valid, 8 * p, pos);
+#pragma unroll
+      for (int r = 0; r < kL2Per; r++)
+        if ((valid >> r) & 1u) s.perm[cur ^ 1u][pos[r]] = (uint16_t)j[r];
       __syncthreads();
     }
-    uint32_t* const fk = fin_key;
-    uint32_t* const fi = (a.passes2 & 1u) ? a.a_idx : a.b_idx;
+    // gather every command index first: the final pair may be b itself (an even pass
+    // count), so no write may land before every read
+    uint32_t jj[kL2Per], ci[kL2Per];
 #pragma unroll
     for (int r = 0; r < kL2Per; r++) {
-      const uint32_t q = chunk_pos<kL2Block, kL2Per>(r);
+      const uint32_t q = (uint32_t)r * kL2Block + threadIdx.x;
+      jj[r] = q < cnt ? s.perm[cur][q] : 0u;
+      ci[r] = q < cnt ? a.b_idx[lo + jj[r]] : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kL2Per; r++) {
+      const uint32_t q = (uint32_t)r * kL2Block + threadIdx.x;
       if (q < cnt) {
-        fk[lo + q] = key[r];
-        fi[lo + q] = idx[r];
+        fin_key[lo + q] = s.key[jj[r]];
+        fin_idx[lo + q] = ci[r];
       }
     }
     return;
@@ -1353,7 +1371,7 @@ __global__ __launch_bounds__(kL2Block) void kv_l2_sort_kernel(SortArgs a) {
     for (uint32_t i = lo + threadIdx.x; i < hi; i += kL2Block) atomicAdd(&s_hist[(sk[i] >> shift) & 255u], 1u);
     __syncthreads();
     uint32_t all;
-    const uint32_t ex = radix_excl_scan(s, threadIdx.x < kRadix ? s_hist[threadIdx.x] : 0u, &all);
+    const uint32_t ex = radix_excl_scan(s.r, threadIdx.x < kRadix ? s_hist[threadIdx.x] : 0u, &all);
     if (threadIdx.x < kRadix) s_run[threadIdx.x] = lo + ex;
     __syncthreads();
     for (uint32_t c = lo; c < hi; c += kL2Chunk) {
@@ -1364,23 +1382,23 @@ __global__ __launch_bounds__(kL2Block) void kv_l2_sort_kernel(SortArgs a) {
         valid |= (i < hi ? 1u : 0u) << r;
         key[r] = i < hi ? sk[i] : 0u;
       }
-      rank_chunk(s, key, valid, shift, pos);
+      rank_chunk(s.r, key, valid, shift, pos);
 #pragma unroll
-      for (int r = 0; r < kL2Per; r++) {
+      for (int r = 0; r < kL2Per; r++) {  // chunk-local sorted position -> chunk offset
         if (!((valid >> r) & 1u)) continue;
         s.key[pos[r]] = key[r];
-        s.idx[pos[r]] = si[c + chunk_pos<kL2Block, kL2Per>(r)];
+        s.perm[0][pos[r]] = (uint16_t)chunk_pos<kL2Block, kL2Per>(r);
       }
       __syncthreads();
-      const uint32_t nv = s.dstart[kRadix];
+      const uint32_t nv = s.r.dstart[kRadix];
       for (uint32_t q = threadIdx.x; q < nv; q += kL2Block) {
         const uint32_t k = s.key[q], d = (k >> shift) & 255u;
-        const uint32_t dst = s_run[d] + (q - s.dstart[d]);
+        const uint32_t dst = s_run[d] + (q - s.r.dstart[d]);
         dk[dst] = k;
-        di[dst] = s.idx[q];
+        di[dst] = si[c + s.perm[0][q]];
       }
       __syncthreads();
-      if (threadIdx.x < kRadix) s_run[threadIdx.x] += s.dstart[threadIdx.x + 1] - s.dstart[threadIdx.x];
+      if (threadIdx.x < kRadix) s_run[threadIdx.x] += s.r.dstart[threadIdx.x + 1] - s.r.dstart[threadIdx.x];
       __syncthreads();
     }
   }

@@ -21,10 +21,10 @@ lib = N.load()
 stream = torch.cuda.Stream()
 torch.cuda.set_stream(stream)
 sp = stream.cuda_stream
-n, T = 5, 1024
+n, T = int(os.environ.get("STAMP_N", 5)), 1024
 S = int(os.environ.get("STAMP_SLOTS", 1 << 28))
 nw = S // 32
-ev = PhaseEvaluator(n, self_lane=4, seed=42, tile_words=T)
+ev = PhaseEvaluator(n, self_lane=n - 1, seed=42, tile_words=T)
 sets = []
 for i in range(3):
     v = torch.empty(((nw + T - 1) // T) * (4 * n + 1) * T, dtype=torch.int32, device="cuda")
@@ -77,9 +77,22 @@ for r in range(int(rounds.max()) + 1):
     if meds:
         drift.append(max(meds) - min(meds))
 pct = lambda a: {p: float(np.percentile(a, p)) for p in (10, 50, 90, 99)}  # noqa: E731
+# back-to-back launches of a trivial kernel: the per-launch cost outside any tile
+tiny = torch.zeros(1, dtype=torch.int32, device="cuda")
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+for _ in range(5):
+    tiny.add_(1)
+e0.record(stream)
+for _ in range(50):
+    tiny.add_(1)
+e1.record(stream)
+torch.cuda.synchronize()
+out["trivial_launch_us"] = e0.elapsed_time(e1) * 1000.0 / 50
 out.update({
-    "slots": S, "tiles": tiles,
+    "slots": S, "n": n, "tiles": tiles,
     "kernel_span_us": float(t[:, 4].max()),
+    "last_tile_fold_us": float(t[:, 5].max() - t[:, 4].max()),
+    "tile_start_us": pct(t[:, 0]),
     "tally_us": pct(tally), "wait_us": pct(wait), "after_wait_us": pct(tail),
     "pred_aggregate_later_than_own_us": pct(pred_late),
     "wait_minus_pred_late_us": pct(wait - pred_late),
