@@ -54,26 +54,25 @@ def bytes_per_slot_ref(n: int) -> float:
 
 
 def c3_roofline(r, bytes_slot):
-    """C3 is VALU-issue bound (per phase 2n keyed scheduler hashes per slot + the coin),
+    """C3 is VALU-issue bound (per phase 2n keyed scheduler picks per slot + the coin),
     not HBM bound. achieved = VALU wave-instructions per launch (per-slot count from the
-    SQ_INSTS_VALU pass committed in profiles/r02_pmc_c3.json, tools/pmc_c3.sh) / the live
-    kernel time; peak = 256 CUs x 4 SIMDs x 1/4 wave64 instruction per cycle (a SIMD issues
-    one wave64 VALU instruction per 4 cycles, MI355X_MICROARCH.md 'vector-instruction ISSUE
-    cost'; the pure-VALU trace kernel reaches 98 % of it, profiles/r03_pmc_c2_sq_*) at the
-    2.4 GHz peak engine clock. The HBM fraction is kept beside it."""
+    SQ_INSTS_VALU pass of THIS round's kernel, profiles/r04_pmc_c3.json, tools/pmc_c3.sh)
+    / the live kernel time; peak = 256 CUs x 4 SIMDs x 1/2 wave64 instruction per cycle
+    (a SIMD-32 issues a wave64 VALU instruction over 2 cycles, MI355X_MICROARCH.md "Wave
+    scheduling") = 512 per cycle at the 2.4 GHz peak engine clock. The HBM fraction is
+    kept beside it."""
     kern_s = r["kern_ms"] / 1000.0
     hbm = r["S"] * bytes_slot / kern_s / 1e9
-    out = {"bound": "valu", "achieved": None, "peak": 256 * 2.4, "unit": "G VALU wave-instr/s", "frac": None,
+    out = {"bound": "valu", "achieved": None, "peak": 512 * 2.4, "unit": "G VALU wave-instr/s", "frac": None,
            "traffic": None, "kernel_avg_us": r["kern_ms"] * 1000.0, "hbm_gbs": hbm, "hbm_frac": hbm / HBM_PEAK_GBS}
-    path = os.path.join(ROOT, "profiles", "r02_pmc_c3.json")
+    path = os.path.join(ROOT, "profiles", "r04_pmc_c3.json")
     if os.path.exists(path):
         pmc = json.load(open(path))
         achieved = pmc["valu_wave_instr_per_slot"] * r["S"] / kern_s / 1e9
-        pd = pmc["per_dispatch"]
-        util = sum(x["SQ_INSTS_VALU"] / (256.0 * x["active_cycles"]) for x in pd) / len(pd)
-        out.update(achieved=achieved, frac=achieved / out["peak"], counter_issue_util=util,
-                   note="counter_issue_util = SQ_INSTS_VALU / (256 x GRBM_GUI_ACTIVE/8 cycles): the same "
-                        "ratio at the clock the chip actually ran (DVFS)")
+        out.update(achieved=achieved, frac=achieved / out["peak"], counter_issue_util=pmc["valu_issue_util"],
+                   counter_file="profiles/r04_pmc_c3.json",
+                   note="counter_issue_util = SQ_INSTS_VALU / (512 x GRBM_GUI_ACTIVE/8 cycles): the same ratio at "
+                        "the clock the chip actually ran (DVFS); mix_per_slot in the counter file")
     return out
 
 
@@ -100,8 +99,12 @@ def parse():
     ap.add_argument("--c5-windows", type=int, default=64, help="C5: 2^20-slot windows per C5 window, all ranks")
     ap.add_argument("--c5-batch", type=int, default=8,
                     help="C5 sharded pipeline: consecutive C5 windows per shard-step launch (a bench step)")
-    ap.add_argument("--c5-sharded", action="store_true",
-                    help="C5 on 1 GPU: run the sharded pipeline (shard step + fix-up + commit) with one shard")
+    ap.add_argument("--sharded", "--c5-sharded", dest="sharded", action="store_true",
+                    help="N = 1: run the multi-GPU pipeline (shard step + fix-up + commit, exchanges with one "
+                         "rank) instead of the single evaluator: the per-GPU cost of the N > 1 path")
+    ap.add_argument("--fixup-stream", choices=["fix", "comp"], default="comp",
+                    help="N > 1 / --sharded: the fix-up of step t on the second stream (overlapping step t + 1) "
+                         "or on the compute stream right behind step t + 1's launch")
     ap.add_argument("--diag", type=lambda x: int(x, 0), default=0,
                     help="rg_debug_set switches for experiments (include/rabia_gpu_debug.h); 0 = the product path")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
@@ -427,7 +430,12 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, bitmaps):
         bm_all = torch.zeros((n_total, world, K, 2, nw), dtype=torch.int32, device="cuda")
     torch.cuda.synchronize()
     e_main = [torch.cuda.Event() for _ in range(n_total)]
+    e_rows = [torch.cuda.Event() for _ in range(n_total)]
+    e_fixed = [torch.cuda.Event() for _ in range(n_total)]
     e_done = [torch.cuda.Event() for _ in range(n_total)]
+    # the fix-up of step t: on the second stream, overlapping step t + 1's launch, or on the
+    # compute stream right behind step t + 1's launch (no competition for the CUs)
+    fix_on_comp = a.fixup_stream == "comp"
 
     def shard_step(votes, out, rec, base, t):
         if K == 1:
@@ -438,7 +446,7 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, bitmaps):
                                               base + start, window_slots, rec.data_ptr(), cap, rows[t].data_ptr(),
                                               stream=comp.cuda_stream)
 
-    def step(t, evs=None):
+    def step(t, evs=None, chain=True):
         votes, out, rec = sets[t % a.sets]
         base = 1 + t * K * window_slots
         if t >= a.sets:  # the output buffers and records of step t - sets must be fixed up first
@@ -460,13 +468,28 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, bitmaps):
         if evs is not None:
             evs[1].record(comp)
         e_main[t].record(comp)
-        with torch.cuda.stream(fix):  # the K windows' later stages: one call / one all-gather each
+        with torch.cuda.stream(fix):  # the rows' all-gather
             fix.wait_event(e_main[t])
-            fs = fix.cuda_stream
             gather(g_rows[t], rows[t])
-            ev.shard_fixup_windows_async(K, out.data_ptr(), out_words, S, stride, base + start, window_slots,
-                                         rec.data_ptr(), cap, g_rows[t].data_ptr(), rank, world,
-                                         fixed[t].data_ptr(), stream=fs)
+            e_rows[t].record(fix)
+        if not fix_on_comp:
+            later(t, fix)
+        elif chain and t >= 1:  # the previous step's fix-up behind this step's launch, on the compute stream
+            later(t - 1, comp)
+
+    def later(t, fs_stream):
+        """Stages 3-4 of step t (+ C5 bitmaps): the fix-up on fs_stream, the final rows'
+        all-gather, the commit and the bitmaps on the second stream."""
+        votes, out, rec = sets[t % a.sets]
+        base = 1 + t * K * window_slots
+        fs_stream.wait_event(e_rows[t])
+        ev.shard_fixup_windows_async(K, out.data_ptr(), out_words, S, stride, base + start, window_slots,
+                                     rec.data_ptr(), cap, g_rows[t].data_ptr(), rank, world,
+                                     fixed[t].data_ptr(), stream=fs_stream.cuda_stream)
+        e_fixed[t].record(fs_stream)
+        with torch.cuda.stream(fix):
+            fix.wait_event(e_fixed[t])
+            fs = fix.cuda_stream
             gather(g_fixed[t], fixed[t])
             ev.shard_commit_windows_async(K, g_fixed[t].data_ptr(), world, base, window_slots, result[t].data_ptr(),
                                           stream=fs)
@@ -482,14 +505,18 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, bitmaps):
 
     for t in range(a.warmup):
         step(t)
+    if fix_on_comp and a.warmup:
+        later(a.warmup - 1, comp)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
     t_begin, t_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t_begin.record(comp)
-    for k in range(a.steps):
-        step(a.warmup + k, evs[k])
+    for k in range(a.steps):  # (the warm-up's last fix-up is done: the timed chain starts afresh)
+        step(a.warmup + k, evs[k], chain=k > 0)
+    if fix_on_comp:
+        later(n_total - 1, comp)
     comp.wait_event(e_done[n_total - 1])
     t_end.record(comp)
     torch.cuda.synchronize()
@@ -683,7 +710,7 @@ def main():
     else:
         n, S = a.replicas, a.windows * WINDOW
         window_slots = S * world
-    if world == 1 and not (a.config == "c5" and a.c5_sharded):
+    if world == 1 and not a.sharded:
         r = run_single(a, n, S, a.config)
     else:
         r = run_sharded(a, n, S, window_slots, world, rank, dist, bitmaps=a.config == "c5")

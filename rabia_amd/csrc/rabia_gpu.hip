@@ -55,6 +55,8 @@ struct rg_ctx {
   unsigned long long* cluster_stats = nullptr;  // [kClusterStats]
   unsigned long long* fix_acc = nullptr;        // sharded REF fix-up accumulators [4][windows]
   uint64_t fix_acc_cap = 4;
+  uint32_t* fix_seg = nullptr;                  // sharded REF fix-up: first record per segment [windows][segments]
+  uint64_t fix_seg_cap = 0;
   unsigned long long* follow_acc = nullptr;     // follower commit accumulator [4]
   // results of the shard fix-up / shard commit / follower commit: each stage writes
   // its own (a fix-up may run on another stream than the next window's step, whose
@@ -364,6 +366,7 @@ int rg_destroy(rg_ctx* ctx) {
   (void)hipFree(ctx->cluster_stats);
   (void)hipFree(ctx->fix_acc);
   (void)hipFree(ctx->follow_acc);
+  (void)hipFree(ctx->fix_seg);
   (void)hipFree(ctx->stage_result);
   (void)hipFree(ctx->d_votes);
   (void)hipFree(ctx->d_out);
@@ -631,12 +634,23 @@ static int fixup_impl(rg_ctx* ctx, uint32_t n_win, uint32_t* out_dev, uint64_t o
   f.n_win = n_win;
   f.out_pitch = out_pitch;
   f.id_stride = id_stride;
-  // one ChaCha12 block per thread per pass; the record count lives on the device,
-  // so the grid covers the largest possible count (all slots VQ) and strides
-  const uint64_t blocks_max = (records_cap < n_slots ? records_cap : n_slots) / 8 + 2;
-  const uint64_t g = (blocks_max + 255) / 256;
-  const uint32_t grid = (uint32_t)(g < 1024 ? g : 1024);
-  hipLaunchKernelGGL(shard_fixup_kernel, dim3(grid, n_win), dim3(256), 0, s, f);
+  // per 65,536-slot segment: the index of its first record (pass A, a grid-stride loop
+  // over the records: their count lives on the device), then one wave per segment
+  const uint32_t n_seg = (uint32_t)((n_words + kFixSegWords - 1) / kFixSegWords);
+  if ((uint64_t)n_seg * n_win > ctx->fix_seg_cap) {
+    RG_HIP(ctx, hipDeviceSynchronize());
+    (void)hipFree(ctx->fix_seg);
+    ctx->fix_seg = nullptr;
+    ctx->fix_seg_cap = 0;
+    RG_HIP(ctx, hipMalloc(&ctx->fix_seg, (uint64_t)n_seg * n_win * 4));
+    ctx->fix_seg_cap = (uint64_t)n_seg * n_win;
+  }
+  RG_HIP(ctx, hipMemsetAsync(ctx->fix_seg, 0, (uint64_t)n_seg * n_win * 4, s));
+  const uint64_t rec_max = records_cap < n_slots ? records_cap : n_slots;
+  const uint64_t ga = (rec_max + 255) / 256;
+  hipLaunchKernelGGL(shard_fixup_seg_kernel, dim3((uint32_t)(ga < 1024 ? ga : 1024), n_win), dim3(256), 0, s, f,
+                     ctx->fix_seg, n_seg);
+  hipLaunchKernelGGL(shard_fixup_kernel, dim3((n_seg + 3) / 4, n_win), dim3(256), 0, s, f, ctx->fix_seg, n_seg);
   hipLaunchKernelGGL(shard_fixup_finish_kernel, dim3(1), dim3(64), 0, s, f, ctx->stage_result + 0,
                      reinterpret_cast<DevResult*>(rows_out_dev));
   RG_HIP(ctx, hipGetLastError());

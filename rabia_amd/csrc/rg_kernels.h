@@ -1804,74 +1804,124 @@ __device__ __forceinline__ unsigned long long fix_first_draw(const FixParams& f,
   return pre;
 }
 
-__device__ __forceinline__ void fix_flush(const FixParams& f, uint64_t w, const uint32_t (&x)[5]) {
-  constexpr int kPl[5] = {2, 4, 5, 6, 7};
-  const uint64_t base = f.lout.base(w);
-#pragma unroll
-  for (int i = 0; i < 5; i++)
-    if (x[i]) atomicXor(f.out + base + (uint64_t)kPl[i] * f.lout.pstride, x[i]);
-}
+// The fix-up runs per 65,536-slot segment of the window (2,048 words of every plane;
+// a lag or tiled tile never spans two segments): pass A finds each segment's first
+// record (records are in ascending slot order), pass B gives one wave per segment.
+// The wave re-draws its records' VQ slots at their global positions (64 ChaCha12
+// blocks per pass, one per lane, into LDS), counts them into the shard's statistics,
+// collects the own-vote bits that change in an LDS mask of the segment, and rewrites
+// the segment's own-vote plane in one coalesced read-XOR-write stream (an own-vote bit
+// changes for ~25 % of the VQ slots when the position moved, so nearly every line of
+// the plane is touched: per-bit atomics cost a random line read-modify-write each).
+// The rare decision changes (the own vote decides the round-2 count) are atomic XORs.
+constexpr uint32_t kFixSegShift = 16;                      // 65,536 slots per segment
+constexpr uint32_t kFixSegWords = 1u << (kFixSegShift - 5);  // 2,048 words
 
-static __global__ __launch_bounds__(256) void shard_fixup_kernel(FixParams f) {
+static __global__ __launch_bounds__(256) void shard_fixup_seg_kernel(FixParams f, uint32_t* seg_first,
+                                                                    uint32_t n_seg) {
   const uint32_t win = blockIdx.y;
   const unsigned long long n = f.rows[(uint64_t)f.shard * f.n_win + win].n_draws;
+  const unsigned long long nn = n < f.vq_cap ? n : f.vq_cap;
+  const unsigned long long* rec = f.rec + win * f.vq_cap;
+  uint32_t* sf = seg_first + (uint64_t)win * n_seg;
+  for (unsigned long long k = (unsigned long long)blockIdx.x * 256 + threadIdx.x; k < nn;
+       k += (unsigned long long)gridDim.x * 256) {
+    const uint32_t seg = (uint32_t)rec[k] >> kFixSegShift;
+    const uint32_t prev = k ? (uint32_t)rec[k - 1] >> kFixSegShift : ~0u;
+    if (seg != prev && seg < n_seg) sf[seg] = (uint32_t)k + 1u;  // 0: no record in the segment
+  }
+}
+
+static __global__ __launch_bounds__(256) void shard_fixup_kernel(FixParams f, const uint32_t* seg_first,
+                                                                uint32_t n_seg) {
+  __shared__ uint32_t s_blk[4][64][17];         // per wave: 64 ChaCha12 blocks (+1 word: no conflicts)
+  __shared__ uint32_t s_m2[4][kFixSegWords];    // per wave: own-vote bits that change in its segment
+  const uint32_t win = blockIdx.y;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const unsigned long long n = f.rows[(uint64_t)f.shard * f.n_win + win].n_draws;
   const unsigned long long g0 = fix_first_draw(f, win);  // global position of local draw 0
-  if (win) {  // this window's outputs, slot ids, records and accumulators
+  if (win) {  // this window's outputs, slot ids, records
     f.out += win * f.out_pitch;
     f.slot_base += win * f.id_stride;
     f.rec += win * f.vq_cap;
   }
   const unsigned long long nn = n < f.vq_cap ? n : f.vq_cap;
-  const unsigned long long b_first = g0 >> 3, b_end = nn ? ((g0 + nn - 1) >> 3) + 1 : b_first;
   unsigned long long dec = 0, v1 = 0, mx = 0, mn = ~0ull;
-  for (unsigned long long b = b_first + (unsigned long long)blockIdx.x * 256 + threadIdx.x; b < b_end;
-       b += (unsigned long long)gridDim.x * 256) {
-    uint32_t x[16];
-    chacha_block<12>(f.key, b, 0, x);
-    const unsigned long long lo = (b << 3) > g0 ? (b << 3) - g0 : 0;
-    const unsigned long long hi = ((b + 1) << 3) - g0 < nn ? ((b + 1) << 3) - g0 : nn;
-    uint64_t cur = ~0ull;
-    uint32_t xm[5] = {0, 0, 0, 0, 0};
-    for (unsigned long long k = lo; k < hi; k++) {
-      const unsigned long long r = f.rec[k];
-      const uint32_t off = (uint32_t)r, info = (uint32_t)(r >> 32);
-      const uint32_t ws = (uint32_t)((g0 + k) & 7u) * 2u;
-      const unsigned long long u =
-          (unsigned long long)select16(x, ws) | ((unsigned long long)select16(x, ws + 1) << 32);
-      const uint32_t cls = info & 3u;
-      const uint32_t own = cls == kRecGt ? (u < kP90) : (cls == kRecLt ? (u >= kP90) : (u < kP80));
-      const uint32_t prov = (info >> 6) & 1u;
-      const uint32_t d = own ? (info >> 4) & 3u : (info >> 2) & 3u;
-      const uint32_t dp = prov ? (info >> 4) & 3u : (info >> 2) & 3u;
-      const unsigned long long id = f.slot_base + off;
-      if (d <= kCodeV1) {
-        dec++;
-        if (d == kCodeV1) {
-          v1++;
-          if ((f.max_phase == 0 || id <= f.max_phase) && id + 1 > mx) mx = id + 1;
-        }
-      } else if (id < mn) {
-        mn = id;
+  const uint32_t seg = blockIdx.x * 4 + wave;
+  const uint32_t k1 = seg < n_seg ? seg_first[(uint64_t)win * n_seg + seg] : 0u;
+  if (k1) {  // wave-uniform
+    for (uint32_t i = lane; i < kFixSegWords; i += 64) s_m2[wave][i] = 0u;
+    bool changed = false;
+    const uint64_t seg_w0 = (uint64_t)seg * kFixSegWords;
+    for (unsigned long long kb = k1 - 1;; kb += 512) {  // 512 records (64 blocks of 8 draws) per pass
+      const unsigned long long b0 = (g0 + kb) >> 3;
+      {
+        uint32_t x[16];
+        chacha_block<12>(f.key, b0 + (unsigned long long)lane, 0, x);
+#pragma unroll
+        for (int j = 0; j < 16; j++) s_blk[wave][lane][j] = x[j];
       }
-      if (own != prov) {
-        const uint64_t w = off >> 5;
-        if (w != cur) {
-          if (cur != ~0ull) fix_flush(f, cur, xm);
-          cur = w;
-          xm[0] = xm[1] = xm[2] = xm[3] = xm[4] = 0;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      bool more = true;
+      for (int sub = 0; sub < 8 && more; sub++) {
+        const unsigned long long k = kb + (unsigned long long)sub * 64 + lane;
+        const unsigned long long r = k < nn ? f.rec[k] : ~0ull;
+        const uint32_t off = (uint32_t)r, info = (uint32_t)(r >> 32);
+        const bool mine = k < nn && (off >> kFixSegShift) == seg;
+        more = __ballot(mine) == ~0ull;  // every lane still in this segment: the next 64 may be too
+        if (mine) {
+          const unsigned long long g = g0 + k;
+          const uint32_t row = (uint32_t)((g >> 3) - b0), ws = (uint32_t)(g & 7u) * 2u;
+          const unsigned long long u =
+              (unsigned long long)s_blk[wave][row][ws] | ((unsigned long long)s_blk[wave][row][ws + 1] << 32);
+          const uint32_t cls = info & 3u;
+          const uint32_t own = cls == kRecGt ? (u < kP90) : (cls == kRecLt ? (u >= kP90) : (u < kP80));
+          const uint32_t prov = (info >> 6) & 1u;
+          const uint32_t d = own ? (info >> 4) & 3u : (info >> 2) & 3u;
+          const uint32_t dp = prov ? (info >> 4) & 3u : (info >> 2) & 3u;
+          const unsigned long long id = f.slot_base + off;
+          if (d <= kCodeV1) {
+            dec++;
+            if (d == kCodeV1) {
+              v1++;
+              if ((f.max_phase == 0 || id <= f.max_phase) && id + 1 > mx) mx = id + 1;
+            }
+          } else if (id < mn) {
+            mn = id;
+          }
+          if (own != prov) {
+            const uint32_t wl = (off >> 5) & (kFixSegWords - 1u), bit = 1u << (off & 31u);
+            atomicXor(&s_m2[wave][wl], bit);
+            changed = true;
+            const uint32_t dd = d ^ dp;
+            if (dd || (d <= kCodeV1) != (dp <= kCodeV1)) {  // the decision changed: rare
+              const uint64_t base = f.lout.base(off >> 5);
+              if (dd & 1u) atomicXor(f.out + base + 4 * f.lout.pstride, bit);
+              if (dd & 2u) atomicXor(f.out + base + 5 * f.lout.pstride, bit);
+              if ((d <= kCodeV1) != (dp <= kCodeV1)) atomicXor(f.out + base + 6 * f.lout.pstride, bit);
+              if ((d == kCodeV1) != (dp == kCodeV1)) atomicXor(f.out + base + 7 * f.lout.pstride, bit);
+            }
+          }
         }
-        const uint32_t bit = 1u << (off & 31u), dd = d ^ dp;
-        xm[0] ^= bit;
-        xm[1] ^= (dd & 1u) ? bit : 0u;
-        xm[2] ^= (dd & 2u) ? bit : 0u;
-        xm[3] ^= ((d <= kCodeV1) != (dp <= kCodeV1)) ? bit : 0u;
-        xm[4] ^= ((d == kCodeV1) != (dp == kCodeV1)) ? bit : 0u;
+      }
+      if (!more) break;
+    }
+    if (__ballot(changed)) {  // the segment's own-vote plane: one coalesced read-XOR-write pass
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      uint32_t* p2 = f.out + 2 * f.lout.pstride;
+#pragma unroll 4
+      for (uint32_t i = lane; i < kFixSegWords; i += 64) {
+        const uint32_t m = s_m2[wave][i];
+        if (m) {
+          const uint64_t a = f.lout.base(seg_w0 + i);
+          p2[a] ^= m;
+        }
       }
     }
-    if (cur != ~0ull) fix_flush(f, cur, xm);
   }
   __shared__ unsigned long long red[4][4];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   dec = wave_sum64(dec);
   v1 = wave_sum64(v1);
   mx = wave_max64(mx);

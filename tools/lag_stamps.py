@@ -19,12 +19,12 @@ PHASES = ["start_to_loop", "tally", "scan_barrier", "decisions", "draws", "store
 def main():
     extra = int(sys.argv[1], 0) if len(sys.argv) > 1 else 0
     S = int(os.environ.get("STAMP_SLOTS", 1 << 30))
-    n, T = 5, 1024
+    n, T = int(os.environ.get("STAMP_N", 5)), 1024
     nw = S // 32
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
-    ev = PhaseEvaluator(n, self_lane=4, seed=42, tile_words=T)
+    ev = PhaseEvaluator(n, self_lane=n - 1, seed=42, tile_words=T)
     v = torch.empty(((nw + T - 1) // T) * (4 * n + 1) * T, dtype=torch.int32, device="cuda")
     o = torch.empty(((nw + T - 1) // T) * 8 * T, dtype=torch.int32, device="cuda")
     ev.trace_generate_async(N.RG_TRACE_AGREE90, 1, 1, S, T, v.data_ptr(), sp)
