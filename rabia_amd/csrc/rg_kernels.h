@@ -1423,6 +1423,17 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
         for (int i = 0; i < W; i++) {
           if (!mq[i] || k >= k_lim) continue;
           const uint32_t e0 = pp[2][tid][i], e1 = pp[3][tid][i];
+          // SHARD: the draw record of each VQ slot, written as it is drawn (index = local
+          // draw number, ascending slot order): offset, class, the decision under each
+          // own vote, the provisional own vote (built in a loop of its own: 765 vs 697 us
+          // per 2^30 slots against no records at all)
+          uint32_t dv[4] = {0u, 0u, 0u, 0u};
+#ifndef RG_SHARD_NOREC  // experiment build: the SHARD kernel without its records (wrong fix-up)
+          if constexpr (SHARD) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) dv[j] = pp[4 + j][tid][i];
+          }
+#endif
           while (mq[i] && k < k_lim) {
             const int b = __builtin_ctz(mq[i]);
             mq[i] &= mq[i] - 1;
@@ -1432,6 +1443,17 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
             const bool x0 = (e0 >> b) & 1u, x1 = (e1 >> b) & 1u;  // gt: 1/0, lt: 0/1, tie: 1/1
             const bool v1 = (x0 && !x1) ? (u < kP90) : ((x1 && !x0) ? (u >= kP90) : (u < kP80));
             own[i] |= (uint32_t)v1 << b;
+#ifndef RG_SHARD_NOREC
+            if constexpr (SHARD) {
+              const uint32_t cls = (x0 && !x1) ? kRecGt : ((x1 && !x0) ? kRecLt : 0u);
+              const uint32_t d4 = ((dv[0] >> b) & 1u) | (((dv[1] >> b) & 1u) << 1) | (((dv[2] >> b) & 1u) << 2) |
+                                  (((dv[3] >> b) & 1u) << 3);
+              const uint32_t info = cls | (d4 << 2) | ((uint32_t)v1 << 6);
+              const unsigned long long kr = k - k_base;
+              const uint32_t off = 32u * ((uint32_t)park_tile * kTW + (uint32_t)tid * W + i) + b;
+              if (kr < p.vq_cap) p.vq_rec[kr] = ((unsigned long long)info << 32) | off;
+            }
+#endif
             k++;
           }
         }
@@ -1440,32 +1462,6 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
         // orders these reads before the next writes of s_blk (686.5 -> 670.9 us per
         // 2^30 slots, interleaved A/B)
         if (cb + kRows <= b_last) lds_barrier();
-      }
-    }
-    if constexpr (SHARD) {  // draw records, indexed by local draw number (ascending slot order)
-      const uint32_t pw0 = (uint32_t)park_tile * kTW + (uint32_t)tid * W;
-      uint32_t e0[W], e1[W], alo[W], ahi[W], blo[W], bhi[W];
-      lds_ld<W>(pp[2][tid], e0);
-      lds_ld<W>(pp[3][tid], e1);
-      lds_ld<W>(pp[4][tid], alo);
-      lds_ld<W>(pp[5][tid], ahi);
-      lds_ld<W>(pp[6][tid], blo);
-      lds_ld<W>(pp[7][tid], bhi);
-      unsigned long long kr = excl + park_thr;
-#pragma unroll
-      for (int i = 0; i < W; i++) {
-        uint32_t m = e0[i] | e1[i];
-        while (m) {
-          const int b = __builtin_ctz(m);
-          m &= m - 1;
-          const uint32_t x0 = (e0[i] >> b) & 1u, x1 = (e1[i] >> b) & 1u;
-          const uint32_t cls = (x0 && !x1) ? kRecGt : ((x1 && !x0) ? kRecLt : 0u);
-          const uint32_t d_v0 = ((alo[i] >> b) & 1u) | (((ahi[i] >> b) & 1u) << 1);
-          const uint32_t d_v1 = ((blo[i] >> b) & 1u) | (((bhi[i] >> b) & 1u) << 1);
-          const uint32_t info = cls | (d_v0 << 2) | (d_v1 << 4) | (((own[i] >> b) & 1u) << 6);
-          if (kr < p.vq_cap) p.vq_rec[kr] = ((unsigned long long)info << 32) | (32u * (pw0 + i) + b);
-          kr++;
-        }
       }
     }
   };
@@ -1853,8 +1849,17 @@ static __global__ __launch_bounds__(256) void shard_fixup_kernel(FixParams f, co
     for (uint32_t i = lane; i < kFixSegWords; i += 64) s_m2[wave][i] = 0u;
     bool changed = false;
     const uint64_t seg_w0 = (uint64_t)seg * kFixSegWords;
-    for (unsigned long long kb = k1 - 1;; kb += 512) {  // 512 records (64 blocks of 8 draws) per pass
+    // passes of 64 ChaCha12 blocks (one per lane): the records whose draws they hold
+    // (<= 512, fewer when the first position is not a multiple of 8)
+    for (unsigned long long kb = k1 - 1;;) {
       const unsigned long long b0 = (g0 + kb) >> 3;
+      const unsigned long long kend = ((b0 + 64) << 3) - g0;  // the first record past this pass's blocks
+      unsigned long long rr[8];  // the pass's records, all loads in flight behind the ChaCha blocks
+#pragma unroll
+      for (int sub = 0; sub < 8; sub++) {
+        const unsigned long long k = kb + 64u * sub + lane;
+        rr[sub] = k < kend && k < nn ? f.rec[k] : ~0ull;
+      }
       {
         uint32_t x[16];
         chacha_block<12>(f.key, b0 + (unsigned long long)lane, 0, x);
@@ -1863,13 +1868,16 @@ static __global__ __launch_bounds__(256) void shard_fixup_kernel(FixParams f, co
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_wave_barrier();
-      bool more = true;
-      for (int sub = 0; sub < 8 && more; sub++) {
-        const unsigned long long k = kb + (unsigned long long)sub * 64 + lane;
-        const unsigned long long r = k < nn ? f.rec[k] : ~0ull;
+      bool seg_done = false;
+#pragma unroll
+      for (int sub = 0; sub < 8; sub++) {
+        if (seg_done) break;
+        const unsigned long long k = kb + 64u * sub + lane;
+        const bool inpass = k < kend;
+        const unsigned long long r = rr[sub];
         const uint32_t off = (uint32_t)r, info = (uint32_t)(r >> 32);
-        const bool mine = k < nn && (off >> kFixSegShift) == seg;
-        more = __ballot(mine) == ~0ull;  // every lane still in this segment: the next 64 may be too
+        const bool mine = inpass && k < nn && (off >> kFixSegShift) == seg;
+        seg_done = __ballot(inpass && !mine) != 0;  // records are in slot order: the segment ended
         if (mine) {
           const unsigned long long g = g0 + k;
           const uint32_t row = (uint32_t)((g >> 3) - b0), ws = (uint32_t)(g & 7u) * 2u;
@@ -1905,19 +1913,26 @@ static __global__ __launch_bounds__(256) void shard_fixup_kernel(FixParams f, co
           }
         }
       }
-      if (!more) break;
+      if (seg_done) break;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every lane's block reads done before the next pass writes
+      __builtin_amdgcn_wave_barrier();
+      kb = kend;
     }
     if (__ballot(changed)) {  // the segment's own-vote plane: one coalesced read-XOR-write pass
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_wave_barrier();
       uint32_t* p2 = f.out + 2 * f.lout.pstride;
-#pragma unroll 4
-      for (uint32_t i = lane; i < kFixSegWords; i += 64) {
-        const uint32_t m = s_m2[wave][i];
-        if (m) {
-          const uint64_t a = f.lout.base(seg_w0 + i);
-          p2[a] ^= m;
+#pragma unroll
+      for (uint32_t h = 0; h < kFixSegWords; h += 16 * 64) {  // 16 words per lane in flight at once
+        uint32_t m[16], v[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+          m[j] = s_m2[wave][h + 64u * j + lane];
+          v[j] = m[j] ? p2[f.lout.base(seg_w0 + h + 64u * j + lane)] : 0u;
         }
+#pragma unroll
+        for (int j = 0; j < 16; j++)
+          if (m[j]) p2[f.lout.base(seg_w0 + h + 64u * j + lane)] = v[j] ^ m[j];
       }
     }
   }

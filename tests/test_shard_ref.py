@@ -100,6 +100,12 @@ def run_sharded(n, world, window_sizes, votes, out, stride, seed=42, self_lane=N
             for r in range(world):
                 ctxs[r].shard_commit_async(fg.data_ptr(), world, base, S, result[w, r].data_ptr())
             torch.cuda.synchronize()
+        # rg_last_stage_result: each context keeps its latest fix-up row and commit result
+        last = len(window_sizes) - 1
+        for r, ev in enumerate(ctxs):
+            if plan[last][3][r][1]:
+                assert shard.result_row(ev.last_stage_result(0)) == fixed[last, r].cpu().numpy().view(np.uint64).tolist()
+            assert shard.result_row(ev.last_stage_result(1)) == result[last, r].cpu().numpy().view(np.uint64).tolist()
         states = [ev.get_state() for ev in ctxs]
         if keep is not None:
             keep.extend(r.cpu().numpy().view(np.uint64) for r in recs)
