@@ -57,7 +57,7 @@ struct rg_ctx {
   uint64_t fix_acc_cap = 4;
   uint32_t* fix_seg = nullptr;                  // sharded REF fix-up: first record per segment [windows][segments]
   uint64_t fix_seg_cap = 0;
-  unsigned long long* follow_acc = nullptr;     // follower commit accumulator [4]
+  unsigned long long* follow_acc = nullptr;     // follower commit partials [kFollowGrid][4]
   // results of the shard fix-up / shard commit / follower commit: each stage writes
   // its own (a fix-up may run on another stream than the next window's step, whose
   // result is ctx->result, the one rg_last_result reads)
@@ -322,7 +322,7 @@ int rg_create(rg_ctx** out, const rg_config* cfg) {
   if ((e = hipMalloc(&ctx->result, sizeof(DevResult))) != hipSuccess) return bail(e, "hipMalloc(result)");
   if ((e = hipMalloc(&ctx->stage_result, 3 * sizeof(DevResult))) != hipSuccess) return bail(e, "hipMalloc(stage_result)");
   if ((e = hipMalloc(&ctx->fix_acc, 4 * sizeof(unsigned long long))) != hipSuccess) return bail(e, "hipMalloc(fix_acc)");
-  if ((e = hipMalloc(&ctx->follow_acc, 4 * sizeof(unsigned long long))) != hipSuccess)
+  if ((e = hipMalloc(&ctx->follow_acc, 4ull * kFollowGrid * sizeof(unsigned long long))) != hipSuccess)
     return bail(e, "hipMalloc(follow_acc)");
   Record recs[2] = {fresh_record(), fresh_record()};
   DevState st{0, 0, 1, 0, 0};  // PhaseIds start at 1 (state.rs:59-63)
@@ -607,17 +607,20 @@ static int fixup_impl(rg_ctx* ctx, uint32_t n_win, uint32_t* out_dev, uint64_t o
   if (int rc = make_layout(ctx, kOutPlanes, n_words, stride_words, &lout, &need, "rg_shard_fixup")) return rc;
   if (n_win > 1 && out_pitch < (ctx->cfg.tile_words ? need : n_words))
     return fail(ctx, RG_EINVAL, "rg_shard_fixup_windows: out pitch is smaller than one window's output planes");
-  if (4ull * n_win > ctx->fix_acc_cap) {
+  // per 32,768-slot segment: the index of its first record (pass A, a grid-stride loop
+  // over the records: their count lives on the device), then one wave per segment,
+  // four per workgroup, each workgroup's statistics a partial folded by the finish
+  const uint32_t n_seg = (uint32_t)((n_words + kFixSegWords - 1) / kFixSegWords);
+  const uint32_t n_part = (n_seg + 3) / 4;
+  if (4ull * n_part * n_win > ctx->fix_acc_cap) {
     RG_HIP(ctx, hipDeviceSynchronize());
     (void)hipFree(ctx->fix_acc);
     ctx->fix_acc = nullptr;
-    RG_HIP(ctx, hipMalloc(&ctx->fix_acc, 4ull * n_win * sizeof(unsigned long long)));
-    ctx->fix_acc_cap = 4ull * n_win;
+    ctx->fix_acc_cap = 0;
+    RG_HIP(ctx, hipMalloc(&ctx->fix_acc, 4ull * n_part * n_win * sizeof(unsigned long long)));
+    ctx->fix_acc_cap = 4ull * n_part * n_win;
   }
   hipStream_t s = pick_stream(ctx, stream);
-  // acc [4][n_win]: decided, V1, max V1 id + 1 (0) and min undecided id (all ones)
-  RG_HIP(ctx, hipMemsetAsync(ctx->fix_acc, 0, 3ull * n_win * sizeof(unsigned long long), s));
-  RG_HIP(ctx, hipMemsetAsync(ctx->fix_acc + 3ull * n_win, 0xFF, n_win * sizeof(unsigned long long), s));
   FixParams f;
   f.rec = reinterpret_cast<const unsigned long long*>(records_dev);
   f.rows = reinterpret_cast<const DevResult*>(rows_dev);
@@ -631,12 +634,10 @@ static int fixup_impl(rg_ctx* ctx, uint32_t n_win, uint32_t* out_dev, uint64_t o
   f.vq_cap = records_cap;
   f.key = ctx->ref_key;
   f.acc = ctx->fix_acc;
+  f.n_part = n_part;
   f.n_win = n_win;
   f.out_pitch = out_pitch;
   f.id_stride = id_stride;
-  // per 65,536-slot segment: the index of its first record (pass A, a grid-stride loop
-  // over the records: their count lives on the device), then one wave per segment
-  const uint32_t n_seg = (uint32_t)((n_words + kFixSegWords - 1) / kFixSegWords);
   if ((uint64_t)n_seg * n_win > ctx->fix_seg_cap) {
     RG_HIP(ctx, hipDeviceSynchronize());
     (void)hipFree(ctx->fix_seg);
@@ -647,11 +648,11 @@ static int fixup_impl(rg_ctx* ctx, uint32_t n_win, uint32_t* out_dev, uint64_t o
   }
   RG_HIP(ctx, hipMemsetAsync(ctx->fix_seg, 0, (uint64_t)n_seg * n_win * 4, s));
   const uint64_t rec_max = records_cap < n_slots ? records_cap : n_slots;
-  const uint64_t ga = (rec_max + 255) / 256;
-  hipLaunchKernelGGL(shard_fixup_seg_kernel, dim3((uint32_t)(ga < 1024 ? ga : 1024), n_win), dim3(256), 0, s, f,
+  const uint64_t ga = (rec_max + 1023) / 1024;  // 4 records per thread; blocks past the count exit at once
+  hipLaunchKernelGGL(shard_fixup_seg_kernel, dim3((uint32_t)(ga < 8192 ? ga : 8192), n_win), dim3(256), 0, s, f,
                      ctx->fix_seg, n_seg);
-  hipLaunchKernelGGL(shard_fixup_kernel, dim3((n_seg + 3) / 4, n_win), dim3(256), 0, s, f, ctx->fix_seg, n_seg);
-  hipLaunchKernelGGL(shard_fixup_finish_kernel, dim3(1), dim3(64), 0, s, f, ctx->stage_result + 0,
+  hipLaunchKernelGGL(shard_fixup_kernel, dim3(n_part, n_win), dim3(256), 0, s, f, ctx->fix_seg, n_seg);
+  hipLaunchKernelGGL(shard_fixup_finish_kernel, dim3(1), dim3(256), 0, s, f, ctx->stage_result + 0,
                      reinterpret_cast<DevResult*>(rows_out_dev));
   RG_HIP(ctx, hipGetLastError());
   return RG_OK;
@@ -686,8 +687,6 @@ int rg_follower_commit_async(rg_ctx* ctx, const uint32_t* out_dev, uint64_t n_sl
   uint64_t need;
   if (int rc = make_layout(ctx, kOutPlanes, n_words, stride_words, &lout, &need, "rg_follower_commit")) return rc;
   hipStream_t s = pick_stream(ctx, stream);
-  RG_HIP(ctx, hipMemsetAsync(ctx->follow_acc, 0, 3 * sizeof(unsigned long long), s));
-  RG_HIP(ctx, hipMemsetAsync(ctx->follow_acc + 3, 0xFF, sizeof(unsigned long long), s));
   FollowParams f;
   f.out = out_dev;
   f.lout = lout;
@@ -699,8 +698,9 @@ int rg_follower_commit_async(rg_ctx* ctx, const uint32_t* out_dev, uint64_t n_sl
   f.applied = applied_dev;
   f.acc = ctx->follow_acc;
   const uint64_t g = (n_words + 255) / 256;
-  hipLaunchKernelGGL(follower_kernel, dim3((uint32_t)(g < 2048 ? g : 2048)), dim3(256), 0, s, f);
-  hipLaunchKernelGGL(follower_finish_kernel, dim3(1), dim3(64), 0, s, f,
+  f.n_part = (uint32_t)(g < kFollowGrid ? g : kFollowGrid);
+  hipLaunchKernelGGL(follower_kernel, dim3(f.n_part), dim3(256), 0, s, f);
+  hipLaunchKernelGGL(follower_finish_kernel, dim3(1), dim3(256), 0, s, f,
                      reinterpret_cast<unsigned long long*>(gate_dev), ctx->stage_result + 2,
                      reinterpret_cast<DevResult*>(result_dev));
   RG_HIP(ctx, hipGetLastError());

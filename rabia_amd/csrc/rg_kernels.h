@@ -1770,6 +1770,38 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
 // slots into the shard's statistics. One thread per ChaCha12 block (8 draws),
 // grid-stride; one atomic per changed (plane, word) run of a thread.
 // ============================================================================
+// Statistics partials: (sum, sum, max, min) quadruples, one per workgroup.
+// fold4: element j of the 4 waves' values in red[wave][j];
+// fold_partials: n quadruples at acc folded by one 256-thread block (result in thread 0's a).
+__device__ __forceinline__ unsigned long long fold4(const unsigned long long (&red)[4][4], int j) {
+  unsigned long long x = red[0][j];
+  for (int w = 1; w < 4; w++) {
+    const unsigned long long y = red[w][j];
+    x = j < 2 ? x + y : (j == 2 ? (y > x ? y : x) : (y < x ? y : x));
+  }
+  return x;
+}
+__device__ __forceinline__ void fold_partials(const unsigned long long* acc, uint32_t n, unsigned long long (&red)[4][4],
+                                              unsigned long long (&a)[4]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  a[0] = 0; a[1] = 0; a[2] = 0; a[3] = ~0ull;
+  for (uint32_t b = threadIdx.x; b < n; b += 256) {
+    const unsigned long long* x = acc + (uint64_t)b * 4;
+    a[0] += x[0];
+    a[1] += x[1];
+    a[2] = x[2] > a[2] ? x[2] : a[2];
+    a[3] = x[3] < a[3] ? x[3] : a[3];
+  }
+  a[0] = wave_sum64(a[0]);
+  a[1] = wave_sum64(a[1]);
+  a[2] = wave_max64(a[2]);
+  a[3] = wave_min64(a[3]);
+  if (lane == 0) for (int j = 0; j < 4; j++) red[wave][j] = a[j];
+  __syncthreads();
+  for (int j = 0; j < 4; j++) a[j] = fold4(red, j);
+  __syncthreads();  // red may be rewritten by the caller's next fold
+}
+
 struct FixParams {
   const unsigned long long* rec;  // [vq_cap] draw records of this shard's step
   const DevResult* rows;          // [n_shards] step rows of every shard, rank order
@@ -1779,7 +1811,11 @@ struct FixParams {
   Layout lout;
   uint64_t slot_base, max_phase, vq_cap;
   Key key;
-  unsigned long long* acc;        // [4][n_win] decided, V1, max V1 id + 1, min undecided id
+  // per-workgroup partials [n_win][n_part][4]: decided, V1, max V1 id + 1, min undecided
+  // id (folded by the finish kernel: one same-address atomic per workgroup serialises
+  // at one memory channel, 4 x 4096 of them cost ~200 us per 2^30-slot fix-up)
+  unsigned long long* acc;
+  uint32_t n_part;
   // n_win windows (grid.y): window w's outputs at out + w * out_pitch, slot ids + w *
   // id_stride, records + w * vq_cap; rows [n_shards][n_win] (rank-major, as an
   // all-gather of every shard's n_win rows lays them out)
@@ -1800,19 +1836,20 @@ __device__ __forceinline__ unsigned long long fix_first_draw(const FixParams& f,
   return pre;
 }
 
-// The fix-up runs per 65,536-slot segment of the window (2,048 words of every plane;
-// a lag or tiled tile never spans two segments): pass A finds each segment's first
-// record (records are in ascending slot order), pass B gives one wave per segment.
-// The wave re-draws its records' VQ slots at their global positions (64 ChaCha12
-// blocks per pass, one per lane, into LDS), counts them into the shard's statistics,
-// collects the own-vote bits that change in an LDS mask of the segment, and rewrites
-// the segment's own-vote plane in one coalesced read-XOR-write stream (an own-vote bit
-// changes for ~25 % of the VQ slots when the position moved, so nearly every line of
-// the plane is touched: per-bit atomics cost a random line read-modify-write each).
-// The rare decision changes (the own vote decides the round-2 count) are atomic XORs.
-constexpr uint32_t kFixSegShift = 16;                      // 65,536 slots per segment
-constexpr uint32_t kFixSegWords = 1u << (kFixSegShift - 5);  // 2,048 words
-
+// The fix-up runs per 32,768-slot segment of the window (1,024 words of every plane):
+// pass A finds each segment's first record (records are in ascending slot order),
+// pass B gives one wave per segment. The wave re-draws its records' VQ slots at their
+// global positions (64 ChaCha12 blocks per pass, one per lane, into LDS: up to 505
+// records, one pass for a segment under ~1.5 % VQ slots), counts them into the shard's
+// statistics, collects the own-vote bits that change in an LDS mask of the segment,
+// and rewrites the segment's own-vote plane in one coalesced read-XOR-write stream (an
+// own-vote bit changes for ~25 % of the VQ slots when the position moved, so nearly
+// every line of the plane is touched: per-bit atomics cost a random line
+// read-modify-write each). The rare decision changes (the own vote decides the
+// round-2 count) are atomic XORs. (65,536-slot segments: two passes per segment at
+// the bench's 0.8 % VQ and 3 workgroups per CU (LDS), 151 vs ... us per 2^30 slots.)
+constexpr uint32_t kFixSegShift = 15;                      // 32,768 slots per segment
+constexpr uint32_t kFixSegWords = 1u << (kFixSegShift - 5);  // 1,024 words
 static __global__ __launch_bounds__(256) void shard_fixup_seg_kernel(FixParams f, uint32_t* seg_first,
                                                                     uint32_t n_seg) {
   const uint32_t win = blockIdx.y;
@@ -1820,11 +1857,17 @@ static __global__ __launch_bounds__(256) void shard_fixup_seg_kernel(FixParams f
   const unsigned long long nn = n < f.vq_cap ? n : f.vq_cap;
   const unsigned long long* rec = f.rec + win * f.vq_cap;
   uint32_t* sf = seg_first + (uint64_t)win * n_seg;
-  for (unsigned long long k = (unsigned long long)blockIdx.x * 256 + threadIdx.x; k < nn;
-       k += (unsigned long long)gridDim.x * 256) {
-    const uint32_t seg = (uint32_t)rec[k] >> kFixSegShift;
-    const uint32_t prev = k ? (uint32_t)rec[k - 1] >> kFixSegShift : ~0u;
-    if (seg != prev && seg < n_seg) sf[seg] = (uint32_t)k + 1u;  // 0: no record in the segment
+  // 4 consecutive records per thread, all loads in flight at once (a grid-stride loop
+  // of one record per thread waits out one load latency per record)
+  for (unsigned long long k0 = ((unsigned long long)blockIdx.x * 256 + threadIdx.x) * 4; k0 < nn;
+       k0 += (unsigned long long)gridDim.x * 1024) {
+    uint32_t seg[5];
+    seg[0] = k0 ? (uint32_t)rec[k0 - 1] >> kFixSegShift : ~0u;
+#pragma unroll
+    for (int j = 0; j < 4; j++) seg[j + 1] = k0 + j < nn ? (uint32_t)rec[k0 + j] >> kFixSegShift : ~0u;
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      if (k0 + j < nn && seg[j + 1] != seg[j] && seg[j + 1] < n_seg) sf[seg[j + 1]] = (uint32_t)(k0 + j) + 1u;  // 0: none
   }
 }
 
@@ -1924,6 +1967,7 @@ static __global__ __launch_bounds__(256) void shard_fixup_kernel(FixParams f, co
       uint32_t* p2 = f.out + 2 * f.lout.pstride;
 #pragma unroll
       for (uint32_t h = 0; h < kFixSegWords; h += 16 * 64) {  // 16 words per lane in flight at once
+        static_assert(kFixSegWords % (16 * 64) == 0, "whole batches");
         uint32_t m[16], v[16];
 #pragma unroll
         for (int j = 0; j < 16; j++) {
@@ -1943,30 +1987,24 @@ static __global__ __launch_bounds__(256) void shard_fixup_kernel(FixParams f, co
   mn = wave_min64(mn);
   if (lane == 0) { red[wave][0] = dec; red[wave][1] = v1; red[wave][2] = mx; red[wave][3] = mn; }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int w = 1; w < 4; w++) {
-      dec += red[w][0]; v1 += red[w][1];
-      mx = red[w][2] > mx ? red[w][2] : mx;
-      mn = red[w][3] < mn ? red[w][3] : mn;
-    }
-    if (dec) atomicAdd(f.acc + win, dec);
-    if (v1) atomicAdd(f.acc + f.n_win + win, v1);
-    if (mx) atomicMax(f.acc + 2 * f.n_win + win, mx);
-    if (mn != ~0ull) atomicMin(f.acc + 3 * f.n_win + win, mn);
-  }
+  // every workgroup writes its partial (zeros / all ones when it had no records)
+  if (threadIdx.x < 4) f.acc[((uint64_t)win * f.n_part + blockIdx.x) * 4 + threadIdx.x] = fold4(red, threadIdx.x);
 }
 
 // The shard's final row: VQ-slot counts and extremes folded in, the engine's
 // stream position advanced past the whole window's draws (every shard's).
-static __global__ void shard_fixup_finish_kernel(FixParams f, DevResult* row_ctx, DevResult* row_user) {
-  if (threadIdx.x != 0) return;
+static __global__ __launch_bounds__(256) void shard_fixup_finish_kernel(FixParams f, DevResult* row_ctx,
+                                                                        DevResult* row_user) {
+  __shared__ unsigned long long red[4][4];
   unsigned long long pos = f.state->rng_next;
   for (uint32_t w = 0; w < f.n_win; w++) {
+    unsigned long long a[4];  // the window's workgroup partials (shard_fixup_kernel)
+    fold_partials(f.acc + (uint64_t)w * f.n_part * 4, f.n_part, red, a);
+    if (threadIdx.x != 0) continue;
+    const unsigned long long a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3];
     DevResult r = f.rows[(uint64_t)f.shard * f.n_win + w];
     unsigned long long total = 0;
     for (uint32_t s = 0; s < f.n_shards; s++) total += f.rows[(uint64_t)s * f.n_win + w].n_draws;
-    const unsigned long long a0 = f.acc[w], a1 = f.acc[f.n_win + w], a2 = f.acc[2 * f.n_win + w],
-                             a3 = f.acc[3 * f.n_win + w];
     r.n_decided += a0;
     r.n_v1 += a1;
     if (a2 && a2 - 1 > r.last_committed_max) r.last_committed_max = a2 - 1;
@@ -1979,7 +2017,7 @@ static __global__ void shard_fixup_finish_kernel(FixParams f, DevResult* row_ctx
     if (w + 1 == f.n_win) *row_ctx = r;
     if (row_user) row_user[w] = r;
   }
-  f.state->rng_next = pos;
+  if (threadIdx.x == 0) f.state->rng_next = pos;
 }
 
 // Fold the shards' final rows of one window into the engine state exactly as one
@@ -2037,8 +2075,12 @@ struct FollowParams {
   uint64_t n_slots, n_words, slot_base, max_phase;
   DevState* state;
   uint32_t* applied;          // optional: one plane of n_words words
-  unsigned long long* acc;    // [4] applied, committed, max applied id + 1 (<= max_phase), min uncommitted id
+  // per-workgroup partials [n_part][4]: applied, committed, max applied id + 1 (<= max_phase),
+  // min uncommitted id (folded by the finish kernel: no same-address atomics)
+  unsigned long long* acc;
+  uint32_t n_part;
 };
+constexpr uint32_t kFollowGrid = 2048;  // follower_kernel workgroups at most (grid-stride)
 
 static __global__ __launch_bounds__(256) void follower_kernel(FollowParams f) {
   const unsigned long long lc = f.state->last_committed;
@@ -2073,34 +2115,27 @@ static __global__ __launch_bounds__(256) void follower_kernel(FollowParams f) {
   mn = wave_min64(mn);
   if (lane == 0) { red[wave][0] = app; red[wave][1] = com; red[wave][2] = mx; red[wave][3] = mn; }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int w = 1; w < 4; w++) {
-      app += red[w][0]; com += red[w][1];
-      mx = red[w][2] > mx ? red[w][2] : mx;
-      mn = red[w][3] < mn ? red[w][3] : mn;
-    }
-    if (app) atomicAdd(f.acc + 0, app);
-    if (com) atomicAdd(f.acc + 1, com);
-    if (mx) atomicMax(f.acc + 2, mx);
-    if (mn != ~0ull) atomicMin(f.acc + 3, mn);
-  }
+  if (threadIdx.x < 4) f.acc[(uint64_t)blockIdx.x * 4 + threadIdx.x] = fold4(red, threadIdx.x);
 }
 
-static __global__ void follower_finish_kernel(FollowParams f, unsigned long long* gate_out, DevResult* res_ctx,
-                                              DevResult* res_user) {
+static __global__ __launch_bounds__(256) void follower_finish_kernel(FollowParams f, unsigned long long* gate_out,
+                                                                     DevResult* res_ctx, DevResult* res_user) {
+  __shared__ unsigned long long red[4][4];
+  unsigned long long a[4];
+  fold_partials(f.acc, f.n_part, red, a);
   if (threadIdx.x != 0) return;
   DevState s = *f.state;
   DevResult r;
   r.n_slots = f.n_slots;
-  r.n_v1 = f.acc[0];
-  r.n_decided = f.acc[1];
+  r.n_v1 = a[0];
+  r.n_decided = a[1];
   r.n_pending_r1 = 0;
   r.n_draws = 0;
   if (gate_out) *gate_out = s.last_committed;
   unsigned long long lc = s.last_committed;
-  if (f.acc[2] && f.acc[2] - 1 > lc) lc = f.acc[2] - 1;
+  if (a[2] && a[2] - 1 > lc) lc = a[2] - 1;
   const unsigned long long end = f.slot_base + f.n_slots;
-  const unsigned long long fu = f.acc[3] < end ? f.acc[3] : end;
+  const unsigned long long fu = a[3] < end ? a[3] : end;
   unsigned long long wm = s.commit_watermark;
   if (f.slot_base <= wm && wm < fu) wm = fu;
   r.last_committed_max = lc;
