@@ -82,7 +82,7 @@ def parse():
                     help="GPUs (ranks) of the run; without an external launcher (no WORLD_SIZE) N > 1 starts N "
                          "rank processes itself; under torch.distributed.run it must equal WORLD_SIZE")
     ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=25)  # clocks settle over ~20 launches (tools/warm_probe.py)
     ap.add_argument("--windows", type=int, default=1024)
     ap.add_argument("--replicas", type=int, default=5)
     ap.add_argument("--sets", type=int, default=3)

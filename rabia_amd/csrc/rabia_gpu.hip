@@ -607,11 +607,19 @@ static int fixup_impl(rg_ctx* ctx, uint32_t n_win, uint32_t* out_dev, uint64_t o
   if (int rc = make_layout(ctx, kOutPlanes, n_words, stride_words, &lout, &need, "rg_shard_fixup")) return rc;
   if (n_win > 1 && out_pitch < (ctx->cfg.tile_words ? need : n_words))
     return fail(ctx, RG_EINVAL, "rg_shard_fixup_windows: out pitch is smaller than one window's output planes");
+#ifdef RG_FIX_SEGMENT
   // per 32,768-slot segment: the index of its first record (pass A, a grid-stride loop
   // over the records: their count lives on the device), then one wave per segment,
   // four per workgroup, each workgroup's statistics a partial folded by the finish
   const uint32_t n_seg = (uint32_t)((n_words + kFixSegWords - 1) / kFixSegWords);
   const uint32_t n_part = (n_seg + 3) / 4;
+#else
+  // one thread per ChaCha12 block of the records' global positions, grid-stride over
+  // at most kFixGrid workgroups (the record count lives on the device)
+  const uint64_t rec_most = records_cap < n_slots ? records_cap : n_slots;
+  const uint64_t blk_most = rec_most / 8 + 2;
+  const uint32_t n_part = (uint32_t)std::min<uint64_t>((blk_most + 255) / 256, kFixGrid);
+#endif
   if (4ull * n_part * n_win > ctx->fix_acc_cap) {
     RG_HIP(ctx, hipDeviceSynchronize());
     (void)hipFree(ctx->fix_acc);
@@ -638,6 +646,7 @@ static int fixup_impl(rg_ctx* ctx, uint32_t n_win, uint32_t* out_dev, uint64_t o
   f.n_win = n_win;
   f.out_pitch = out_pitch;
   f.id_stride = id_stride;
+#ifdef RG_FIX_SEGMENT
   if ((uint64_t)n_seg * n_win > ctx->fix_seg_cap) {
     RG_HIP(ctx, hipDeviceSynchronize());
     (void)hipFree(ctx->fix_seg);
@@ -651,7 +660,10 @@ static int fixup_impl(rg_ctx* ctx, uint32_t n_win, uint32_t* out_dev, uint64_t o
   const uint64_t ga = (rec_max + 1023) / 1024;  // 4 records per thread; blocks past the count exit at once
   hipLaunchKernelGGL(shard_fixup_seg_kernel, dim3((uint32_t)(ga < 8192 ? ga : 8192), n_win), dim3(256), 0, s, f,
                      ctx->fix_seg, n_seg);
-  hipLaunchKernelGGL(shard_fixup_kernel, dim3(n_part, n_win), dim3(256), 0, s, f, ctx->fix_seg, n_seg);
+  hipLaunchKernelGGL(shard_fixup_seg_wave_kernel, dim3(n_part, n_win), dim3(256), 0, s, f, ctx->fix_seg, n_seg);
+#else
+  hipLaunchKernelGGL(shard_fixup_kernel, dim3(n_part, n_win), dim3(256), 0, s, f);
+#endif
   hipLaunchKernelGGL(shard_fixup_finish_kernel, dim3(1), dim3(256), 0, s, f, ctx->stage_result + 0,
                      reinterpret_cast<DevResult*>(rows_out_dev));
   RG_HIP(ctx, hipGetLastError());

@@ -1836,6 +1836,95 @@ __device__ __forceinline__ unsigned long long fix_first_draw(const FixParams& f,
   return pre;
 }
 
+// The fix-up, one thread per ChaCha12 block of the window's global draw positions
+// (grid-stride): the thread loads the (up to) 8 records whose draws the block holds
+// (records are indexed by local draw number, so block b holds records 8b - g0 ..
+// 8b + 7 - g0), re-draws their VQ slots, counts them into the statistics and
+// XOR-patches the own-vote bits that change, one atomic per changed word of its run
+// (records are in slot order: a block's changes fall in a few neighbouring words), and
+// the rare decision changes (the own vote decides the round-2 count). Every lane works
+// on a block of its own, so no lane idles on a partial pass and no LDS is needed; the
+// statistics are one partial per workgroup.
+constexpr uint32_t kFixGrid = 2048;  // fix-up workgroups at most (grid-stride beyond)
+static __global__ __launch_bounds__(256) void shard_fixup_kernel(FixParams f) {
+  const uint32_t win = blockIdx.y;
+  const unsigned long long n = f.rows[(uint64_t)f.shard * f.n_win + win].n_draws;
+  const unsigned long long g0 = fix_first_draw(f, win);  // global position of local draw 0
+  if (win) {  // this window's outputs, slot ids, records
+    f.out += win * f.out_pitch;
+    f.slot_base += win * f.id_stride;
+    f.rec += win * f.vq_cap;
+  }
+  const unsigned long long nn = n < f.vq_cap ? n : f.vq_cap;
+  unsigned long long dec = 0, v1 = 0, mx = 0, mn = ~0ull;
+  uint32_t* p2 = f.out + 2 * f.lout.pstride;
+  const unsigned long long b_end = (g0 + nn + 7) >> 3;
+  for (unsigned long long b = (g0 >> 3) + (unsigned long long)blockIdx.x * 256 + threadIdx.x; nn && b < b_end;
+       b += (unsigned long long)gridDim.x * 256) {
+    const long long k0 = (long long)(b << 3) - (long long)g0;  // local index of the block's first draw
+    unsigned long long rr[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const long long k = k0 + j;
+      rr[j] = (k >= 0 && (unsigned long long)k < nn) ? f.rec[k] : ~0ull;
+    }
+    uint32_t x[16];
+    chacha_block<12>(f.key, b, 0, x);
+    uint32_t cur_w = ~0u, cur_m = 0;  // the run's word being patched and its XOR mask
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const unsigned long long r = rr[j];
+      if (r == ~0ull) continue;
+      const uint32_t off = (uint32_t)r, info = (uint32_t)(r >> 32);
+      const unsigned long long u = (unsigned long long)x[2 * j] | ((unsigned long long)x[2 * j + 1] << 32);
+      const uint32_t cls = info & 3u;
+      const uint32_t own = cls == kRecGt ? (u < kP90) : (cls == kRecLt ? (u >= kP90) : (u < kP80));
+      const uint32_t prov = (info >> 6) & 1u;
+      const uint32_t d = own ? (info >> 4) & 3u : (info >> 2) & 3u;
+      const unsigned long long id = f.slot_base + off;
+      if (d <= kCodeV1) {
+        dec++;
+        if (d == kCodeV1) {
+          v1++;
+          if ((f.max_phase == 0 || id <= f.max_phase) && id + 1 > mx) mx = id + 1;
+        }
+      } else if (id < mn) {
+        mn = id;
+      }
+      if (own != prov) {
+        const uint32_t w = off >> 5, bit = 1u << (off & 31u);
+        if (w != cur_w) {
+          if (cur_m) atomicXor(p2 + f.lout.base(cur_w), cur_m);
+          cur_w = w;
+          cur_m = 0;
+        }
+        cur_m ^= bit;
+        const uint32_t dp = prov ? (info >> 4) & 3u : (info >> 2) & 3u;
+        const uint32_t dd = d ^ dp;
+        if (dd || (d <= kCodeV1) != (dp <= kCodeV1)) {  // the decision changed: rare
+          const uint64_t base = f.lout.base(w);
+          if (dd & 1u) atomicXor(f.out + base + 4 * f.lout.pstride, bit);
+          if (dd & 2u) atomicXor(f.out + base + 5 * f.lout.pstride, bit);
+          if ((d <= kCodeV1) != (dp <= kCodeV1)) atomicXor(f.out + base + 6 * f.lout.pstride, bit);
+          if ((d == kCodeV1) != (dp == kCodeV1)) atomicXor(f.out + base + 7 * f.lout.pstride, bit);
+        }
+      }
+    }
+    if (cur_m) atomicXor(p2 + f.lout.base(cur_w), cur_m);
+  }
+  __shared__ unsigned long long red[4][4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  dec = wave_sum64(dec);
+  v1 = wave_sum64(v1);
+  mx = wave_max64(mx);
+  mn = wave_min64(mn);
+  if (lane == 0) { red[wave][0] = dec; red[wave][1] = v1; red[wave][2] = mx; red[wave][3] = mn; }
+  __syncthreads();
+  // every workgroup writes its partial (zeros / all ones when it had no records)
+  if (threadIdx.x < 4) f.acc[((uint64_t)win * f.n_part + blockIdx.x) * 4 + threadIdx.x] = fold4(red, threadIdx.x);
+}
+
+#ifdef RG_FIX_SEGMENT  // experiment build: the per-segment fix-up (round 4, LDS own-vote masks)
 // The fix-up runs per 32,768-slot segment of the window (1,024 words of every plane):
 // pass A finds each segment's first record (records are in ascending slot order),
 // pass B gives one wave per segment. The wave re-draws its records' VQ slots at their
@@ -1871,7 +1960,7 @@ static __global__ __launch_bounds__(256) void shard_fixup_seg_kernel(FixParams f
   }
 }
 
-static __global__ __launch_bounds__(256) void shard_fixup_kernel(FixParams f, const uint32_t* seg_first,
+static __global__ __launch_bounds__(256) void shard_fixup_seg_wave_kernel(FixParams f, const uint32_t* seg_first,
                                                                 uint32_t n_seg) {
   __shared__ uint32_t s_blk[4][64][17];         // per wave: 64 ChaCha12 blocks (+1 word: no conflicts)
   __shared__ uint32_t s_m2[4][kFixSegWords];    // per wave: own-vote bits that change in its segment
@@ -1990,6 +2079,8 @@ static __global__ __launch_bounds__(256) void shard_fixup_kernel(FixParams f, co
   // every workgroup writes its partial (zeros / all ones when it had no records)
   if (threadIdx.x < 4) f.acc[((uint64_t)win * f.n_part + blockIdx.x) * 4 + threadIdx.x] = fold4(red, threadIdx.x);
 }
+
+#endif  // RG_FIX_SEGMENT
 
 // The shard's final row: VQ-slot counts and extremes folded in, the engine's
 // stream position advanced past the whole window's draws (every shard's).
