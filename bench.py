@@ -91,7 +91,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="threads of the all-core CPU baseline (0: OMP_NUM_THREADS, else min(cpus, 16))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_c2.json"))
+    ap.add_argument("--pmc-file", default=None,
+                    help="HBM traffic record (tools/pmc_traffic.py); default profiles/pmc_<config>[_sharded].json, "
+                         "used when its replicas and slots per launch match the run's step launch")
     ap.add_argument("--c3-slots", type=int, default=1 << 24, help="C3: slots per step, all ranks")
     ap.add_argument("--config", choices=["c2", "c3", "c5"], default="c2",
                     help="c2: the headline (weak scaling); c5: 9 replicas x 2^26 slots per step split over the "
@@ -102,9 +104,11 @@ def parse():
     ap.add_argument("--sharded", "--c5-sharded", dest="sharded", action="store_true",
                     help="N = 1: run the multi-GPU pipeline (shard step + fix-up + commit, exchanges with one "
                          "rank) instead of the single evaluator: the per-GPU cost of the N > 1 path")
-    ap.add_argument("--fixup-stream", choices=["fix", "comp"], default="comp",
-                    help="N > 1 / --sharded: the fix-up of step t on the second stream (overlapping step t + 1) "
-                         "or on the compute stream right behind step t + 1's launch")
+    ap.add_argument("--fixup-stream", choices=["fix", "comp"], default="fix",
+                    help="N > 1 / --sharded: the fix-up of step t on the second stream (overlapping step t + 1; "
+                         "0.80 vs 0.81, 0.84 vs 0.86, 0.86 vs 0.88 ms per one-shard step in three round-4 "
+                         "runs, profiles/r04_c2_sharded_n1*.json) or on the compute stream right behind step "
+                         "t + 1's launch")
     ap.add_argument("--diag", type=lambda x: int(x, 0), default=0,
                     help="rg_debug_set switches for experiments (include/rabia_gpu_debug.h); 0 = the product path")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
@@ -754,7 +758,8 @@ def main():
                        "layout": f"slot-tiled {a.tile_words}" if a.tile_words else "planar", "parallelism": par},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": load_pmc(a.pmc_file, n, S) if world == 1 else None,
+                         "traffic": load_pmc(a.pmc_file or os.path.join(
+                             ROOT, "profiles", f"pmc_{a.config}{'_sharded' if sharded else ''}.json"), n, K * S),
                          "alg_bytes_per_launch": alg_bytes, "kernel_avg_us": r["kern_ms"] * 1000.0,
                          "kernel": r["launch"]},
             "cpu_baseline": cpu,
