@@ -14,4 +14,5 @@ RABIA_GPU_LIB=$R/rabia_amd/lib/variants/librabia_gpu_norec.so timeout -k 10 300 
   > $OUT/shard_probe_norec.json 2>> $OUT/probe.err &&
 cd /tmp &&
 timeout -s KILL 240 rocprofv3 --kernel-trace --stats -d $OUT/fix_trace -o fix --output-format csv -- \
-  python3 $R/tools/fixup_probe.py > $OUT/fixup.json 2> $OUT/fixup.err
+  python3 $R/tools/fixup_probe.py > $OUT/fixup.json 2> $OUT/fixup.err &&
+cd $R && timeout -k 10 300 python bench.py --steps 20 --warmup 5 --sharded --no-cpu-baseline > $OUT/c2_sharded.json 2> $OUT/err.log
