@@ -106,10 +106,16 @@ int hip_fail(rg_ctx* ctx, hipError_t e, const char* what) {
   } while (0)
 
 constexpr int wmax_for(int n) { return n <= 5 ? 4 : (n <= 10 ? 2 : 1); }
-// persistent lag kernel: one 1024-thread workgroup per CU (launches of >= 2 tiles per
-// CU), else two 512-thread workgroups per CU; lag_words(n) words per thread
+// persistent lag kernel: one workgroup per CU with tiles of kLagBlock x lag_words(n)
+// words (launches of >= 2 such tiles per CU), else two 512-thread workgroups per CU
+// with tiles of 512 x lag_words(n). The one-per-CU tile runs as lag_one_block(n)
+// threads x lag_one_words(n) words: n <= 5 as 512 x 4 (16-byte plane loads per lane:
+// 662.6 vs 668.2 us per 2^30 slots against 1024 x 2, interleaved A/B,
+// profiles/r04_ab_lag_w4_2e30.json), n > 5 as 1024 x 1.
 constexpr int kLagBlock = 1024, kLagBlockSmall = 512;
 constexpr int lag_words(int n) { return n <= 5 ? 2 : 1; }
+constexpr int lag_one_block(int n) { return n <= 5 ? 512 : 1024; }
+constexpr int lag_one_words(int n) { return kLagBlock * lag_words(n) / lag_one_block(n); }
 
 // Tile shapes of the tiled kernel: {threads, words per thread}. Big tiles keep the
 // per-launch count of tiles and look-back hand-offs low on large windows; small
@@ -138,8 +144,12 @@ struct Disp {
   }
   // persistent lag kernel (large launches): grid = resident workgroups, tiles by ticket
   static void ref_lag(uint32_t grid, hipStream_t s, const StepParams& p) {  // n <= 10 (step_impl)
-    if constexpr (N <= 10)
-      hipLaunchKernelGGL((ref_lag_kernel<N, lag_words(N), kLagBlock, false>), dim3(grid), dim3(kLagBlock), 0, s, p);
+    if constexpr (N <= 5)  // 8 waves per CU, up to 256 VGPRs each
+      hipLaunchKernelGGL((ref_lag_kernel<N, lag_one_words(N), lag_one_block(N), false, 2>), dim3(grid),
+                         dim3(lag_one_block(N)), 0, s, p);
+    else if constexpr (N <= 10)
+      hipLaunchKernelGGL((ref_lag_kernel<N, lag_one_words(N), lag_one_block(N), false>), dim3(grid),
+                         dim3(lag_one_block(N)), 0, s, p);
   }
   static void ref_lag512(uint32_t grid, hipStream_t s, const StepParams& p) {
     if constexpr (N <= 10)
@@ -525,8 +535,8 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
   hipStream_t s = pick_stream(ctx, stream);
   ctx->last_launch[0] = lag ? 1u : (wmvc ? 2u : 0u);
   ctx->last_launch[1] = shard ? 1u : 0u;
-  ctx->last_launch[2] = lag ? (uint32_t)lag_block : (uint32_t)cfg_block(cfg);
-  ctx->last_launch[3] = lag ? (uint32_t)lag_words(n) : (uint32_t)cfg_words(cfg, n);
+  ctx->last_launch[2] = lag ? (uint32_t)(lag1024 ? lag_one_block(n) : kLagBlockSmall) : (uint32_t)cfg_block(cfg);
+  ctx->last_launch[3] = lag ? (uint32_t)(lag1024 ? lag_one_words(n) : lag_words(n)) : (uint32_t)cfg_words(cfg, n);
   ctx->last_launch[4] = lag ? lag_grid : (uint32_t)n_tiles;
   ctx->last_launch[5] = win.n;
   std::unique_lock<std::mutex> chain_lk;

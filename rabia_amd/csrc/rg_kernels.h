@@ -1177,17 +1177,20 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const uint32_t* bas
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(base), (short)0, (int)kOffNone, 0x00020000);
 }
 constexpr int kAuxNT = 2;  // non-temporal (read or written once)
+#ifndef RG_LAG_LD_AUX        // experiment builds: the plane loads' cache policy
+#define RG_LAG_LD_AUX kAuxNT
+#endif
 
 template <int W>
 __device__ __forceinline__ void buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, uint32_t (&v)[W]) {
   if constexpr (W == 4) {
-    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, kAuxNT);
+    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, RG_LAG_LD_AUX);
     v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
   } else if constexpr (W == 2) {
-    const u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, kAuxNT);
+    const u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, RG_LAG_LD_AUX);
     v[0] = x.x; v[1] = x.y;
   } else {
-    v[0] = __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, kAuxNT);
+    v[0] = __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, RG_LAG_LD_AUX);
   }
 }
 template <int W>

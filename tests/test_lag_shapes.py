@@ -3,11 +3,11 @@ C ABI's dispatch (step_impl, rabia_gpu.hip) can pick, compared with the oracle
 directly — not only with the tiled kernel:
 
 - the bench shape: n = 5, 2^30 slots, slot-tiled 1024, default dispatch
-  (ref_lag_kernel<5, 2, 1024, false>): size-independent properties over all 2^30
+  (ref_lag_kernel<5, 4, 512, false>): size-independent properties over all 2^30
   slots, oracle slices at both ends, across workgroup-tile boundaries and in the
   middle (each slice's StdRng offset = the VQ slots before it), the tiled kernel's
   output over the same slots, and one call == two calls;
-- the 1024-thread shape forced at 2^25 (+ ragged) slots for n = 3, 5, 7, 9 against
+- the one-workgroup-per-CU shape forced at 2^25 (+ ragged) slots for n = 3, 5, 7, 9 against
   the full oracle, on the default grid and on a 5-workgroup grid (many tickets each);
 - the shape chosen without any switch for n = 3, 7, 9 at the first size that selects it;
 - the SHARD = true instantiation (draw records, VQ slots left to the fix-up) in 2-4
@@ -40,7 +40,15 @@ def n_cu(torch):
 
 
 def lag_words(n):
+    """Words per thread of the two-workgroups-per-CU (512-thread) lag shape; its tile
+    (512 x lag_words) is half the one-workgroup-per-CU tile (1024 x lag_words words)."""
     return 2 if n <= 5 else 1
+
+
+def one_shape(n):
+    """(threads, words per thread) of the one-workgroup-per-CU lag shape: the same
+    1024 x lag_words(n)-word tile as 512 x 4 at n <= 5 (16-byte plane loads), 1024 x 1 above."""
+    return (512, 4) if n <= 5 else (1024, 1)
 
 
 def popc(torch, x):
@@ -124,7 +132,7 @@ def check_slices(oracle, torch, p, cvq, n, kind, seed, slot_base, rng0, self_lan
 @pytest.mark.parametrize("kind", [N.RG_TRACE_AGREE90, N.RG_TRACE_UNIFORM])
 def test_bench_shape_vs_oracle(oracle, kind):
     """The launch bench.py times (n = 5, 2^30 slots = 1024 windows, slot-tiled 1024,
-    default dispatch): ref_lag_kernel<5, 2, 1024, false> on one workgroup per CU."""
+    default dispatch): ref_lag_kernel<5, 4, 512, false> on one workgroup per CU."""
     torch = torch_cuda()
     n, S, T = 5, 1 << 30, 1024
     nw = S // 32
@@ -141,7 +149,7 @@ def test_bench_shape_vs_oracle(oracle, kind):
         launch = ev.last_launch()
         res = ev.last_result()
         st = ev.get_state()
-    assert launch == {"kernel": "lag", "shard": False, "block": 1024, "words": 2, "grid": n_cu(torch),
+    assert launch == {"kernel": "lag", "shard": False, "block": 512, "words": 4, "grid": n_cu(torch),
                       "windows": 1}, launch
     assert res["flags"] == 0 and res["n_slots"] == S
     assert res == N.RgStepResult(*res_d.cpu().numpy().view(np.uint64).tolist()).as_dict()
@@ -196,7 +204,7 @@ def _planar_step(torch, n, S, kind, seed, slot_base, diag, rng0=99, lc_in=3, wm_
 
 @pytest.mark.parametrize("n,kind", [(3, 1), (5, 1), (5, 2), (7, 1), (9, 1), (9, 0)])
 def test_forced_lag1024_vs_full_oracle(oracle, n, kind):
-    """The 1024-thread shape (forced, ragged 2^25 + 4099 slots) on the default grid
+    """The one-workgroup-per-CU shape (forced, ragged 2^25 + 4099 slots) on the default grid
     and on 5 workgroups (~100 tickets each): every slot and the step result equal the
     oracle's."""
     torch = torch_cuda()
@@ -208,7 +216,7 @@ def test_forced_lag1024_vs_full_oracle(oracle, n, kind):
     del r1, r2
     for grid in (0, 5):
         out, stride, res, launch = _planar_step(torch, n, S, kind, 300 + n, base, LAG | (grid << 24), max_phase=mp)
-        assert launch["kernel"] == "lag" and launch["block"] == 1024 and launch["words"] == lag_words(n)
+        assert launch["kernel"] == "lag" and (launch["block"], launch["words"]) == one_shape(n)
         assert launch["grid"] == (grid or n_cu(torch))
         got = decode_outputs(out.view(8, stride).cpu().numpy().view(np.uint32), S)
         for k in KEYS:
@@ -220,14 +228,14 @@ def test_forced_lag1024_vs_full_oracle(oracle, n, kind):
 @pytest.mark.parametrize("n", [3, 7, 9])
 def test_default_dispatch_lag1024(oracle, n):
     """No switch: at the first size where every CU runs >= 32 lag tiles step_impl
-    picks ref_lag_kernel<n, W, 1024, false> (n = 3: 2^29 slots, n = 7, 9: 2^28).
+    picks the one-workgroup-per-CU lag shape (n = 3: 2^29 slots, 512 x 4; n = 7, 9: 2^28, 1024 x 1).
     Properties over every slot, oracle slices, the tiled kernel's output."""
     torch = torch_cuda()
     S = 32 * 32 * n_cu(torch) * 1024 * lag_words(n)
     base, kind, seed = 1, N.RG_TRACE_AGREE90, 50 + n
     out, stride, res, launch = _planar_step(torch, n, S, kind, seed, base, 0, rng0=5, lc_in=0, wm_in=1)
-    assert launch == {"kernel": "lag", "shard": False, "block": 1024, "words": lag_words(n), "grid": n_cu(torch),
-                      "windows": 1}, launch
+    assert launch == {"kernel": "lag", "shard": False, "block": one_shape(n)[0], "words": one_shape(n)[1],
+                      "grid": n_cu(torch), "windows": 1}, launch
     nw = S // 32
     p = word_planes(out, nw, 0, stride)
     cvq = check_properties(torch, p, S, base, 0, res, 5, res["rng_next"], lc_in=0)
@@ -247,8 +255,8 @@ SHARD_CASES = [
     (3, 4, [1_000_003, 777], 0, 2),
     (9, 3, [1 << 21], 2, 5),
     (7, 2, [524_288, 131_071], 1, 0),
-    (9, 2, [1 << 25], 1, 7),   # 2^24-slot shards: the 1024-thread shape
-    (5, 2, [1 << 26], 2, 0),   # 2^25-slot shards: the 1024-thread shape, all VQ
+    (9, 2, [1 << 25], 1, 7),   # 2^24-slot shards: the one-workgroup-per-CU shape
+    (5, 2, [1 << 26], 2, 0),   # 2^25-slot shards: the one-workgroup-per-CU shape, all VQ
 ]
 
 
@@ -270,7 +278,7 @@ def test_shard_lag_forced_vs_one_engine_and_oracle(oracle, n, world, sizes, kind
         assert la["kernel"] == "lag" and la["shard"], la
     assert all(1 <= la["grid"] <= (grid or 2 * n_cu(torch)) for la in launches)
     if sizes[0] >= 1 << 25:
-        assert launches[0]["block"] == 1024
+        assert (launches[0]["block"], launches[0]["words"]) == one_shape(n)
     res_1, st_1 = run_single(n, sizes, votes, out_1, stride, state=state, max_phase=mp)
     assert torch.equal(out_s, out_1)
     for w in range(len(sizes)):
@@ -317,8 +325,8 @@ def test_shard_lag_windows_entry_k1(n, world, S, grid):
 
 def test_shard_lag_default_dispatch_2e29():
     """No switch: 2^30 slots (n = 5, slot-tiled 1024, as the bench lays them out) over
-    2 shards of 2^29 — each shard launch picks ref_lag_kernel<5, 2, 1024, true> —
-    equals one evaluator over the 2^30 slots (ref_lag_kernel<5, 2, 1024, false>):
+    2 shards of 2^29 — each shard launch picks ref_lag_kernel<5, 4, 512, true> —
+    equals one evaluator over the 2^30 slots (ref_lag_kernel<5, 4, 512, false>):
     outputs, per-rank results, engine states. (Planar planes of 2^30 slots exceed the
     lag kernel's 31-bit buffer offsets, so this shape needs the tiled layout.)"""
     torch = torch_cuda()
@@ -357,7 +365,7 @@ def test_shard_lag_default_dispatch_2e29():
     finally:
         for ev in ctxs:
             ev.close()
-    assert all(la == {"kernel": "lag", "shard": True, "block": 1024, "words": 2, "grid": n_cu(torch),
+    assert all(la == {"kernel": "lag", "shard": True, "block": 512, "words": 4, "grid": n_cu(torch),
                       "windows": 1} for la in launches), launches
     out_1 = torch.zeros_like(out_s)
     res_1 = torch.zeros(10, **i64)
