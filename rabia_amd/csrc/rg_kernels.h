@@ -1788,12 +1788,21 @@ __device__ __forceinline__ void fold_partials(const unsigned long long* acc, uin
                                               unsigned long long (&a)[4]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   a[0] = 0; a[1] = 0; a[2] = 0; a[3] = ~0ull;
-  for (uint32_t b = threadIdx.x; b < n; b += 256) {
-    const unsigned long long* x = acc + (uint64_t)b * 4;
-    a[0] += x[0];
-    a[1] += x[1];
-    a[2] = x[2] > a[2] ? x[2] : a[2];
-    a[3] = x[3] < a[3] ? x[3] : a[3];
+  for (uint32_t b0 = threadIdx.x; b0 < n; b0 += 256 * 8) {  // 8 quadruples per thread in flight at once
+    unsigned long long x[8][4];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const uint32_t b = b0 + 256u * u;
+#pragma unroll
+      for (int j = 0; j < 4; j++) x[u][j] = b < n ? acc[(uint64_t)b * 4 + j] : (j == 3 ? ~0ull : 0ull);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      a[0] += x[u][0];
+      a[1] += x[u][1];
+      a[2] = x[u][2] > a[2] ? x[u][2] : a[2];
+      a[3] = x[u][3] < a[3] ? x[u][3] : a[3];
+    }
   }
   a[0] = wave_sum64(a[0]);
   a[1] = wave_sum64(a[1]);
@@ -1848,7 +1857,10 @@ __device__ __forceinline__ unsigned long long fix_first_draw(const FixParams& f,
 // the rare decision changes (the own vote decides the round-2 count). Every lane works
 // on a block of its own, so no lane idles on a partial pass and no LDS is needed; the
 // statistics are one partial per workgroup.
-constexpr uint32_t kFixGrid = 2048;  // fix-up workgroups at most (grid-stride beyond)
+#ifndef RG_FIX_GRID  // experiment builds: other grids
+#define RG_FIX_GRID 2048
+#endif
+constexpr uint32_t kFixGrid = RG_FIX_GRID;  // fix-up workgroups at most (grid-stride beyond)
 static __global__ __launch_bounds__(256) void shard_fixup_kernel(FixParams f) {
   const uint32_t win = blockIdx.y;
   const unsigned long long n = f.rows[(uint64_t)f.shard * f.n_win + win].n_draws;
