@@ -1180,6 +1180,9 @@ constexpr int kAuxNT = 2;  // non-temporal (read or written once)
 #ifndef RG_LAG_LD_AUX        // experiment builds: the plane loads' cache policy
 #define RG_LAG_LD_AUX kAuxNT
 #endif
+#ifndef RG_LAG_ST_AUX        // experiment builds: the plane stores' cache policy
+#define RG_LAG_ST_AUX kAuxNT
+#endif
 
 template <int W>
 __device__ __forceinline__ void buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, uint32_t (&v)[W]) {
@@ -1198,13 +1201,13 @@ __device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, uint32_t voff, 
   if constexpr (W == 4) {
     u32x4 x;
     x.x = v[0]; x.y = v[1]; x.z = v[2]; x.w = v[3];
-    __builtin_amdgcn_raw_buffer_store_b128(x, r, voff, soff, kAuxNT);
+    __builtin_amdgcn_raw_buffer_store_b128(x, r, voff, soff, RG_LAG_ST_AUX);
   } else if constexpr (W == 2) {
     u32x2 x;
     x.x = v[0]; x.y = v[1];
-    __builtin_amdgcn_raw_buffer_store_b64(x, r, voff, soff, kAuxNT);
+    __builtin_amdgcn_raw_buffer_store_b64(x, r, voff, soff, RG_LAG_ST_AUX);
   } else {
-    __builtin_amdgcn_raw_buffer_store_b32(v[0], r, voff, soff, kAuxNT);
+    __builtin_amdgcn_raw_buffer_store_b32(v[0], r, voff, soff, RG_LAG_ST_AUX);
   }
 }
 // 2N vote planes starting at plane `first` (lo, hi per replica lane)
@@ -1422,6 +1425,24 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
         lds_barrier();
         lap(11);
         const unsigned long long k_lim = (cb + kRows) << 3;
+#ifdef RG_LAG_SEL8  // experiment build: this lane's first 8 draws of the pass read from LDS at once
+        const unsigned long long kp = k;
+        unsigned long long uu[8];
+        {
+          uint32_t rem = 0;
+#pragma unroll
+          for (int i = 0; i < W; i++) rem += (uint32_t)__builtin_popcount(mq[i]);
+#pragma unroll
+          for (int j = 0; j < 8; j++) {
+            const unsigned long long kk = kp + (unsigned long long)j;
+            uu[j] = 0;
+            if ((uint32_t)j < rem && kk < k_lim) {
+              const uint32_t row = (uint32_t)((kk >> 3) - cb), ws = (uint32_t)(kk & 7u) * 2u;
+              uu[j] = (unsigned long long)s_blk[row][ws] | ((unsigned long long)s_blk[row][ws + 1] << 32);
+            }
+          }
+        }
+#endif
 #pragma unroll
         for (int i = 0; i < W; i++) {
           if (!mq[i] || k >= k_lim) continue;
@@ -1440,9 +1461,22 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
           while (mq[i] && k < k_lim) {
             const int b = __builtin_ctz(mq[i]);
             mq[i] &= mq[i] - 1;
+#ifdef RG_LAG_SEL8
+            unsigned long long u;
+            const uint32_t dj = (uint32_t)(k - kp);
+            if (dj < 8) {
+              u = uu[0];
+#pragma unroll
+              for (int j = 1; j < 8; j++) u = dj == (uint32_t)j ? uu[j] : u;
+            } else {
+              const uint32_t row = (uint32_t)((k >> 3) - cb), ws = (uint32_t)(k & 7u) * 2u;
+              u = (unsigned long long)s_blk[row][ws] | ((unsigned long long)s_blk[row][ws + 1] << 32);
+            }
+#else
             const uint32_t row = (uint32_t)((k >> 3) - cb), ws = (uint32_t)(k & 7u) * 2u;
             const unsigned long long u =
                 (unsigned long long)s_blk[row][ws] | ((unsigned long long)s_blk[row][ws + 1] << 32);
+#endif
             const bool x0 = (e0 >> b) & 1u, x1 = (e1 >> b) & 1u;  // gt: 1/0, lt: 0/1, tie: 1/1
             const bool v1 = (x0 && !x1) ? (u < kP90) : ((x1 && !x0) ? (u >= kP90) : (u < kP80));
             own[i] |= (uint32_t)v1 << b;
