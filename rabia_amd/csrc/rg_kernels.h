@@ -1425,24 +1425,6 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
         lds_barrier();
         lap(11);
         const unsigned long long k_lim = (cb + kRows) << 3;
-#ifdef RG_LAG_SEL8  // experiment build: this lane's first 8 draws of the pass read from LDS at once
-        const unsigned long long kp = k;
-        unsigned long long uu[8];
-        {
-          uint32_t rem = 0;
-#pragma unroll
-          for (int i = 0; i < W; i++) rem += (uint32_t)__builtin_popcount(mq[i]);
-#pragma unroll
-          for (int j = 0; j < 8; j++) {
-            const unsigned long long kk = kp + (unsigned long long)j;
-            uu[j] = 0;
-            if ((uint32_t)j < rem && kk < k_lim) {
-              const uint32_t row = (uint32_t)((kk >> 3) - cb), ws = (uint32_t)(kk & 7u) * 2u;
-              uu[j] = (unsigned long long)s_blk[row][ws] | ((unsigned long long)s_blk[row][ws + 1] << 32);
-            }
-          }
-        }
-#endif
 #pragma unroll
         for (int i = 0; i < W; i++) {
           if (!mq[i] || k >= k_lim) continue;
@@ -1461,22 +1443,9 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
           while (mq[i] && k < k_lim) {
             const int b = __builtin_ctz(mq[i]);
             mq[i] &= mq[i] - 1;
-#ifdef RG_LAG_SEL8
-            unsigned long long u;
-            const uint32_t dj = (uint32_t)(k - kp);
-            if (dj < 8) {
-              u = uu[0];
-#pragma unroll
-              for (int j = 1; j < 8; j++) u = dj == (uint32_t)j ? uu[j] : u;
-            } else {
-              const uint32_t row = (uint32_t)((k >> 3) - cb), ws = (uint32_t)(k & 7u) * 2u;
-              u = (unsigned long long)s_blk[row][ws] | ((unsigned long long)s_blk[row][ws + 1] << 32);
-            }
-#else
             const uint32_t row = (uint32_t)((k >> 3) - cb), ws = (uint32_t)(k & 7u) * 2u;
             const unsigned long long u =
                 (unsigned long long)s_blk[row][ws] | ((unsigned long long)s_blk[row][ws + 1] << 32);
-#endif
             const bool x0 = (e0 >> b) & 1u, x1 = (e1 >> b) & 1u;  // gt: 1/0, lt: 0/1, tie: 1/1
             const bool v1 = (x0 && !x1) ? (u < kP90) : ((x1 && !x0) ? (u >= kP90) : (u < kP80));
             own[i] |= (uint32_t)v1 << b;
