@@ -1,0 +1,54 @@
+"""bench.py pieces that need no GPU: the defaults the driver's plain `python bench.py`
+relies on (N = 1, the C2 headline at 2^30 slots per step, a warm-up past the clock
+ramp), and the HBM traffic records the line attaches: one per step-kernel launch shape,
+picked only when its replica count and slots per launch match the run's launch."""
+import json
+import os
+import sys
+
+import pytest
+
+import bench
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_defaults(monkeypatch):
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    a = bench.parse()
+    assert a.gpus is None and a.config == "c2" and not a.sharded and a.backend == "nccl"
+    assert a.windows * bench.WINDOW == 1 << 30 and a.replicas == 5 and a.tile_words == 1024
+    assert a.steps == 50 and a.warmup >= 20  # tools/warm_probe.py: clocks settle over ~20 launches
+    assert a.fixup_stream == "fix" and a.diag == 0 and a.pmc_file is None
+
+
+def test_bytes_per_slot():
+    assert bench.bytes_per_slot_ref(5) == 3.5  # 4n bits read + 8 bits written
+    assert bench.bytes_per_slot_ref(9) == 5.5
+
+
+@pytest.mark.parametrize("name,n,slots", [("pmc_c2.json", 5, 1 << 30), ("pmc_c2_sharded.json", 5, 1 << 30),
+                                          ("pmc_c5.json", 9, 1 << 26), ("pmc_c5_sharded.json", 9, 1 << 26)])
+def test_pmc_records(name, n, slots):
+    path = os.path.join(ROOT, "profiles", name)
+    with open(path) as f:
+        d = json.load(f)
+    assert d["replicas"] == n and d["slots_per_launch"] == slots
+    assert d["alg_bytes_per_launch"] == slots * bench.bytes_per_slot_ref(n)
+    # FETCH_SIZE doubled (the gfx950 correction) + WRITE_SIZE, both in KB
+    assert d["hbm_bytes_per_launch"] == 2 * d["fetch_size_kb_median"] * 1024 + d["write_size_kb_median"] * 1024
+    assert d["traffic_over_alg"] == pytest.approx(d["hbm_bytes_per_launch"] / d["alg_bytes_per_launch"])
+    assert 1.0 <= d["traffic_over_alg"] < 1.05
+    assert min(d["dispatches"]) >= 5
+    assert bench.load_pmc(path, n, slots) == d["hbm_bytes_per_launch"]
+    assert bench.load_pmc(path, n + 2, slots) is None
+    assert bench.load_pmc(path, n, slots // 2) is None
+    assert bench.load_pmc(path + ".missing", n, slots) is None
+
+
+def test_layout():
+    stride, in_w, out_w = bench.layout(5, 1 << 30, 1024)
+    tiles = (1 << 25) // 1024
+    assert stride == 1024 and in_w == tiles * 21 * 1024 and out_w == tiles * 8 * 1024
+    stride, in_w, out_w = bench.layout(9, 1000, 0)  # planar: 16-byte aligned plane stride in words
+    assert stride == 32 and in_w == 37 * 32 and out_w == 8 * 32
