@@ -319,7 +319,7 @@ def run_single(a, n, S, label):
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
-    ev = PhaseEvaluator(n, self_lane=n - 1, mode="ref", seed=SEED, tile_words=T)
+    ev = PhaseEvaluator(n, self_lane=n - 1, mode="ref", seed=SEED, tile_words=T, device=torch.cuda.current_device())
     if a.diag:
         N.check(ev.lib.rg_debug_set(ev.ctx, a.diag), ev.ctx)
     sets = []
@@ -407,7 +407,8 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, bitmaps):
     comp = torch.cuda.Stream()
     fix = torch.cuda.Stream()
     torch.cuda.set_stream(comp)
-    ev = PhaseEvaluator(n, self_lane=n - 1, mode="ref", seed=SEED, tile_words=T)  # one seed on every rank
+    # one seed on every rank; the context on this rank's GPU (main: torch.cuda.set_device(LOCAL_RANK))
+    ev = PhaseEvaluator(n, self_lane=n - 1, mode="ref", seed=SEED, tile_words=T, device=torch.cuda.current_device())
     if a.diag:
         N.check(ev.lib.rg_debug_set(ev.ctx, a.diag), ev.ctx)
     cap = max(S // 8, 1 << 16)  # draw records per shard window (agree90: ~1 % of slots are VQ); overflow -> flags
@@ -564,7 +565,7 @@ def run_c3(a, world, rank, dist):
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
-    ev = PhaseEvaluator(n, mode="wmvc", coin_seed=SEED, epoch=1)
+    ev = PhaseEvaluator(n, mode="wmvc", coin_seed=SEED, epoch=1, device=torch.cuda.current_device())
     states = torch.empty(n * stride, dtype=torch.int32, device="cuda")
     info = torch.empty(max(S, 1), dtype=torch.int32, device="cuda")
     nw = (S + 31) // 32
