@@ -160,6 +160,19 @@ class PhaseWindow:
             self.planes[4 * self.n, wd] &= ~m
 
 
+def _current_device() -> int:
+    """torch's current device when torch has initialised the GPU in this process, else 0
+    (no GPU initialisation here)."""
+    import sys
+    torch = sys.modules.get("torch")
+    try:
+        if torch is not None and torch.cuda.is_initialized():
+            return int(torch.cuda.current_device())
+    except Exception:
+        pass
+    return 0
+
+
 class PhaseEvaluator:
     """Owns one rg_ctx (device state: StdRng position, last_committed_phase,
     commit watermark). Not thread-safe, like the single &mut engine task
@@ -167,8 +180,10 @@ class PhaseEvaluator:
 
     def __init__(self, n_replicas: int, *, quorum: int = 0, decide_threshold: int = 0,
                  self_lane: int = -1, mode: str = "ref", seed: int = 0, coin_seed=None,
-                 epoch: int = 0, device: int = 0, tile_words: int = 0):
+                 epoch: int = 0, device=None, tile_words: int = 0):
         self.lib = N.load()
+        if device is None:  # the caller's current device (a rank's GPU after torch.cuda.set_device), else 0
+            device = _current_device()
         self.n = int(n_replicas)
         self.mode = mode
         cfg = N.RgConfig(n_replicas=self.n, quorum=quorum, decide_threshold=decide_threshold,
