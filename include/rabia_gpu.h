@@ -168,7 +168,12 @@ int rg_last_stage_result(rg_ctx* ctx, int stage, rg_step_result* out_host);
  *  1. every shard: rg_phase_step_shard_async — evaluates its slots with draws taken
  *     at a provisional position (no cross-GPU wait), writes one 8-B draw record per
  *     VQ slot (records_dev, capacity records_cap; n_slots always suffices) and its
- *     row (rg_step_result): counts, extremes and n_draws of its NON-VQ slots;
+ *     row (rg_step_result): counts, extremes and n_draws of its NON-VQ slots.
+ *     Draw-record overflow (n_draws > records_cap: the records past the cap are not
+ *     written) is NOT flagged in this row: the step cannot know it before its
+ *     statistics fold. The fix-up flags it (flags bit 8) in its final row, and the
+ *     commit carries the bit into the window's result, so a caller checks the
+ *     fix-up's or the commit's row, not the step's;
  *  2. exchange the rows (all-gather, rank order) -> rows_dev[n_shards];
  *  3. every shard: rg_shard_fixup_async — re-draws its VQ slots at their global
  *     positions, XOR-patches the output bits that change, and writes its final row
@@ -201,9 +206,12 @@ int rg_phase_step_shard_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* 
  * fix-up re-draws every VQ slot at its global position, so the fixed outputs, rows
  * and engine state are the same). Stages (2)-(4) then run per window as above, with
  * that window's out buffer, records and rows. The context's last result is the last
- * window's row. For n_windows > 1 the pitches must cover one window's planes (planar:
- * >= ceil(n_slots/32) words; slot-tiled: >= the window's tiles x planes x tile_words),
- * else RG_EINVAL: overlapping windows would be patched twice by the fix-up. */
+ * window's row. For n_windows > 1 no word may belong to two windows, else RG_EINVAL
+ * (overlapping windows would be patched twice by the fix-up). Slot-tiled: pitch >= the
+ * window's tiles x planes x tile_words. Planar (plane p of window w at w * pitch + p *
+ * stride_words), one of: plane-major, pitch >= ceil(n_slots/32) and (n_windows - 1) *
+ * pitch + ceil(n_slots/32) <= stride_words; window-major, pitch >= (planes - 1) *
+ * stride_words + ceil(n_slots/32). */
 int rg_phase_step_shard_windows_async(rg_ctx* ctx, uint32_t n_windows, const uint32_t* votes_dev,
                                       uint64_t votes_pitch_words, uint32_t* out_dev, uint64_t out_pitch_words,
                                       uint64_t n_slots, uint64_t stride_words, uint64_t slot_base,

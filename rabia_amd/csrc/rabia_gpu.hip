@@ -55,8 +55,6 @@ struct rg_ctx {
   unsigned long long* cluster_stats = nullptr;  // [kClusterStats]
   unsigned long long* fix_acc = nullptr;        // sharded REF fix-up accumulators [4][windows]
   uint64_t fix_acc_cap = 4;
-  uint32_t* fix_seg = nullptr;                  // sharded REF fix-up: first record per segment [windows][segments]
-  uint64_t fix_seg_cap = 0;
   unsigned long long* follow_acc = nullptr;     // follower commit partials [kFollowGrid][4]
   // results of the shard fix-up / shard commit / follower commit: each stage writes
   // its own (a fix-up may run on another stream than the next window's step, whose
@@ -254,6 +252,22 @@ int make_layout(rg_ctx* ctx, uint32_t planes, uint64_t n_words, uint64_t stride,
   return RG_OK;
 }
 
+// Multi-window buffers: window w's copy of a P-plane buffer starts w * pitch words after
+// window 0's. Slot-tiled: a window's planes are one block of `need` words, so pitch >=
+// need. Planar (plane p of window w at w * pitch + p * stride): either plane-major (the
+// windows side by side inside each plane: pitch >= n_words and the last window's words
+// end within the plane, (n_win - 1) * pitch + n_words <= stride) or window-major (each
+// window's P planes one after another: pitch >= (P - 1) * stride + n_words). Anything
+// else aliases some word of two windows, which the fix-up would XOR-patch twice.
+bool windows_disjoint(const rg_ctx* ctx, uint32_t planes, uint64_t n_words, uint64_t stride, uint64_t pitch,
+                      uint64_t need, uint32_t n_win) {
+  if (n_win <= 1) return true;
+  if (ctx->cfg.tile_words) return pitch >= need;
+  const bool plane_major = pitch >= n_words && (uint64_t)(n_win - 1) * pitch + n_words <= stride;
+  const bool window_major = pitch >= (uint64_t)(planes - 1) * stride + n_words;
+  return plane_major || window_major;
+}
+
 }  // namespace
 
 extern "C" {
@@ -376,7 +390,6 @@ int rg_destroy(rg_ctx* ctx) {
   (void)hipFree(ctx->cluster_stats);
   (void)hipFree(ctx->fix_acc);
   (void)hipFree(ctx->follow_acc);
-  (void)hipFree(ctx->fix_seg);
   (void)hipFree(ctx->stage_result);
   (void)hipFree(ctx->d_votes);
   (void)hipFree(ctx->d_out);
@@ -445,12 +458,13 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
   uint64_t need_in, need_out;
   if (int rc = make_layout(ctx, 4 * n + 1, n_words, stride_words, &lin, &need_in, "rg_phase_step")) return rc;
   if (int rc = make_layout(ctx, kOutPlanes, n_words, stride_words, &lout, &need_out, "rg_phase_step")) return rc;
-  if (win.n > 1) {  // window w's planes must not overlap window w + 1's (the fix-up patches them by XOR)
-    const uint64_t min_in = ctx->cfg.tile_words ? need_in : n_words, min_out = ctx->cfg.tile_words ? need_out : n_words;
-    if (win.in_pitch < min_in || win.out_pitch < min_out)
-      return fail(ctx, RG_EINVAL, "rg_phase_step_shard_windows: a pitch is smaller than one window's planes "
-                                  "(planar: ceil(n_slots/32) words; slot-tiled: the window's tiles)");
-  }
+  // window w's planes must not overlap another window's (the fix-up patches them by XOR)
+  if (!windows_disjoint(ctx, 4 * n + 1, n_words, stride_words, win.in_pitch, need_in, win.n) ||
+      !windows_disjoint(ctx, kOutPlanes, n_words, stride_words, win.out_pitch, need_out, win.n))
+    return fail(ctx, RG_EINVAL, "rg_phase_step_shard_windows: the windows' planes overlap (slot-tiled: pitch >= "
+                                "the window's tiles; planar: plane-major, pitch >= ceil(n_slots/32) and "
+                                "(n_windows - 1) * pitch + ceil(n_slots/32) <= stride, or window-major, pitch >= "
+                                "(planes - 1) * stride + ceil(n_slots/32))");
   uint32_t force = (ctx->diag >> 8) & 7u;  // diagnostics: force a tile shape of the tiled kernel
   if (force > 3) force = 0;
   int cfg = force ? (int)force - 1 : pick_cfg(n, n_words);
@@ -458,7 +472,7 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
   // 1024-thread workgroup per CU when the launch gives every CU >= 2 such tiles, else
   // two 512-thread workgroups per CU. diag bit 20 keeps the tiled kernel (A/B), bit 21
   // forces the lag kernel at any size, bit 22 forces the 512-thread shape.
-  const bool lag_ok = !wmvc && cfg == kCfgBig && !force && !(ctx->diag & 0x3u);  // (diag 4: stamps, both kernels)
+  const bool lag_ok = !wmvc && !force && !(ctx->diag & 0x3u);  // (diag 4: stamps, both kernels)
   // (its buffer offsets are 31-bit: every plane of a tile within 2 GiB of the tile base)
   const bool lag_fits = (uint64_t)(4 * n + 1) * lin.pstride * 4 + 4096 < (1ull << 31) &&
                         (uint64_t)kOutPlanes * lout.pstride * 4 + 4096 < (1ull << 31);
@@ -467,19 +481,31 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
   // Measured (tools/ab_variants.py, tools/gpu_c5diag.sh): the lag kernel wins once every
   // CU runs many of its tiles (n = 5: 2^30 slots 700 vs 732 us), the tiled kernel below
   // that (2^28: 195 vs 203; n = 9, 2^26: 90 vs 96; 2^23: 21 vs 41) -> lag from 32
-  // 1024-thread tiles per CU. Multi-window shard launches run the tiled kernel.
-  const bool lag_big = n_words >= 32ull * ctx->n_cu * kLagBlock * (uint64_t)lag_words(n);
-  const bool lag = lag_fits && n <= 10 && win.n == 1 &&
-                   ((ctx->diag & 0x200000u) ? !wmvc : (lag_ok && lag_big && !(ctx->diag & 0x100000u)));
-  const bool lag1024 = lag && !(ctx->diag & 0x400000u) &&
-                       n_words >= 2ull * ctx->n_cu * kLagBlock * (uint64_t)lag_words(n);
+  // 1024-thread tiles per CU. A multi-window shard launch counts all its windows' words
+  // (its tickets run through every window): n = 9, 32 windows of 2^23 slots: 0.59 of the
+  // HBM peak for one 2^28-slot lag launch against 0.54 for the tiled K-window launch
+  // (profiles/r05/c5_probe_n9_k32_before.json).
+  const bool mw = shard && win.n > 1;
+  const uint64_t launch_words = n_words * (mw ? win.n : 1u);
+  const bool lag_big = launch_words >= 32ull * ctx->n_cu * kLagBlock * (uint64_t)lag_words(n);
+  const uint64_t tiles_1024 = (n_words + kLagBlock * lag_words(n) - 1) / (kLagBlock * lag_words(n));
+  const bool mw_fits = !mw || tiles_1024 * win.n < (1ull << 30);  // tickets and look-back indices are 31-bit
+  const bool lag = lag_fits && mw_fits && n <= 10 &&
+                   ((ctx->diag & 0x200000u) ? !wmvc
+                                            : (lag_ok && lag_big && !(ctx->diag & 0x100000u) &&
+                                               (mw || cfg == kCfgBig)));
+  // multi-window launches run only the one-workgroup-per-CU shape
+  const bool lag1024 = lag && (mw || (!(ctx->diag & 0x400000u) &&
+                                      n_words >= 2ull * ctx->n_cu * kLagBlock * (uint64_t)lag_words(n)));
   const uint64_t lag_block = lag1024 ? kLagBlock : kLagBlockSmall;
   uint64_t tile_words = lag ? lag_block * lag_words(n) : (uint64_t)cfg_block(cfg) * cfg_words(cfg, n);
-  uint64_t n_tiles = (n_words + tile_words - 1) / tile_words;
+  uint64_t n_tiles = (n_words + tile_words - 1) / tile_words;  // per window
+  const uint64_t launch_tiles = n_tiles * (mw ? win.n : 1u);
   const uint32_t grid_force = (ctx->diag >> 24) & 0xFFu;  // diagnostics: lag-kernel grid (tests: many tiles per WG)
   const uint64_t lag_grid_max = grid_force ? grid_force : (lag1024 ? 1ull : 2ull) * ctx->n_cu;
-  const uint32_t lag_grid = (uint32_t)(n_tiles < lag_grid_max ? n_tiles : lag_grid_max);
-  const uint64_t gran_tiles = lag ? (n_tiles > 3ull * lag_grid ? n_tiles : 3ull * lag_grid) : n_tiles * win.n;
+  const uint32_t lag_grid = (uint32_t)(launch_tiles < lag_grid_max ? launch_tiles : lag_grid_max);
+  const uint64_t gran_tiles = lag ? (launch_tiles > 3ull * lag_grid ? launch_tiles : 3ull * lag_grid)
+                                  : n_tiles * win.n;
   if (int rc = ensure_tiles(ctx, gran_tiles, false)) return rc;
   // Statistics granules carry 12 bits of seq and look-back granules 31: start a
   // fresh epoch on zeroed granules whenever either wraps.
@@ -547,7 +573,7 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
     else if (dc->owner && (dc->owner != ctx || dc->stream != s)) RG_HIP(ctx, hipStreamWaitEvent(s, dc->ev, 0));
   }
   if (shard)
-    launch_ref_shard(n, lag ? (lag1024 ? -1 : 0) : cfg_block(cfg), cfg_words(cfg, n),
+    launch_ref_shard(n, lag ? (mw ? -2 : (lag1024 ? -1 : 0)) : cfg_block(cfg), cfg_words(cfg, n),
                      lag ? lag_grid : (uint32_t)n_tiles, s, p);
   else if (lag1024) kRefLagLaunch[n](lag_grid, s, p);
   else if (lag) kRefLag512Launch[n](lag_grid, s, p);
@@ -615,21 +641,13 @@ static int fixup_impl(rg_ctx* ctx, uint32_t n_win, uint32_t* out_dev, uint64_t o
   Layout lout;
   uint64_t need;
   if (int rc = make_layout(ctx, kOutPlanes, n_words, stride_words, &lout, &need, "rg_shard_fixup")) return rc;
-  if (n_win > 1 && out_pitch < (ctx->cfg.tile_words ? need : n_words))
-    return fail(ctx, RG_EINVAL, "rg_shard_fixup_windows: out pitch is smaller than one window's output planes");
-#ifdef RG_FIX_SEGMENT
-  // per 32,768-slot segment: the index of its first record (pass A, a grid-stride loop
-  // over the records: their count lives on the device), then one wave per segment,
-  // four per workgroup, each workgroup's statistics a partial folded by the finish
-  const uint32_t n_seg = (uint32_t)((n_words + kFixSegWords - 1) / kFixSegWords);
-  const uint32_t n_part = (n_seg + 3) / 4;
-#else
+  if (!windows_disjoint(ctx, kOutPlanes, n_words, stride_words, out_pitch, need, n_win))
+    return fail(ctx, RG_EINVAL, "rg_shard_fixup_windows: the windows' output planes overlap (same rule as the step)");
   // one thread per ChaCha12 block of the records' global positions, grid-stride over
   // at most kFixGrid workgroups (the record count lives on the device)
   const uint64_t rec_most = records_cap < n_slots ? records_cap : n_slots;
   const uint64_t blk_most = rec_most / 8 + 2;
   const uint32_t n_part = (uint32_t)std::min<uint64_t>((blk_most + 255) / 256, kFixGrid);
-#endif
   if (4ull * n_part * n_win > ctx->fix_acc_cap) {
     RG_HIP(ctx, hipDeviceSynchronize());
     (void)hipFree(ctx->fix_acc);
@@ -656,24 +674,7 @@ static int fixup_impl(rg_ctx* ctx, uint32_t n_win, uint32_t* out_dev, uint64_t o
   f.n_win = n_win;
   f.out_pitch = out_pitch;
   f.id_stride = id_stride;
-#ifdef RG_FIX_SEGMENT
-  if ((uint64_t)n_seg * n_win > ctx->fix_seg_cap) {
-    RG_HIP(ctx, hipDeviceSynchronize());
-    (void)hipFree(ctx->fix_seg);
-    ctx->fix_seg = nullptr;
-    ctx->fix_seg_cap = 0;
-    RG_HIP(ctx, hipMalloc(&ctx->fix_seg, (uint64_t)n_seg * n_win * 4));
-    ctx->fix_seg_cap = (uint64_t)n_seg * n_win;
-  }
-  RG_HIP(ctx, hipMemsetAsync(ctx->fix_seg, 0, (uint64_t)n_seg * n_win * 4, s));
-  const uint64_t rec_max = records_cap < n_slots ? records_cap : n_slots;
-  const uint64_t ga = (rec_max + 1023) / 1024;  // 4 records per thread; blocks past the count exit at once
-  hipLaunchKernelGGL(shard_fixup_seg_kernel, dim3((uint32_t)(ga < 8192 ? ga : 8192), n_win), dim3(256), 0, s, f,
-                     ctx->fix_seg, n_seg);
-  hipLaunchKernelGGL(shard_fixup_seg_wave_kernel, dim3(n_part, n_win), dim3(256), 0, s, f, ctx->fix_seg, n_seg);
-#else
   hipLaunchKernelGGL(shard_fixup_kernel, dim3(n_part, n_win), dim3(256), 0, s, f);
-#endif
   hipLaunchKernelGGL(shard_fixup_finish_kernel, dim3(1), dim3(256), 0, s, f, ctx->stage_result + 0,
                      reinterpret_cast<DevResult*>(rows_out_dev));
   RG_HIP(ctx, hipGetLastError());

@@ -51,7 +51,7 @@ struct StepParams {
   uint32_t diag;                  // diagnostic build switches (0 in production):
                                   //  1 skip the look-back wait, 2 skip finish_tile, 4 stamps
   unsigned long long* dbg;        // [n_tiles][8] s_memrealtime stamps when diag & 4
-  uint64_t in_bytes, out_bytes;   // the plane buffers' extents (RG_LAG_CHECK builds check every access)
+  uint64_t in_bytes, out_bytes;   // the plane buffers' extents
   unsigned long long* vq_rec;     // sharded REF: draw records [vq_cap] (rg_common.h)
   uint64_t vq_cap;
   // Sharded REF over n_win windows in one launch (grid.y = window; tiled kernel): window
@@ -1176,24 +1176,18 @@ constexpr uint32_t kOffNone = 0x80000000u;
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const uint32_t* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(base), (short)0, (int)kOffNone, 0x00020000);
 }
-constexpr int kAuxNT = 2;  // non-temporal (read or written once)
-#ifndef RG_LAG_LD_AUX        // experiment builds: the plane loads' cache policy
-#define RG_LAG_LD_AUX kAuxNT
-#endif
-#ifndef RG_LAG_ST_AUX        // experiment builds: the plane stores' cache policy
-#define RG_LAG_ST_AUX kAuxNT
-#endif
+constexpr int kAuxNT = 2;  // non-temporal (read or written once; default policy measured slower)
 
 template <int W>
 __device__ __forceinline__ void buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, uint32_t (&v)[W]) {
   if constexpr (W == 4) {
-    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, RG_LAG_LD_AUX);
+    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, kAuxNT);
     v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
   } else if constexpr (W == 2) {
-    const u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, RG_LAG_LD_AUX);
+    const u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, kAuxNT);
     v[0] = x.x; v[1] = x.y;
   } else {
-    v[0] = __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, RG_LAG_LD_AUX);
+    v[0] = __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, kAuxNT);
   }
 }
 template <int W>
@@ -1201,13 +1195,13 @@ __device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, uint32_t voff, 
   if constexpr (W == 4) {
     u32x4 x;
     x.x = v[0]; x.y = v[1]; x.z = v[2]; x.w = v[3];
-    __builtin_amdgcn_raw_buffer_store_b128(x, r, voff, soff, RG_LAG_ST_AUX);
+    __builtin_amdgcn_raw_buffer_store_b128(x, r, voff, soff, kAuxNT);
   } else if constexpr (W == 2) {
     u32x2 x;
     x.x = v[0]; x.y = v[1];
-    __builtin_amdgcn_raw_buffer_store_b64(x, r, voff, soff, RG_LAG_ST_AUX);
+    __builtin_amdgcn_raw_buffer_store_b64(x, r, voff, soff, kAuxNT);
   } else {
-    __builtin_amdgcn_raw_buffer_store_b32(v[0], r, voff, soff, RG_LAG_ST_AUX);
+    __builtin_amdgcn_raw_buffer_store_b32(v[0], r, voff, soff, kAuxNT);
   }
 }
 // 2N vote planes starting at plane `first` (lo, hi per replica lane)
@@ -1240,12 +1234,112 @@ __device__ __forceinline__ uint32_t take_ticket(Record* rec) {
   return atomicAdd(reinterpret_cast<unsigned int*>(&rec->ticket.v) + zero, 1u);
 }
 
-template <int N, int W, int BLOCK, bool SHARD, int OCC = 4>
+// Where a ticket's tile lives: window w of a multi-window launch, tile c inside it.
+struct TileLoc {
+  uint32_t w, c;
+};
+
+// Multi-window lag launch: the last workgroup folds the per-tile granules (finish_tile's
+// format, tile-relative offsets) window by window, one wave per window, and writes each
+// window's shard row (the kFinShard row of step_commit: VQ slots left to the fix-up, every
+// window drawn from the same provisional position, shard_draws left alone).
+template <int WAVES, uint32_t kTileSlots>
+__device__ __forceinline__ void lag_fold_windows(const StepParams& p, Record* rec, int lane, int wave) {
+  constexpr int kB = 4;  // tiles per lane with their loads in flight together
+  constexpr unsigned long long kTagMask = ~0ull << 51;
+  const unsigned long long tag = stat_tag(p.seq);
+  const unsigned long long err0 = atomicAdd(&rec->error.v, 0ull);
+  for (uint32_t w = (uint32_t)wave; w < p.n_win; w += WAVES) {
+    const unsigned long long* st = p.stats + (uint64_t)w * p.n_tiles * kStatGranules;
+    const unsigned long long sbase = p.slot_base + (unsigned long long)w * p.win_id_stride;
+    unsigned long long v[7] = {0, 0, 0, 0, 0, ~0ull, 0};  // dec v1 pend draws max(id+1) min(id) fault
+    for (uint32_t i0 = (uint32_t)lane; i0 < p.n_tiles; i0 += 64 * kB) {
+      unsigned long long g[kB][2];
+#pragma unroll
+      for (int k = 0; k < kB; k++) {
+        const uint32_t i = i0 + 64u * k;
+        unsigned long long* gp = const_cast<unsigned long long*>(st) + (uint64_t)i * kStatGranules;
+        g[k][0] = i < p.n_tiles ? atomic_load_agent(gp) : tag;
+        g[k][1] = i < p.n_tiles ? atomic_load_agent(gp + 1) : tag;
+      }
+      SpinBound spin;
+      for (;;) {  // visible already (arrival counter): a guard, not a wait
+        bool ready = true;
+#pragma unroll
+        for (int k = 0; k < kB; k++) ready &= ((g[k][0] & kTagMask) == tag) & ((g[k][1] & kTagMask) == tag);
+        if (ready) break;
+        if (spin.expired()) { v[6] = 2; break; }
+        __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+        for (int k = 0; k < kB; k++) {
+          unsigned long long* gp = const_cast<unsigned long long*>(st) + (uint64_t)(i0 + 64u * k) * kStatGranules;
+          if ((g[k][0] & kTagMask) != tag) g[k][0] = atomic_load_agent(gp);
+          if ((g[k][1] & kTagMask) != tag) g[k][1] = atomic_load_agent(gp + 1);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kB; k++) {
+        const uint32_t i = i0 + 64u * k;
+        if (i >= p.n_tiles) continue;
+        const uint32_t dec = (uint32_t)(g[k][0] & kStatNone), v1 = (uint32_t)((g[k][0] >> 17) & kStatNone);
+        const uint32_t pend = (uint32_t)((g[k][0] >> 34) & kStatNone);
+        const uint32_t draws = (uint32_t)(g[k][1] & kStatNone), mx = (uint32_t)((g[k][1] >> 17) & kStatNone);
+        const uint32_t mn = (uint32_t)((g[k][1] >> 34) & kStatNone);
+        const unsigned long long tb = sbase + (unsigned long long)i * kTileSlots;
+        v[0] += dec; v[1] += v1; v[2] += pend; v[3] += draws;
+        if (mx && tb + mx > v[4]) v[4] = tb + mx;
+        if (mn != kStatNone && tb + mn < v[5]) v[5] = tb + mn;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) v[k] = wave_sum64(v[k]);
+    v[4] = wave_max64(v[4]);
+    v[5] = wave_min64(v[5]);
+    v[6] = wave_max64(v[6]);
+    if (lane == 0) {
+      DevResult r;
+      r.n_slots = p.n_slots;
+      r.n_decided = v[0];
+      r.n_v1 = v[1];
+      r.n_pending_r1 = v[2];
+      r.n_draws = v[3];
+      const unsigned long long end = sbase + p.n_slots;
+      r.last_committed_max = v[4] ? v[4] - 1 : 0;
+      r.first_undecided = v[5] < end ? v[5] : end;
+      r.rng_next = p.state->shard_draws + r.n_draws;
+      r.commit_watermark = 0;
+      r.flags = err0 | v[6];
+      p.result_user[w] = r;
+      if (w + 1 == p.n_win && p.result) *p.result = r;
+    }
+  }
+}
+
+// MW = the multi-window sharded launch (rg_phase_step_shard_windows_async, SHARD only):
+// tickets run window-major over n_win windows of n_tiles tiles each (ticket t = window
+// t / n_tiles, tile t % n_tiles), so the grid streams through the K windows as through
+// one long launch and pays the ramp and drain once. Each window keeps its own look-back
+// chain (its tile 0 publishes an inclusive prefix; a look-back never reads below its
+// window's first ticket), its own draw records and its own row. The statistics are per
+// tile (two tagged granules, as the tiled kernel's), published one iteration after the
+// tile's stores by wave 0, and the last workgroup to arrive folds them window by window
+// (one wave per window).
+template <int N, int W, int BLOCK, bool SHARD, int OCC = 4, bool MW = false>
 __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  // OCC waves/SIMD: 2 x 512 or 1 x 1024 per CU
+  static_assert(!MW || SHARD, "multi-window lag launches are sharded launches");
   constexpr int B = ctr_bits(N);
   constexpr int WAVES = BLOCK / 64;
   constexpr int kRows = BLOCK / 4;  // ChaCha12 blocks per pass, one per quad of lanes
   constexpr uint32_t kTW = (uint32_t)BLOCK * W;  // words per tile
+  const uint32_t n_tix = MW ? p.n_tiles * p.n_win : p.n_tiles;  // tickets of the launch
+  auto loc_of = [&](uint32_t t) -> TileLoc {
+    if constexpr (MW) {
+      const uint32_t w = t / p.n_tiles;
+      return {w, t - w * p.n_tiles};
+    } else {
+      return {0u, t};
+    }
+  };
   __shared__ __attribute__((aligned(16))) uint32_t s_park[2][kParkFields][BLOCK][W];
   __shared__ uint32_t s_blk[kRows][17];  // ChaCha12 blocks of the parked tile's draws (+1 word: no conflicts)
   // Broadcast slots written before a barrier and read after it are double-buffered by
@@ -1283,72 +1377,78 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
   const uint32_t in_lane = (uint32_t)p.lin.base((uint64_t)tid * W) * 4u;
   const uint32_t out_lane = (uint32_t)p.lout.base((uint64_t)tid * W) * 4u;
   uint32_t in_pb = (uint32_t)p.lin.pstride * 4u, out_pb = (uint32_t)p.lout.pstride * 4u;
-  auto in_rsrc = [&](uint32_t t) { return plane_rsrc(p.votes + p.lin.base((uint64_t)t * kTW)); };
-  auto out_rsrc = [&](uint32_t t) { return plane_rsrc(p.out + p.lout.base((uint64_t)t * kTW)); };
-  auto active = [&](uint32_t t) { return (uint64_t)t * kTW + (uint64_t)tid * W < p.n_words; };
+  // (MW: window l.w's planes start l.w pitches after window 0's)
+  auto in_rsrc = [&](TileLoc l) {
+    return plane_rsrc(p.votes + (MW ? (uint64_t)l.w * p.win_in_pitch : 0ull) + p.lin.base((uint64_t)l.c * kTW));
+  };
+  auto out_rsrc = [&](TileLoc l) {
+    return plane_rsrc(p.out + (MW ? (uint64_t)l.w * p.win_out_pitch : 0ull) + p.lout.base((uint64_t)l.c * kTW));
+  };
+  auto active = [&](TileLoc l) { return (uint64_t)l.c * kTW + (uint64_t)tid * W < p.n_words; };
   // a thread past the window loads its tile's first word (valid; its masks are 0)
   // and its stores go out of range (dropped)
-  auto in_off = [&](uint32_t t) { return active(t) ? in_lane : 0u; };
-  auto out_off = [&](uint32_t t) { return active(t) ? out_lane : kOffNone; };
-#ifdef RG_LAG_CHECK  // experiment build: report (printf) the first out-of-extent access of a launch
-  // returns the offset to use: a bad one is reported and replaced (0 for loads,
-  // out of range for stores), so the checked build never faults
-  auto chk = [&](const char* what, uint64_t base_words, uint32_t voff, uint32_t soff, uint64_t extent,
-                 uint32_t safe) -> uint32_t {
-    if (voff == kOffNone) return voff;
-    const uint64_t end = base_words * 4 + voff + soff + 4 * W;
-    if (end <= extent) return voff;
-    if (atomicOr(&rec->error.v, 64ull) == 0)
-      printf("RG_LAG_CHECK %s: tile base %llu words, voff %u, soff %u, end %llu > extent %llu (tid %d)\n", what,
-             (unsigned long long)base_words, voff, soff, (unsigned long long)end, (unsigned long long)extent, tid);
-    return safe;
-  };
-#define LAG_CHK_IN(t, voff, first) \
-  voff = chk("load", p.lin.base((uint64_t)(t) * kTW), voff, (uint32_t)((first) + 2 * N - 1) * in_pb, p.in_bytes, 0u)
-#define LAG_CHK_OUT(t, voff, plane) \
-  voff = chk("store", p.lout.base((uint64_t)(t) * kTW), voff, (plane) * out_pb, p.out_bytes, kOffNone)
-#else
-#define LAG_CHK_IN(t, voff, first) ((void)0)
-#define LAG_CHK_OUT(t, voff, plane) ((void)0)
-#endif
-
+  auto in_off = [&](TileLoc l) { return active(l) ? in_lane : 0u; };
+  auto out_off = [&](TileLoc l) { return active(l) ? out_lane : kOffNone; };
   // tickets: c = the tile being tallied (its round-1 planes were loaded during the
   // previous iteration); the ticket after it is requested one iteration ahead
   uint32_t nt = 0;
   if (tid == 0) s_bcast[1][0] = take_ticket(rec);
   lds_barrier();
   uint32_t c = s_bcast[1][0];
+  TileLoc cl = loc_of(c < n_tix ? c : 0u);
   if (tid == 0) nt = take_ticket(rec);
   uint32_t r1lo[N][W], r1hi[N][W];
   unsigned long long lbg;  // the look-back poll of the tile parked next (issued before its successor's loads)
 
-  int32_t prev_tile = -1;   // this workgroup's last finished tile and its inclusive prefix
+  int32_t prev_tile = -1;   // this workgroup's last finished tile (ticket) and its inclusive prefix
   uint32_t prev_incl = 0;
-  int32_t park_tile = -1;   // the parked tile, its VQ total and this thread's offset in it
+  int32_t park_tile = -1;   // the parked tile (ticket), its VQ total and this thread's offset in it
+  TileLoc park_l{0u, 0u};
   uint32_t park_total = 0, park_thr = 0;
   uint32_t pk = 0;          // park buffer of the tile being tallied (the parked tile: pk ^ 1)
   uint32_t a_dec = 0, a_v1 = 0, a_pend = 0, a_draws = 0, a_max1 = 0, a_min = ~0u;  // launch-relative offsets
+  // MW: per-tile statistics, one row per wave {dec | v1 << 16, pend, max_off1, min_off} of the
+  // tile stored last (by parity), published by wave 0 after the next barrier
+  __shared__ uint32_t s_tst[MW ? 2 : 1][MW ? WAVES : 1][4];
+  int32_t st_tile = -1;     // the tile whose statistics wait for publication, its draws
+  uint32_t st_draws = 0;
 
   // ---- look-back of the parked tile p: every wave polls 64 predecessor granules
   // (wave w: distances 64w .. 64w + 63 below p; one load per lane, so every wave
   // issues the same memory operations) with the round-1 planes' wait, evaluates them
   // after the tally, and the waves' results combine after the scan barrier.
+  // The look-back floor: granules at or below it are known (synthetic). Single window:
+  // this workgroup's last finished tile (inclusive). MW: the same if it lies in the
+  // parked tile's window, else the ticket before the window's first (a prefix of 0).
   constexpr int kPollWaves = WAVES < 8 ? WAVES : 8;  // 512 granules per poll (waves 8-15 repeat 0-7)
+  auto lb_floor = [&]() -> int32_t {
+    if constexpr (MW) {
+      const int32_t ws = park_tile - (int32_t)park_l.c;
+      return prev_tile >= ws ? prev_tile : ws - 1;
+    } else {
+      return prev_tile;
+    }
+  };
+  auto lb_floor_incl = [&]() -> uint32_t {
+    if constexpr (MW) return prev_tile >= park_tile - (int32_t)park_l.c ? prev_incl : 0u;
+    else return prev_incl;
+  };
   auto lb_poll = [&](int32_t tile) -> unsigned long long {
     const int32_t idx = tile - 1 - (64 * (wave % kPollWaves) + lane);
-    return atomic_load_agent(p.lookback + (idx > prev_tile ? idx : 0));
+    return atomic_load_agent(p.lookback + (idx > lb_floor() ? idx : 0));
   };
   auto lb_eval = [&](unsigned long long g) {
     if (wave >= kPollWaves) return;
+    const int32_t floor = lb_floor();
     const int32_t idx = park_tile - 1 - (64 * wave + lane);
     const uint32_t tag = (uint32_t)(g >> 32);
-    const bool synth = idx <= prev_tile;  // prev_tile is inclusive (this WG computed it)
+    const bool synth = idx <= floor;  // the floor is inclusive (known to this WG)
     const bool ready = synth || (tag >> 1) == p.seq;
     const bool incl = synth || (ready && (tag & 1u));
     const unsigned long long im = __ballot(incl), nr = __ballot(!ready);
     const int f = im ? __builtin_ctzll(im) : 64;
     const unsigned long long need = f >= 63 ? ~0ull : ((2ull << f) - 1ull);
-    const uint32_t val = idx == prev_tile ? prev_incl : (synth ? 0u : (uint32_t)g);
+    const uint32_t val = idx == floor ? lb_floor_incl() : (synth ? 0u : (uint32_t)g);
     const uint32_t sum = wave_sum32(lane <= f ? val : 0u);
     if (lane == 0)
       s_lb[pk][wave] = (unsigned long long)sum | ((unsigned long long)(f < 64) << 32) |
@@ -1391,8 +1491,8 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
     const bool lb_done = lb_combine(excl);
     if (!lb_done) {  // uniform: the rare continued look-back (wave 0, 256 granules per poll)
       if (wave == 0) {
-        const uint32_t e = lag_finish(p.lookback, park_tile - 1 + 64 * kLagPoll, prev_tile, prev_incl, p.seq, lane,
-                                      0u, false, &rec->error.v);
+        const uint32_t e = lag_finish(p.lookback, park_tile - 1 + 64 * kLagPoll, lb_floor(), lb_floor_incl(), p.seq,
+                                      lane, 0u, false, &rec->error.v);
         if (lane == 0) s_bcast[pk][1] = e;
       }
       lds_barrier();
@@ -1405,6 +1505,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
     prev_tile = park_tile;
     prev_incl = excl + park_total;
     const unsigned long long k_tile = k_base + excl;
+    unsigned long long* const vq_rec = p.vq_rec + (MW ? (uint64_t)park_l.w * p.vq_cap : 0ull);
     // VQ slots whose draw gave V1 (engine.rs:523-537, 567-611)
 #pragma unroll
     for (int i = 0; i < W; i++) own[i] = 0;
@@ -1434,12 +1535,10 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
           // own vote, the provisional own vote (built in a loop of its own: 765 vs 697 us
           // per 2^30 slots against no records at all)
           uint32_t dv[4] = {0u, 0u, 0u, 0u};
-#ifndef RG_SHARD_NOREC  // experiment build: the SHARD kernel without its records (wrong fix-up)
           if constexpr (SHARD) {
 #pragma unroll
             for (int j = 0; j < 4; j++) dv[j] = pp[4 + j][tid][i];
           }
-#endif
           while (mq[i] && k < k_lim) {
             const int b = __builtin_ctz(mq[i]);
             mq[i] &= mq[i] - 1;
@@ -1449,17 +1548,15 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
             const bool x0 = (e0 >> b) & 1u, x1 = (e1 >> b) & 1u;  // gt: 1/0, lt: 0/1, tie: 1/1
             const bool v1 = (x0 && !x1) ? (u < kP90) : ((x1 && !x0) ? (u >= kP90) : (u < kP80));
             own[i] |= (uint32_t)v1 << b;
-#ifndef RG_SHARD_NOREC
             if constexpr (SHARD) {
               const uint32_t cls = (x0 && !x1) ? kRecGt : ((x1 && !x0) ? kRecLt : 0u);
               const uint32_t d4 = ((dv[0] >> b) & 1u) | (((dv[1] >> b) & 1u) << 1) | (((dv[2] >> b) & 1u) << 2) |
                                   (((dv[3] >> b) & 1u) << 3);
               const uint32_t info = cls | (d4 << 2) | ((uint32_t)v1 << 6);
               const unsigned long long kr = k - k_base;
-              const uint32_t off = 32u * ((uint32_t)park_tile * kTW + (uint32_t)tid * W + i) + b;
-              if (kr < p.vq_cap) p.vq_rec[kr] = ((unsigned long long)info << 32) | off;
+              const uint32_t off = 32u * (park_l.c * kTW + (uint32_t)tid * W + i) + b;  // window-relative
+              if (kr < p.vq_cap) vq_rec[kr] = ((unsigned long long)info << 32) | off;
             }
-#endif
             k++;
           }
         }
@@ -1480,11 +1577,10 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
   // same memory operations in flight behind the round-1 loads.
   auto store_parked = [&](const uint32_t (&own)[W], bool have_park) {
     uint32_t(&pp)[kParkFields][BLOCK][W] = s_park[pk ^ 1u];
-    const uint32_t pt = have_park ? (uint32_t)park_tile : 0u;
-    const uint32_t pw0 = pt * kTW + (uint32_t)tid * W;
-    const __amdgpu_buffer_rsrc_t orr = out_rsrc(pt);
-    uint32_t oo = have_park ? out_off(pt) : kOffNone;
-    LAG_CHK_OUT(pt, oo, 7);
+    const TileLoc pl = have_park ? park_l : TileLoc{0u, 0u};
+    const uint32_t pw0 = pl.c * kTW + (uint32_t)tid * W;  // window-relative word of this thread
+    const __amdgpu_buffer_rsrc_t orr = out_rsrc(pl);
+    const uint32_t oo = have_park ? out_off(pl) : kOffNone;
     {  // plane 2: own round-2 vote lo
       uint32_t v[W];
       lds_ld<W>(pp[0][tid], v);
@@ -1517,7 +1613,10 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
 #pragma unroll
       for (int i = 0; i < W; i++) keep[i] &= ~(e0[i] | e1[i]);
     }
-    const uint32_t toff = 32u * pw0;  // launch-relative slot offset of this thread's first word
+    // slot offset of this thread's first word: launch-relative (one window), tile-relative (MW)
+    const uint32_t toff = 32u * (MW ? (uint32_t)tid * W : pw0);
+    const uint64_t sbase = MW ? p.slot_base + (uint64_t)pl.w * p.win_id_stride : p.slot_base;
+    uint32_t t_dec = 0, t_v1 = 0, t_max1 = 0, t_min = ~0u;
 #pragma unroll
     for (int i = 0; i < W; i++) {
       const uint32_t vm = valid_mask(pw0 + i, p.n_words, p.n_slots);
@@ -1526,17 +1625,74 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
       dlo[i] = pdec;
       dhi[i] = pv1;
       const uint32_t cd = pdec & keep[i], c1 = pv1 & keep[i];
-      a_dec += __builtin_popcount(cd);
-      a_v1 += __builtin_popcount(c1);
-      const uint32_t m1 = c1 & phase_limit_mask(p.slot_base, pw0 + i, p.max_phase);
+      t_dec += __builtin_popcount(cd);
+      t_v1 += __builtin_popcount(c1);
+      const uint32_t m1 = c1 & phase_limit_mask(sbase, pw0 + i, p.max_phase);
       const uint32_t o1 = m1 ? toff + 32u * i + (31u - __builtin_clz(m1)) + 1u : 0u;
-      a_max1 = o1 > a_max1 ? o1 : a_max1;
+      t_max1 = o1 > t_max1 ? o1 : t_max1;
       const uint32_t und = ~pdec & vm & keep[i];
       const uint32_t o0 = und ? toff + 32u * i + __builtin_ctz(und) : ~0u;
-      a_min = o0 < a_min ? o0 : a_min;
+      t_min = o0 < t_min ? o0 : t_min;
     }
     buf_st<W>(orr, oo, 6 * out_pb, dlo);
     buf_st<W>(orr, oo, 7 * out_pb, dhi);
+    if constexpr (MW) {
+      // the tile's row per wave: sums by DPP, the extremes from the highest / lowest lane
+      // holding one (threads own ascending words of the tile); pend recounted from the
+      // parked pending plane (the tally counted it into no accumulator)
+      if (have_park) {
+        uint32_t pd[W], t_pend = 0;
+        lds_ld<W>(pp[1][tid], pd);
+#pragma unroll
+        for (int i = 0; i < W; i++) t_pend += __builtin_popcount(pd[i]);
+        const uint32_t s0 = wave_sum32(t_dec | (t_v1 << 16)), s1 = wave_sum32(t_pend);
+        const unsigned long long hmx = __ballot(t_max1 != 0u), hmn = __ballot(t_min != ~0u);
+        const uint32_t mx = hmx ? __builtin_amdgcn_readlane(t_max1, 63 - __builtin_clzll(hmx)) : 0u;
+        const uint32_t mn = hmn ? __builtin_amdgcn_readlane(t_min, __builtin_ctzll(hmn)) : ~0u;
+        if (lane == 0) {
+          s_tst[pk][wave][0] = s0;
+          s_tst[pk][wave][1] = s1;
+          s_tst[pk][wave][2] = mx;
+          s_tst[pk][wave][3] = mn;
+        }
+        st_tile = park_tile;
+        st_draws = park_total;
+      }
+    } else {
+      a_dec += t_dec;
+      a_v1 += t_v1;
+      a_max1 = t_max1 > a_max1 ? t_max1 : a_max1;
+      a_min = t_min < a_min ? t_min : a_min;
+    }
+  };
+
+  // MW: wave 0 publishes the statistics of tile st_tile from row buffer `buf` (after a
+  // barrier that follows their writes) as the two tagged granules of finish_tile.
+  auto publish_tile_stats = [&](uint32_t buf) {
+    if constexpr (MW) {
+      if (wave != 0 || st_tile < 0) return;
+      const bool have = lane < WAVES;
+      uint32_t x0 = 0, x1 = 0, mx = 0, mn = ~0u;
+      if (have) {
+        x0 = s_tst[buf][lane][0];
+        x1 = s_tst[buf][lane][1];
+        mx = s_tst[buf][lane][2];
+        mn = s_tst[buf][lane][3];
+      }
+      const uint32_t dec_v1_lo = wave_sum32(x0 & 0xFFFFu), v1 = wave_sum32(x0 >> 16), pend = wave_sum32(x1);
+      const unsigned long long hmx = __ballot(mx != 0u), hmn = __ballot(mn != ~0u);
+      const uint32_t bmx = hmx ? __builtin_amdgcn_readlane(mx, 63 - __builtin_clzll(hmx)) : 0u;
+      const uint32_t bmn = hmn ? __builtin_amdgcn_readlane(mn, __builtin_ctzll(hmn)) : kStatNone;
+      if (lane == 0) {
+        const unsigned long long tag = stat_tag(p.seq);
+        unsigned long long* g = p.stats + (uint64_t)st_tile * kStatGranules;
+        atomic_store_agent(g + 0, tag | ((unsigned long long)pend << 34) | ((unsigned long long)v1 << 17) | dec_v1_lo);
+        atomic_store_agent(g + 1, tag | ((unsigned long long)bmn << 34) | ((unsigned long long)bmx << 17) | st_draws);
+      }
+      st_tile = -1;
+    } else {
+      (void)buf;
+    }
   };
 
   // Software pipeline. Tile c's round-1 planes (r1) were issued right after the
@@ -1550,19 +1706,18 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
   //   | draws + stores of the parked tile | poll for c
   uint32_t r2lo[N][W], r2hi[N][W];
   {  // in the order the loop leaves them: r1, r2, five stores (here out of range), poll
-    const bool any = c < p.n_tiles;
-    uint32_t voff0 = any ? in_off(c) : 0u;
-    LAG_CHK_IN(any ? c : 0u, voff0, 2 * N);
-    buf_ld_planes<N, W>(in_rsrc(any ? c : 0u), voff0, in_pb, 0, r1lo, r1hi);
-    buf_ld_planes<N, W>(in_rsrc(any ? c : 0u), voff0, in_pb, 2 * N, r2lo, r2hi);
+    const bool any = c < n_tix;  // (cl: the tile of c, or tile 0 without one)
+    const uint32_t voff0 = any ? in_off(cl) : 0u;
+    buf_ld_planes<N, W>(in_rsrc(cl), voff0, in_pb, 0, r1lo, r1hi);
+    buf_ld_planes<N, W>(in_rsrc(cl), voff0, in_pb, 2 * N, r2lo, r2hi);
     const uint32_t z[W] = {};
-    const __amdgpu_buffer_rsrc_t orr = out_rsrc(0u);
+    const __amdgpu_buffer_rsrc_t orr = out_rsrc(TileLoc{0u, 0u});
 #pragma unroll
     for (int k = 0; k < 5; k++) buf_st<W>(orr, kOffNone, (uint32_t)k * 4u, z);
     lbg = lb_poll(park_tile);  // no parked tile yet: a harmless poll
   }
   lap(0);
-  while (c < p.n_tiles) {
+  while (c < n_tix) {
     // opaque per iteration: the 28 plane offsets (k * stride) are recomputed by SALU
     // next to their loads and stores instead of living in SGPRs across the loop
     asm volatile("" : "+s"(in_pb), "+s"(out_pb));
@@ -1570,7 +1725,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
     uint32_t(&pc)[kParkFields][BLOCK][W] = s_park[pk];
     // (1) round 1 of tile c: count_votes + |votes| >= quorum fallback (engine.rs:495-505);
     //     the round-1-only output planes (final already) and the tile's state to LDS
-    const uint32_t w0 = c * kTW + (uint32_t)tid * W;
+    const uint32_t w0 = cl.c * kTW + (uint32_t)tid * W;  // window-relative
     uint32_t vq_count = 0;
     {
       uint32_t v1[W], vq[W], pd[W], e0[W], e1[W];
@@ -1608,9 +1763,8 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
       lds_st<W>(pc[1][tid], pd);
       lds_st<W>(pc[2][tid], e0);
       lds_st<W>(pc[3][tid], e1);
-      const __amdgpu_buffer_rsrc_t orr = out_rsrc(c);
-      uint32_t oo = out_off(c);
-      LAG_CHK_OUT(c, oo, 3);
+      const __amdgpu_buffer_rsrc_t orr = out_rsrc(cl);
+      const uint32_t oo = out_off(cl);
       buf_st<W>(orr, oo, 0, x);
 #pragma unroll
       for (int i = 0; i < W; i++) x[i] = vq[i] | pd[i];
@@ -1637,16 +1791,17 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
     }
     const uint32_t nx = s_bcast[pk][0];
     lap(2);
-    if (tid == 0) {
-      atomic_store_agent(p.lookback + c, ((unsigned long long)(c == 0 ? tag_inc : tag_agg) << 32) | total);
-      if (nx < p.n_tiles) nt = take_ticket(rec);
+    if (tid == 0) {  // (a window's first tile starts its chain: inclusive)
+      atomic_store_agent(p.lookback + c, ((unsigned long long)(cl.c == 0 ? tag_inc : tag_agg) << 32) | total);
+      if (nx < n_tix) nt = take_ticket(rec);
     }
+    publish_tile_stats(pk ^ 1u);  // MW: the tile stored in the last iteration
 
     // (3) the next tile's round-1 planes in flight (past the last tile: tile c's first word)
-    const bool more = nx < p.n_tiles;
-    const __amdgpu_buffer_rsrc_t nrr = in_rsrc(more ? nx : c);
-    uint32_t noff = more ? in_off(nx) : 0u;
-    LAG_CHK_IN(more ? nx : c, noff, 2 * N);
+    const bool more = nx < n_tix;
+    const TileLoc nl = more ? loc_of(nx) : cl;
+    const __amdgpu_buffer_rsrc_t nrr = in_rsrc(nl);
+    const uint32_t noff = more ? in_off(nl) : 0u;
     buf_ld_planes<N, W>(nrr, noff, in_pb, 0, r1lo, r1hi);
     // (4) round-2 decisions of tile c for both own votes (engine.rs:540-542, 613-628);
     //     then the next tile's round-2 planes in flight
@@ -1680,19 +1835,49 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
     if (stamps) s_st[7]++;
     a_draws += vq_count;
     park_tile = (int32_t)c;  // tile c is parked; its look-back poll (prev_tile: the tile just finished)
+    park_l = cl;
     park_total = total;
     park_thr = wave_off + incl - vq_count;
     lbg = lb_poll(park_tile);  // (issued ahead of the next round-2 loads instead: 877 vs 705 us per 2^30
                                // slots, its predecessors not yet published: continued look-backs)
     pk ^= 1u;
     c = nx;
+    cl = nl;
   }
   if (park_tile >= 0) {  // the last parked tile (its poll went out in the last iteration)
     lb_eval(lbg);
     lds_barrier();
+    publish_tile_stats(pk ^ 1u);  // MW: the tile stored in the last iteration
     uint32_t own[W];
     draw_parked(own);
     store_parked(own, true);
+    if constexpr (MW) {
+      lds_barrier();
+      publish_tile_stats(pk);
+    }
+  }
+
+  if constexpr (MW) {  // arrival; the last workgroup folds every window's tile granules
+    __shared__ uint32_t s_last_mw;
+    if (stamps) {
+      lap(6);
+      for (int k = 0; k < 10; k++) p.dbg[(uint64_t)blockIdx.x * 16 + k] = s_st[k];
+    }
+    if (tid == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's granules are out
+      const unsigned long long arrived = atomicAdd(&rec->done.v, 1ull);
+      s_last_mw = arrived == gridDim.x - 1 ? 1u : 0u;
+    }
+    lds_barrier();
+    if (!s_last_mw) return;
+    lag_fold_windows<WAVES, kTW * 32u>(p, rec, lane, wave);
+    if (tid == 0) {
+      Record* nxt = p.rec + ((p.seq + 1) & 1u);  // the next launch's record (the previous launch completed)
+      atomic_store_agent(&nxt->error.v, 0ull);
+      atomic_store_agent(&nxt->ticket.v, 0ull);
+      atomic_store_agent(&nxt->done.v, 0ull);
+    }
+    return;
   }
 
   // ---- per-workgroup record; the last workgroup to arrive folds them all
@@ -1860,10 +2045,7 @@ __device__ __forceinline__ unsigned long long fix_first_draw(const FixParams& f,
 // the rare decision changes (the own vote decides the round-2 count). Every lane works
 // on a block of its own, so no lane idles on a partial pass and no LDS is needed; the
 // statistics are one partial per workgroup.
-#ifndef RG_FIX_GRID  // experiment builds: other grids
-#define RG_FIX_GRID 2048
-#endif
-constexpr uint32_t kFixGrid = RG_FIX_GRID;  // fix-up workgroups at most (grid-stride beyond)
+constexpr uint32_t kFixGrid = 2048;  // fix-up workgroups at most (grid-stride beyond)
 static __global__ __launch_bounds__(256) void shard_fixup_kernel(FixParams f) {
   const uint32_t win = blockIdx.y;
   const unsigned long long n = f.rows[(uint64_t)f.shard * f.n_win + win].n_draws;
@@ -1942,163 +2124,6 @@ static __global__ __launch_bounds__(256) void shard_fixup_kernel(FixParams f) {
   if (threadIdx.x < 4) f.acc[((uint64_t)win * f.n_part + blockIdx.x) * 4 + threadIdx.x] = fold4(red, threadIdx.x);
 }
 
-#ifdef RG_FIX_SEGMENT  // experiment build: the per-segment fix-up (round 4, LDS own-vote masks)
-// The fix-up runs per 32,768-slot segment of the window (1,024 words of every plane):
-// pass A finds each segment's first record (records are in ascending slot order),
-// pass B gives one wave per segment. The wave re-draws its records' VQ slots at their
-// global positions (64 ChaCha12 blocks per pass, one per lane, into LDS: up to 505
-// records, one pass for a segment under ~1.5 % VQ slots), counts them into the shard's
-// statistics, collects the own-vote bits that change in an LDS mask of the segment,
-// and rewrites the segment's own-vote plane in one coalesced read-XOR-write stream (an
-// own-vote bit changes for ~25 % of the VQ slots when the position moved, so nearly
-// every line of the plane is touched: per-bit atomics cost a random line
-// read-modify-write each). The rare decision changes (the own vote decides the
-// round-2 count) are atomic XORs. (65,536-slot segments: two passes per segment at
-// the bench's 0.8 % VQ and 3 workgroups per CU (LDS), 151 vs ... us per 2^30 slots.)
-constexpr uint32_t kFixSegShift = 15;                      // 32,768 slots per segment
-constexpr uint32_t kFixSegWords = 1u << (kFixSegShift - 5);  // 1,024 words
-static __global__ __launch_bounds__(256) void shard_fixup_seg_kernel(FixParams f, uint32_t* seg_first,
-                                                                    uint32_t n_seg) {
-  const uint32_t win = blockIdx.y;
-  const unsigned long long n = f.rows[(uint64_t)f.shard * f.n_win + win].n_draws;
-  const unsigned long long nn = n < f.vq_cap ? n : f.vq_cap;
-  const unsigned long long* rec = f.rec + win * f.vq_cap;
-  uint32_t* sf = seg_first + (uint64_t)win * n_seg;
-  // 4 consecutive records per thread, all loads in flight at once (a grid-stride loop
-  // of one record per thread waits out one load latency per record)
-  for (unsigned long long k0 = ((unsigned long long)blockIdx.x * 256 + threadIdx.x) * 4; k0 < nn;
-       k0 += (unsigned long long)gridDim.x * 1024) {
-    uint32_t seg[5];
-    seg[0] = k0 ? (uint32_t)rec[k0 - 1] >> kFixSegShift : ~0u;
-#pragma unroll
-    for (int j = 0; j < 4; j++) seg[j + 1] = k0 + j < nn ? (uint32_t)rec[k0 + j] >> kFixSegShift : ~0u;
-#pragma unroll
-    for (int j = 0; j < 4; j++)
-      if (k0 + j < nn && seg[j + 1] != seg[j] && seg[j + 1] < n_seg) sf[seg[j + 1]] = (uint32_t)(k0 + j) + 1u;  // 0: none
-  }
-}
-
-static __global__ __launch_bounds__(256) void shard_fixup_seg_wave_kernel(FixParams f, const uint32_t* seg_first,
-                                                                uint32_t n_seg) {
-  __shared__ uint32_t s_blk[4][64][17];         // per wave: 64 ChaCha12 blocks (+1 word: no conflicts)
-  __shared__ uint32_t s_m2[4][kFixSegWords];    // per wave: own-vote bits that change in its segment
-  const uint32_t win = blockIdx.y;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const unsigned long long n = f.rows[(uint64_t)f.shard * f.n_win + win].n_draws;
-  const unsigned long long g0 = fix_first_draw(f, win);  // global position of local draw 0
-  if (win) {  // this window's outputs, slot ids, records
-    f.out += win * f.out_pitch;
-    f.slot_base += win * f.id_stride;
-    f.rec += win * f.vq_cap;
-  }
-  const unsigned long long nn = n < f.vq_cap ? n : f.vq_cap;
-  unsigned long long dec = 0, v1 = 0, mx = 0, mn = ~0ull;
-  const uint32_t seg = blockIdx.x * 4 + wave;
-  const uint32_t k1 = seg < n_seg ? seg_first[(uint64_t)win * n_seg + seg] : 0u;
-  if (k1) {  // wave-uniform
-    for (uint32_t i = lane; i < kFixSegWords; i += 64) s_m2[wave][i] = 0u;
-    bool changed = false;
-    const uint64_t seg_w0 = (uint64_t)seg * kFixSegWords;
-    // passes of 64 ChaCha12 blocks (one per lane): the records whose draws they hold
-    // (<= 512, fewer when the first position is not a multiple of 8)
-    for (unsigned long long kb = k1 - 1;;) {
-      const unsigned long long b0 = (g0 + kb) >> 3;
-      const unsigned long long kend = ((b0 + 64) << 3) - g0;  // the first record past this pass's blocks
-      unsigned long long rr[8];  // the pass's records, all loads in flight behind the ChaCha blocks
-#pragma unroll
-      for (int sub = 0; sub < 8; sub++) {
-        const unsigned long long k = kb + 64u * sub + lane;
-        rr[sub] = k < kend && k < nn ? f.rec[k] : ~0ull;
-      }
-      {
-        uint32_t x[16];
-        chacha_block<12>(f.key, b0 + (unsigned long long)lane, 0, x);
-#pragma unroll
-        for (int j = 0; j < 16; j++) s_blk[wave][lane][j] = x[j];
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_wave_barrier();
-      bool seg_done = false;
-#pragma unroll
-      for (int sub = 0; sub < 8; sub++) {
-        if (seg_done) break;
-        const unsigned long long k = kb + 64u * sub + lane;
-        const bool inpass = k < kend;
-        const unsigned long long r = rr[sub];
-        const uint32_t off = (uint32_t)r, info = (uint32_t)(r >> 32);
-        const bool mine = inpass && k < nn && (off >> kFixSegShift) == seg;
-        seg_done = __ballot(inpass && !mine) != 0;  // records are in slot order: the segment ended
-        if (mine) {
-          const unsigned long long g = g0 + k;
-          const uint32_t row = (uint32_t)((g >> 3) - b0), ws = (uint32_t)(g & 7u) * 2u;
-          const unsigned long long u =
-              (unsigned long long)s_blk[wave][row][ws] | ((unsigned long long)s_blk[wave][row][ws + 1] << 32);
-          const uint32_t cls = info & 3u;
-          const uint32_t own = cls == kRecGt ? (u < kP90) : (cls == kRecLt ? (u >= kP90) : (u < kP80));
-          const uint32_t prov = (info >> 6) & 1u;
-          const uint32_t d = own ? (info >> 4) & 3u : (info >> 2) & 3u;
-          const uint32_t dp = prov ? (info >> 4) & 3u : (info >> 2) & 3u;
-          const unsigned long long id = f.slot_base + off;
-          if (d <= kCodeV1) {
-            dec++;
-            if (d == kCodeV1) {
-              v1++;
-              if ((f.max_phase == 0 || id <= f.max_phase) && id + 1 > mx) mx = id + 1;
-            }
-          } else if (id < mn) {
-            mn = id;
-          }
-          if (own != prov) {
-            const uint32_t wl = (off >> 5) & (kFixSegWords - 1u), bit = 1u << (off & 31u);
-            atomicXor(&s_m2[wave][wl], bit);
-            changed = true;
-            const uint32_t dd = d ^ dp;
-            if (dd || (d <= kCodeV1) != (dp <= kCodeV1)) {  // the decision changed: rare
-              const uint64_t base = f.lout.base(off >> 5);
-              if (dd & 1u) atomicXor(f.out + base + 4 * f.lout.pstride, bit);
-              if (dd & 2u) atomicXor(f.out + base + 5 * f.lout.pstride, bit);
-              if ((d <= kCodeV1) != (dp <= kCodeV1)) atomicXor(f.out + base + 6 * f.lout.pstride, bit);
-              if ((d == kCodeV1) != (dp == kCodeV1)) atomicXor(f.out + base + 7 * f.lout.pstride, bit);
-            }
-          }
-        }
-      }
-      if (seg_done) break;
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every lane's block reads done before the next pass writes
-      __builtin_amdgcn_wave_barrier();
-      kb = kend;
-    }
-    if (__ballot(changed)) {  // the segment's own-vote plane: one coalesced read-XOR-write pass
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_wave_barrier();
-      uint32_t* p2 = f.out + 2 * f.lout.pstride;
-#pragma unroll
-      for (uint32_t h = 0; h < kFixSegWords; h += 16 * 64) {  // 16 words per lane in flight at once
-        static_assert(kFixSegWords % (16 * 64) == 0, "whole batches");
-        uint32_t m[16], v[16];
-#pragma unroll
-        for (int j = 0; j < 16; j++) {
-          m[j] = s_m2[wave][h + 64u * j + lane];
-          v[j] = m[j] ? p2[f.lout.base(seg_w0 + h + 64u * j + lane)] : 0u;
-        }
-#pragma unroll
-        for (int j = 0; j < 16; j++)
-          if (m[j]) p2[f.lout.base(seg_w0 + h + 64u * j + lane)] = v[j] ^ m[j];
-      }
-    }
-  }
-  __shared__ unsigned long long red[4][4];
-  dec = wave_sum64(dec);
-  v1 = wave_sum64(v1);
-  mx = wave_max64(mx);
-  mn = wave_min64(mn);
-  if (lane == 0) { red[wave][0] = dec; red[wave][1] = v1; red[wave][2] = mx; red[wave][3] = mn; }
-  __syncthreads();
-  // every workgroup writes its partial (zeros / all ones when it had no records)
-  if (threadIdx.x < 4) f.acc[((uint64_t)win * f.n_part + blockIdx.x) * 4 + threadIdx.x] = fold4(red, threadIdx.x);
-}
-
-#endif  // RG_FIX_SEGMENT
 
 // The shard's final row: VQ-slot counts and extremes folded in, the engine's
 // stream position advanced past the whole window's draws (every shard's).

@@ -447,7 +447,7 @@ struct BatchView {
   const uint8_t* data;
   const KvOp* ops;
   const uint32_t* skey;   // sorted hash buckets
-  const uint32_t* sidx;   // command index per sorted position
+  const uint32_t* sidx;   // command index per sorted position (0xFFFFFFFF in the not-applied tail)
   uint64_t n;
   uint8_t* results;
   uint8_t* done;          // per sorted position: handled by an earlier key of its run (multi-key runs)
@@ -1303,8 +1303,12 @@ __global__ __launch_bounds__(kL2Block) void kv_l2_sort_kernel(SortArgs a) {
   // the sorted tail: commands that are not applied (the plan's walks stop there)
   uint32_t* const fin_key = (a.passes2 & 1u) ? a.a_key : a.b_key;
   uint32_t* const fin_idx = (a.passes2 & 1u) ? a.a_idx : a.b_idx;
-  for (uint64_t i = n_app + (uint64_t)blockIdx.x * kL2Block + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * kL2Block)
+  // (the tail's command index is a sentinel, never a stale index of an earlier batch: readers
+  // stop at the invalid bucket, and one that did not would index out of range loudly)
+  for (uint64_t i = n_app + (uint64_t)blockIdx.x * kL2Block + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * kL2Block) {
     fin_key[i] = a.invalid_bucket;
+    fin_idx[i] = 0xFFFFFFFFu;
+  }
   const uint32_t cnt = hi - lo;
   if (a.passes2 == 0 || cnt <= 1) {
     if (cnt == 1 && (a.passes2 & 1u) && threadIdx.x == 0) {  // a single command: just move it

@@ -12,12 +12,16 @@ void launch_n(int block, int words, uint32_t grid, hipStream_t s, const StepPara
   const dim3 g(grid, p.n_win > 1 ? p.n_win : 1);  // grid.y: windows of a multi-window launch (tiled kernel)
   constexpr int WM = N <= 5 ? 4 : (N <= 10 ? 2 : 1);
   if (block <= 0) {  // the lag kernel (n <= 10, step_impl): -1 one WG per CU (2048-word tiles at n <= 5 as
-                     // 512 x 4, 1024-word tiles at n > 5 as 1024 x 1), 0 two 512-thread WGs per CU
+                     // 512 x 4, 1024-word tiles at n > 5 as 1024 x 1), 0 two 512-thread WGs per CU,
+                     // -2 the one-WG-per-CU shape over the tickets of every window (multi-window launch)
     if constexpr (N <= 5) {
-      if (block < 0) hipLaunchKernelGGL((ref_lag_kernel<N, 4, 512, true, 2>), dim3(grid), dim3(512), 0, s, p);
+      if (block == -2) hipLaunchKernelGGL((ref_lag_kernel<N, 4, 512, true, 2, true>), dim3(grid), dim3(512), 0, s, p);
+      else if (block < 0) hipLaunchKernelGGL((ref_lag_kernel<N, 4, 512, true, 2>), dim3(grid), dim3(512), 0, s, p);
       else hipLaunchKernelGGL((ref_lag_kernel<N, 2, 512, true>), dim3(grid), dim3(512), 0, s, p);
     } else if constexpr (N <= 10) {
-      if (block < 0) hipLaunchKernelGGL((ref_lag_kernel<N, 1, 1024, true>), dim3(grid), dim3(1024), 0, s, p);
+      if (block == -2)
+        hipLaunchKernelGGL((ref_lag_kernel<N, 1, 1024, true, 4, true>), dim3(grid), dim3(1024), 0, s, p);
+      else if (block < 0) hipLaunchKernelGGL((ref_lag_kernel<N, 1, 1024, true>), dim3(grid), dim3(1024), 0, s, p);
       else hipLaunchKernelGGL((ref_lag_kernel<N, 1, 512, true>), dim3(grid), dim3(512), 0, s, p);
     }
   } else if (block == 512) hipLaunchKernelGGL((ref_step_kernel<N, WM, 512, true>), g, dim3(512), 0, s, p);

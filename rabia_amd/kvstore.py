@@ -163,7 +163,10 @@ class DeviceKVStore:
                          r.data_ptr(), None)
         self.sync()
         st = self.stats()
-        if st["flags"] & 4:  # a fault inside a commit pass, this batch's or an earlier one (include/rabia_kv.h)
+        if st["flags"] & 4:  # a fault inside a commit pass (include/rabia_kv.h): sticky, later batches refused
+            if flags0 & 4:
+                raise N.RabiaGpuError(N.RG_ESTATE, f"kvstore lost by an earlier faulted batch (flags {st['flags']}): "
+                                                   f"this batch of {n} commands was refused and wrote nothing")
             raise N.RabiaGpuError(N.RG_ESTATE, f"kvstore capacity fault during the commit (flags {st['flags']}): "
                                                f"the batch of {n} commands is partially written; the store is lost")
         if st["last_path"] == 2 or st["flags"] != flags0:

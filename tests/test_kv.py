@@ -187,12 +187,15 @@ def test_gpu_hash_collision_runs(hash_bits):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,hot_frac,warm,key_space", [(60000, 0.4, 10, 5000), (30000, 1.0, 0, 1),
-                                                       (50000, 0.2, 200, 20000)])
+                                                       (50000, 0.2, 200, 20000), (140000, 0.5, 50, 50000)])
 def test_gpu_hot_keys_sort_bins(n, hot_frac, warm, key_space):
     """Skewed batches: a hot key (and warm keys) put far more commands into one
     top-digit bin of the sort than an LDS chunk holds, so the bin is sorted streamed
     through global memory (rg_kv.hip kv_l2_sort_kernel); every result and the final
-    store equal the sequential restatement."""
+    store equal the sequential restatement. The 140,000-command case puts ~49,000
+    applied commands into the hot key's bin (3 x the 16,384-command LDS chunk) in a
+    batch of more than 65,536 commands, whose buckets need 3 digit passes: the streamed
+    path with an odd pass count (final pair a)."""
     rng = random.Random(n + warm)
     blobs = []
     for _ in range(n):

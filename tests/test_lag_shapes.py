@@ -394,3 +394,143 @@ def test_shard_lag_records_overflow_flagged():
     assert all(la["kernel"] == "lag" for la in launches)
     assert rows[0]["n_draws"] > 16  # the step wrote the first 16 records and counted the rest
     assert fixed[0]["flags"] & 8 and res[0][0]["flags"] & 8  # the fix-up flags the incomplete patch
+
+
+MW_CASES = [
+    # n, world, K windows, window slots, trace kind, lag grid (0 = one WG per CU)
+    (5, 2, 4, 300_032, 1, 3),
+    (9, 3, 3, 1 << 20, 2, 5),
+    (3, 4, 5, 100_096, 0, 2),
+    (9, 2, 6, 1 << 22, 1, 0),
+    (7, 1, 3, 266_240, 1, 1),   # one workgroup takes every ticket of every window in turn
+    (5, 3, 2, (1 << 24) + 384, 1, 0),  # ragged shards, the 512 x 4 shape over two windows
+]
+
+
+@pytest.mark.parametrize("n,world,K,S,kind,grid", MW_CASES)
+def test_shard_lag_windows_forced_vs_oracle(oracle, n, world, K, S, kind, grid):
+    """The multi-window lag launch (ref_lag_kernel<.., SHARD, .., MW = true>: tickets
+    window-major over the K windows, one look-back chain, draw-record base and row per
+    window), forced, in 1-4 shards: the K windows' pre-fix-up rows equal the tiled
+    K-window launch's; after the batched fix-up and commit, outputs, per-window results
+    and engine states equal the tiled K-window pipeline, one evaluator window by window,
+    and the oracle over the concatenated windows (one StdRng stream across them)."""
+    torch = torch_cuda()
+    votes, stride, total = make_votes(n, [S] * K, kind, seed=31 + n)
+    state = {"rng_next": 777, "last_committed": 4, "commit_watermark": 1, "steps": 0}
+    mp = K * S * 3 // 4
+    launches = []
+    out_m = torch.zeros(8 * stride, dtype=torch.int32, device="cuda")
+    res_m, st_m, rows_m = run_sharded_windows(n, world, K, S, votes, out_m, stride, state=state, max_phase=mp,
+                                              batched_stages=True, diag=LAG | (grid << 24), launches=launches)
+    for la in launches:
+        assert la["kernel"] == "lag" and la["shard"] and la["windows"] == K, la
+        assert (la["block"], la["words"]) == one_shape(n), la
+        assert 1 <= la["grid"] <= (grid or n_cu(torch)), la
+    tl = []
+    out_t = torch.zeros(8 * stride, dtype=torch.int32, device="cuda")
+    res_t, st_t, rows_t = run_sharded_windows(n, world, K, S, votes, out_t, stride, state=state, max_phase=mp,
+                                              batched_stages=True, diag=TILED, launches=tl)
+    assert all(la["kernel"] == "tiled" for la in tl), tl
+    for w in range(K):
+        for r in range(world):
+            assert rows_m[w][r] == rows_t[w][r], (w, r)
+            assert {k: res_m[w][r][k] for k in RES_CMP} == {k: res_t[w][r][k] for k in RES_CMP}, (w, r)
+            assert res_m[w][r]["flags"] == 0
+    assert torch.equal(out_m, out_t)
+    assert st_m == st_t
+    out_1 = torch.zeros(8 * stride, dtype=torch.int32, device="cuda")
+    res_1, st_1 = run_single(n, [S] * K, votes, out_1, stride, state=state, max_phase=mp)
+    assert torch.equal(out_m, out_1) and all(st == st_1 for st in st_m)
+    for w in range(K):
+        assert {k: res_m[w][0][k] for k in RES_CMP} == {k: res_1[w][k] for k in RES_CMP}, w
+    got = decode_outputs(out_m.view(8, stride).cpu().numpy().view(np.uint32), total)
+    base, off, rng, lc = 1, 0, 777, 4
+    Sp = ((S + 127) // 128) * 128
+    for w in range(K):
+        r1, r2, _ = oracle.trace(kind, n, 31 + n, base, S)
+        exp, eres = oracle.ref_step(n, n // 2 + 1, n // 2, 42, rng, base, r1, r2, max_phase=mp, lc_in=lc,
+                                    wm_in=res_1[w - 1]["commit_watermark"] if w else 1)
+        for k in KEYS:
+            np.testing.assert_array_equal(got[k][off:off + S], exp[k], err_msg=f"window {w} {k}")
+        assert {k: eres[k] for k in RES_CMP if k != "flags"} == {k: res_m[w][0][k] for k in RES_CMP if k != "flags"}
+        rng, lc = eres["rng_next"], eres["last_committed_max"]
+        base += S
+        off += Sp
+
+
+def test_shard_lag_windows_default_dispatch_c5_shape(oracle):
+    """No switch, the 8-GPU C5 per-rank launch shape: n = 9, 32 windows of 2^24 slots
+    split over 2 shards (2^23-slot shards, as 2^26-slot C5 windows over 8 GPUs), slot-tiled
+    1024 as the bench lays them out. Each shard's 32-window launch (2^28 slots) picks the
+    multi-window lag kernel; after the batched fix-up and commit the outputs, the 32
+    per-window results and the engine states equal one evaluator window by window, and
+    oracle slices at window and shard boundaries hold."""
+    torch = torch_cuda()
+    n, world, K, T = 9, 2, 32, 1024
+    S_win = 1 << 24
+    S, P = S_win // world, 4 * n + 1
+    tiles_win, tiles_sh = S_win // 32 // T, S // 32 // T
+    total = K * S_win
+    i64 = dict(dtype=torch.int64, device="cuda")
+    votes = torch.empty(total // 32 // T * P * T, dtype=torch.int32, device="cuda")
+    out_s = torch.zeros(total // 32 // T * 8 * T, dtype=torch.int32, device="cuda")
+    with PhaseEvaluator(n, tile_words=T) as ev:
+        ev.trace_generate_async(N.RG_TRACE_AGREE90, 23, 1, total, T, votes.data_ptr())
+        ev.sync()
+    cap = S // 8
+    rows = [torch.zeros((K, 10), **i64) for _ in range(world)]
+    fixed = [torch.zeros((K, 10), **i64) for _ in range(world)]
+    result = [torch.zeros((K, 10), **i64) for _ in range(world)]
+    recs = [torch.zeros(K * cap, **i64) for _ in range(world)]
+    torch.cuda.synchronize()
+    ctxs = [PhaseEvaluator(n, self_lane=4, seed=42, tile_words=T) for _ in range(world)]
+    try:
+        launches = []
+        for r in range(world):
+            t0 = r * tiles_sh
+            ctxs[r].phase_step_shard_windows_async(K, votes.data_ptr() + 4 * t0 * P * T, tiles_win * P * T,
+                                                   out_s.data_ptr() + 4 * t0 * 8 * T, tiles_win * 8 * T, S, T,
+                                                   1 + r * S, S_win, recs[r].data_ptr(), cap, rows[r].data_ptr())
+            launches.append(ctxs[r].last_launch())
+        torch.cuda.synchronize()
+        g = torch.stack(rows).contiguous()
+        for r in range(world):
+            t0 = r * tiles_sh
+            ctxs[r].shard_fixup_windows_async(K, out_s.data_ptr() + 4 * t0 * 8 * T, tiles_win * 8 * T, S, T, 1 + r * S,
+                                              S_win, recs[r].data_ptr(), cap, g.data_ptr(), r, world,
+                                              fixed[r].data_ptr())
+        torch.cuda.synchronize()
+        fg = torch.stack(fixed).contiguous()
+        for r in range(world):
+            ctxs[r].shard_commit_windows_async(K, fg.data_ptr(), world, 1, S_win, result[r].data_ptr())
+        torch.cuda.synchronize()
+        st_s = [ev.get_state() for ev in ctxs]
+    finally:
+        for ev in ctxs:
+            ev.close()
+    assert all(la == {"kernel": "lag", "shard": True, "block": 1024, "words": 1, "grid": n_cu(torch),
+                      "windows": K} for la in launches), launches
+    rows_h = [x.cpu().numpy().view(np.uint64) for x in rows]
+    assert all(int(x[:, 9].max()) == 0 for x in rows_h)
+    out_1 = torch.zeros_like(out_s)
+    res_1 = torch.zeros((K, 10), **i64)
+    with PhaseEvaluator(n, self_lane=4, seed=42, tile_words=T) as ev:
+        for w in range(K):
+            t0 = w * tiles_win
+            ev.phase_step_async(votes.data_ptr() + 4 * t0 * P * T, out_1.data_ptr() + 4 * t0 * 8 * T, S_win, T,
+                                slot_base=1 + w * S_win, result_ptr=res_1[w].data_ptr())
+        st_1 = ev.get_state()
+    assert torch.equal(out_s, out_1)
+    r1 = res_1.cpu().numpy().view(np.uint64)
+    for r in range(world):
+        assert result[r].cpu().numpy().view(np.uint64)[:, :9].tolist() == r1[:, :9].tolist(), r
+        assert int(result[r].cpu().numpy().view(np.uint64)[:, 9].max()) == 0
+    assert all(st == st_1 for st in st_s)
+    assert int(sum(x[:, 4].sum() for x in rows_h)) == int(r1[:, 4].sum()) > 0
+    del votes, out_1
+    p = word_planes(out_s, total // 32, T, 0)
+    cvq = popc(torch, ~p[0] & p[1])
+    assert int(cvq.sum()) == int(r1[:, 4].sum())
+    slices = [0, S - 4096, S_win - 4096, 5 * S_win + S - 2048, 17 * S_win + 32 * 1000, total - 8192]
+    check_slices(oracle, torch, p, cvq, n, N.RG_TRACE_AGREE90, 23, 1, 0, 4, slices)

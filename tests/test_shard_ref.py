@@ -331,6 +331,26 @@ def test_shard_argument_errors():
             ev.phase_step_shard_async(buf.data_ptr(), buf.data_ptr(), 100, 4, 1, 0, 100)
         with pytest.raises(N.RabiaGpuError):
             ev.shard_fixup_async(buf.data_ptr(), 100, 4, 1, buf.data_ptr(), 100, buf.data_ptr(), 2, 2)
+        # planar multi-window layouts whose windows alias (stride == pitch: window 1's plane p
+        # is window 0's plane p + 1) are refused by the step and the fix-up alike
+        S, nw = 4096, 128
+        rows = torch.zeros((2, 10), dtype=torch.int64, device="cuda")
+        with pytest.raises(N.RabiaGpuError, match="overlap"):
+            ev.phase_step_shard_windows_async(2, buf.data_ptr(), nw, buf.data_ptr(), nw, S, nw, 1, S,
+                                              buf.data_ptr(), S, rows.data_ptr())
+        with pytest.raises(N.RabiaGpuError, match="overlap"):
+            ev.shard_fixup_windows_async(2, buf.data_ptr(), nw, S, nw, 1, S, buf.data_ptr(), S, rows.data_ptr(), 0,
+                                         1, rows.data_ptr())
+        # plane-major (stride >= K x pitch) and window-major (pitch >= 20 planes x stride + n_words) pass the check
+        big = torch.zeros(21 * 2 * nw, dtype=torch.int32, device="cuda")
+        big_out = torch.zeros(8 * 2 * nw, dtype=torch.int32, device="cuda")
+        rec = torch.zeros(2 * S, dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        ev.phase_step_shard_windows_async(2, big.data_ptr(), nw, big_out.data_ptr(), nw, S, 2 * nw, 1, S,
+                                          rec.data_ptr(), S, rows.data_ptr())
+        ev.phase_step_shard_windows_async(2, big.data_ptr(), 21 * nw, big_out.data_ptr(), 8 * nw, S, nw, 1, S,
+                                          rec.data_ptr(), S, rows.data_ptr())
+        ev.sync()
 
 
 def _free_port():
