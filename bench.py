@@ -99,8 +99,9 @@ def parse():
                     help="c2: the headline (weak scaling); c5: 9 replicas x 2^26 slots per step split over the "
                          "ranks (strong scaling) with the decision bitmaps all-gathered every step")
     ap.add_argument("--c5-windows", type=int, default=64, help="C5: 2^20-slot windows per C5 window, all ranks")
-    ap.add_argument("--c5-batch", type=int, default=8,
-                    help="C5 sharded pipeline: consecutive C5 windows per shard-step launch (a bench step)")
+    ap.add_argument("--c5-batch", type=int, default=32,
+                    help="C5: consecutive C5 windows per step: one shard-step launch of K windows per rank (the "
+                         "multi-window lag kernel from 2^28 slots per launch at n = 9), one K-window launch at N = 1")
     ap.add_argument("--sharded", "--c5-sharded", dest="sharded", action="store_true",
                     help="N = 1: run the multi-GPU pipeline (shard step + fix-up + commit, exchanges with one "
                          "rank) instead of the single evaluator: the per-GPU cost of the N > 1 path")
@@ -393,22 +394,29 @@ def make_gather(dist, backend):
     return gather
 
 
-def run_sharded(a, n, S, window_slots, world, rank, dist, bitmaps):
+def run_sharded(a, n, S, window_slots, world, rank, dist, comm, bitmaps):
     """One engine over windows split into `world` contiguous shards. A step is K =
     a.c5_batch consecutive windows: every rank's shard step runs the K windows' shards
     in ONE launch (rg_phase_step_shard_windows_async; K = 1: rg_phase_step_shard_async),
     then per window: rows all-gathered, fix-up, final rows all-gathered, commit, and
     (C5) the committed/V1 bitmaps all-gathered, on a second stream. world = 1 runs the
-    same pipeline with one shard (the 1-GPU measurement of a shard-size step)."""
+    same pipeline with one shard (the 1-GPU measurement of a shard-size step).
+    comm (RCCL, the product path): stages 2-4 and the bitmaps are one C-ABI call per step,
+    rg_shard_exchange_windows_async, whose all-gathers run on the device stream through
+    the context's communicator; no torch.distributed collective. dist (gloo): the
+    one-GPU rehearsal through host copies."""
     T = a.tile_words
     K = max(1, a.c5_batch) if a.config == "c5" else 1  # C2: one 2^30-slot shard per rank, as at N = 1
-    gather = make_gather(dist, a.backend) if world > 1 else (lambda out, inp: out.copy_(inp.unsqueeze(0)))
+    gather = (None if comm is not None else
+              make_gather(dist, a.backend) if world > 1 else (lambda out, inp: out.copy_(inp.unsqueeze(0))))
     stride, in_words, out_words = layout(n, S, T)
     comp = torch.cuda.Stream()
     fix = torch.cuda.Stream()
     torch.cuda.set_stream(comp)
     # one seed on every rank; the context on this rank's GPU (main: torch.cuda.set_device(LOCAL_RANK))
     ev = PhaseEvaluator(n, self_lane=n - 1, mode="ref", seed=SEED, tile_words=T, device=torch.cuda.current_device())
+    if comm is not None:
+        comm.attach(ev)
     if a.diag:
         N.check(ev.lib.rg_debug_set(ev.ctx, a.diag), ev.ctx)
     cap = max(S // 8, 1 << 16)  # draw records per shard window (agree90: ~1 % of slots are VQ); overflow -> flags
@@ -473,10 +481,11 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, bitmaps):
         if evs is not None:
             evs[1].record(comp)
         e_main[t].record(comp)
-        with torch.cuda.stream(fix):  # the rows' all-gather
-            fix.wait_event(e_main[t])
-            gather(g_rows[t], rows[t])
-            e_rows[t].record(fix)
+        if comm is None:
+            with torch.cuda.stream(fix):  # the rows' all-gather
+                fix.wait_event(e_main[t])
+                gather(g_rows[t], rows[t])
+                e_rows[t].record(fix)
         if not fix_on_comp:
             later(t, fix)
         elif chain and t >= 1:  # the previous step's fix-up behind this step's launch, on the compute stream
@@ -487,6 +496,13 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, bitmaps):
         all-gather, the commit and the bitmaps on the second stream."""
         votes, out, rec = sets[t % a.sets]
         base = 1 + t * K * window_slots
+        if comm is not None:  # stages 2-4 + bitmaps: one C-ABI call, RCCL on the device stream
+            fs_stream.wait_event(e_main[t])
+            ev.shard_exchange_windows_async(K, out.data_ptr(), out_words, S, stride, base + start, base, window_slots,
+                                            rec.data_ptr(), cap, rows[t].data_ptr(), result[t].data_ptr(),
+                                            bm_all[t].data_ptr() if bitmaps else 0, stream=fs_stream.cuda_stream)
+            e_done[t].record(fs_stream)
+            return
         fs_stream.wait_event(e_rows[t])
         ev.shard_fixup_windows_async(K, out.data_ptr(), out_words, S, stride, base + start, window_slots,
                                      rec.data_ptr(), cap, g_rows[t].data_ptr(), rank, world,
@@ -505,7 +521,9 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, bitmaps):
             e_done[t].record(fix)
 
     def barrier():
-        if dist is not None:
+        if comm is not None:
+            ev.comm_barrier()
+        elif dist is not None:
             dist.barrier()
 
     for t in range(a.warmup):
@@ -543,12 +561,14 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, bitmaps):
         b_all = bm_all[a.warmup:].cpu().numpy().view(np.uint32)
         pop = int(np.unpackbits(b_all[:, :, :, 0].view(np.uint8)).sum())
         assert pop == decided, (pop, decided)
-    if dist is not None:
+    if comm is not None and world > 1:
+        total_ms, kern_ms = ev.comm_max([total_ms, kern_ms])
+    elif dist is not None:
         tm = torch.tensor([total_ms, kern_ms], dtype=torch.float64, device="cuda" if a.backend == "nccl" else "cpu")
         dist.all_reduce(tm, op=dist.ReduceOp.MAX)
         total_ms, kern_ms = float(tm[0]), float(tm[1])
     return {"total_ms": total_ms, "kern_ms": kern_ms, "decided": decided, "sweep_us": None, "ev": ev,
-            "stream": comp, "windows_per_launch": K, "launch": ev.last_launch()}
+            "stream": comp, "windows_per_launch": K, "launch": ev.last_launch(), "sharded": True}
 
 
 # ---------------------------------------------------------------------------
@@ -557,7 +577,7 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, bitmaps):
 # keyed by the GLOBAL slot id, so the shards need no data-path exchange; the
 # per-shard statistics and decided/V1 bitmaps are all-gathered every step.
 # ---------------------------------------------------------------------------
-def run_c3(a, world, rank, dist):
+def run_c3(a, world, rank, dist, comm):
     from rabia_amd import shard
     n, total = 5, a.c3_slots
     start, S = shard.shard_range(total, world, rank, align=128)
@@ -566,6 +586,8 @@ def run_c3(a, world, rank, dist):
     torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
     ev = PhaseEvaluator(n, mode="wmvc", coin_seed=SEED, epoch=1, device=torch.cuda.current_device())
+    if comm is not None:
+        comm.attach(ev)
     states = torch.empty(n * stride, dtype=torch.int32, device="cuda")
     info = torch.empty(max(S, 1), dtype=torch.int32, device="cuda")
     nw = (S + 31) // 32
@@ -576,7 +598,13 @@ def run_c3(a, world, rank, dist):
     g_bm = torch.zeros((n_total, world, 2, nw), dtype=torch.int32, device="cuda")
     ev.cluster_trace_async(SEED, 1 + start, S, stride, states.data_ptr(), sp)
     torch.cuda.synchronize()
-    gather = make_gather(dist, a.backend) if world > 1 else None
+    if world == 1:
+        gather = None
+    elif comm is not None:  # RCCL through the C ABI, on the step's stream
+        def gather(out, inp):
+            ev.comm_allgather_async(inp.data_ptr(), out.data_ptr(), inp.numel() * inp.element_size(), sp)
+    else:
+        gather = make_gather(dist, a.backend)
     kern = []
 
     def step(t, evs=None):
@@ -591,11 +619,16 @@ def run_c3(a, world, rank, dist):
             gather(g_stats[t], stats[t])
             gather(g_bm[t], bm[t])
 
+    def barrier():
+        if comm is not None:
+            ev.comm_barrier()
+        elif dist is not None:
+            dist.barrier()
+
     for t in range(a.warmup):
         step(t)
     torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
+    barrier()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
     t_begin, t_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t_begin.record(stream)
@@ -603,8 +636,7 @@ def run_c3(a, world, rank, dist):
         step(a.warmup + k, evs[k])
     t_end.record(stream)
     torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
+    barrier()
     total_ms = t_begin.elapsed_time(t_end)
     kern_ms = float(np.mean([b.elapsed_time(e) for b, e in evs]))
     rows = (g_stats if world > 1 else stats[:, None, :]).cpu().numpy().view(np.uint64)
@@ -616,7 +648,9 @@ def run_c3(a, world, rank, dist):
         if world > 1:  # the gathered decided bitmaps carry the folded count
             pop = int(np.unpackbits(g_bm[t, :, 0].cpu().numpy().view(np.uint8)).sum())
             assert pop == g["all_decided"], (pop, g["all_decided"])
-    if dist is not None:
+    if comm is not None and world > 1:
+        total_ms, kern_ms = ev.comm_max([total_ms, kern_ms])
+    elif dist is not None:
         tm = torch.tensor([total_ms, kern_ms], dtype=torch.float64, device="cuda" if a.backend == "nccl" else "cpu")
         dist.all_reduce(tm, op=dist.ReduceOp.MAX)
         total_ms, kern_ms = float(tm[0]), float(tm[1])
@@ -658,6 +692,15 @@ def spawn_ranks(a) -> int:
     return rc
 
 
+def json_stdout():
+    """The one JSON line goes to the process's original stdout; everything written to fd 1
+    after this (native libraries: RCCL prints a version banner when a communicator is
+    created) goes to stderr, so stdout carries exactly the line."""
+    fd = os.dup(1)
+    os.dup2(2, 1)
+    return os.fdopen(fd, "w")
+
+
 def main():
     a = parse()
     if "WORLD_SIZE" not in os.environ and (a.gpus or 1) > 1:
@@ -665,20 +708,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if a.gpus is not None and a.gpus != world:
         raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}")
+    out = json_stdout()
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.backend == "gloo":  # rehearsal: ranks may share the box's one GPU
         local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
-    dist = None
-    if world > 1:
+    dist = comm = None
+    if world > 1 and a.backend == "gloo":  # one-GPU rehearsal: host copies over gloo
         import torch.distributed as dist
-        if a.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group("gloo")
+        dist.init_process_group("gloo")
+    elif world > 1 or a.sharded:  # RCCL through the C ABI (rg_comm_*); the id travels by the launcher's store
+        from rabia_amd.shard import RcclComm
+        comm = RcclComm(rank, world)
     if a.config == "c3":
-        r = run_c3(a, world, rank, dist)
+        r = run_c3(a, world, rank, dist, comm)
         if rank == 0:
             # bytes the cluster kernels move per slot: 5 initial-state bits read, the u32 info word
             # written, the u32 read + 2 bitmap bits written by the bitmap kernel, the coin table
@@ -703,7 +747,7 @@ def main():
                                  else cpu_baseline_c3(a, r["info"].cpu().numpy().view(np.uint32))),
                 "sweep_1m_us": None,
             }
-            print(json.dumps(line), flush=True)
+            print(json.dumps(line), file=out, flush=True)
         r["ev"].close()
         if dist is not None:
             dist.destroy_process_group()
@@ -716,16 +760,22 @@ def main():
         n, S = a.replicas, a.windows * WINDOW
         window_slots = S * world
     if world == 1 and not a.sharded:
-        r = run_single(a, n, S, a.config)
+        if a.config == "c5":  # the N = 1 stream: K consecutive C5 windows per launch (one engine, ascending
+            # slot order: the same outputs and engine state as K one-window launches)
+            r = run_single(a, n, max(1, a.c5_batch) * S, a.config)
+            r["windows_per_launch"] = max(1, a.c5_batch)
+        else:
+            r = run_single(a, n, S, a.config)
     else:
-        r = run_sharded(a, n, S, window_slots, world, rank, dist, bitmaps=a.config == "c5")
+        r = run_sharded(a, n, S, window_slots, world, rank, dist, comm, bitmaps=a.config == "c5")
     K = r.get("windows_per_launch", 1)
     if rank == 0:
         value = r["decided"] / (r["total_ms"] / 1000.0)
         alg_bytes = K * S * bytes_per_slot_ref(n)
         achieved = alg_bytes / (r["kern_ms"] / 1000.0) / 1e9
-        cpu = None if (a.no_cpu_baseline or world > 1 or "sets" not in r) else cpu_baseline(a, n, r)
-        sharded = "windows_per_launch" in r
+        cpu = (None if (a.no_cpu_baseline or world > 1 or "sets" not in r or a.config != "c2")
+               else cpu_baseline(a, n, r))
+        sharded = r.get("sharded", False)
         par = f"slot-shard x{world}" + (
             (f", one engine: sharded draws + fix-up, {K} C5 windows per shard launch" if a.config == "c5" else
              ", one engine: each rank's 2^30-slot shard at provisional draws, shard rows all-gathered, VQ slots "
@@ -766,7 +816,7 @@ def main():
             "cpu_baseline": cpu,
             "sweep_1m_us": r["sweep_us"],
         }
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=out, flush=True)
     r["ev"].close()
     if dist is not None:
         dist.destroy_process_group()

@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define RG_ABI_VERSION 3
+#define RG_ABI_VERSION 4
 #define RG_MAX_REPLICAS 16
 #define RG_OUT_PLANES 8
 
@@ -242,6 +242,44 @@ int rg_shard_commit_windows_async(rg_ctx* ctx, uint32_t n_windows, const rg_step
 int rg_shard_commit_async(rg_ctx* ctx, const rg_step_result* rows_dev, uint32_t n_shards,
                           uint64_t window_base, uint64_t window_slots, rg_step_result* result_dev,
                           void* stream);
+
+/* ---- Multi-GPU exchange (RCCL over xGMI). Replaces, for the decided-slot exchange of
+ * the sharded pipeline, NetworkTransport::broadcast (rabia-core/src/network.rs:36-51):
+ * each GPU's rows and decision bitmaps for a batch of windows travel in one
+ * ncclAllGather instead of per-decision messages. One context per rank, each on its own
+ * GPU. Rank 0 makes the 128-byte id (rg_comm_unique_id) and the host's own channel
+ * (the reference's TCP transport, a rendezvous store) carries it to every rank; every
+ * rank then calls rg_comm_create (collective: it returns when all ranks joined). RCCL
+ * is loaded at run time ($RG_RCCL_LIB, else the ROCm install's librccl.so.1); the
+ * library itself needs no RCCL until rg_comm_unique_id / rg_comm_create.
+ * Exchange calls of one context must be stream-ordered among themselves (they share the
+ * communicator's scratch) and follow the stage rules above. */
+#define RG_COMM_ID_BYTES 128
+int rg_comm_unique_id(uint8_t* id_out /* RG_COMM_ID_BYTES */);
+int rg_comm_create(rg_ctx* ctx, const uint8_t* id /* RG_COMM_ID_BYTES */, int rank, int world);
+int rg_comm_destroy(rg_ctx* ctx); /* also done by rg_destroy */
+int rg_comm_rank(const rg_ctx* ctx, int* rank, int* world);
+/* Rank-ordered all-gather: recv_dev = world x `bytes` (send_dev of rank r at r x bytes). */
+int rg_comm_allgather_async(rg_ctx* ctx, const void* send_dev, void* recv_dev, uint64_t bytes, void* stream);
+/* Stages (2)-(4) of the sharded pipeline for n_windows windows of this rank's shard
+ * (shard = comm rank, n_shards = comm world), after rg_phase_step_shard_async (n_windows
+ * = 1) or rg_phase_step_shard_windows_async: rows_dev = the step's n_windows rows; the
+ * rows are all-gathered, the shard's VQ slots re-drawn (rg_shard_fixup_windows_async:
+ * out_dev / out_pitch_words / n_slots / stride_words / slot_base / max_phase / records
+ * as the step had them, window_stride = window_slots), the final rows all-gathered and
+ * folded (rg_shard_commit_windows_async over windows [window_base + w * window_slots,
+ * + window_slots)) into results_dev[w], identical on every rank. bitmaps_all_dev
+ * (optional) receives every rank's committed and V1 bitmaps, [world][n_windows][2]
+ * [ceil(n_slots/32)] words (rg_decision_bitmap_windows_async's payload). */
+int rg_shard_exchange_windows_async(rg_ctx* ctx, uint32_t n_windows, uint32_t* out_dev, uint64_t out_pitch_words,
+                                    uint64_t n_slots, uint64_t stride_words, uint64_t slot_base, uint64_t window_base,
+                                    uint64_t window_slots, uint64_t max_phase, const uint64_t* records_dev,
+                                    uint64_t records_cap, const rg_step_result* rows_dev, rg_step_result* results_dev,
+                                    uint32_t* bitmaps_all_dev, void* stream);
+/* Host-synchronous helpers for the caller's control loop (bench timing, shutdown):
+ * a barrier over all ranks, and the element-wise max over ranks of 1..64 host doubles. */
+int rg_comm_barrier(rg_ctx* ctx);
+int rg_comm_max_f64(rg_ctx* ctx, double* values, uint32_t count);
 
 /* Follower side of a decided window (RabiaEngine::handle_decision,
  * engine.rs:708-746): the window's decisions, as an output buffer in the context's

@@ -111,6 +111,16 @@ _SIGS = {
     "rg_unpack_planes": (ctypes.c_int, [vp, u32, u64, u64, vp]),
     "rg_planar_to_tiled": (ctypes.c_int, [vp, u32, u64, u64, u32, vp]),
     "rg_tiled_to_planar": (ctypes.c_int, [vp, u32, u64, u32, u64, vp]),
+    # multi-GPU exchange over RCCL (include/rabia_gpu.h)
+    "rg_comm_unique_id": (ctypes.c_int, [vp]),
+    "rg_comm_create": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int]),
+    "rg_comm_destroy": (ctypes.c_int, [vp]),
+    "rg_comm_rank": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    "rg_comm_allgather_async": (ctypes.c_int, [vp, vp, vp, u64, vp]),
+    "rg_shard_exchange_windows_async": (ctypes.c_int, [vp, u32, vp, u64, u64, u64, u64, u64, u64, u64, vp, u64, vp,
+                                                       vp, vp, vp]),
+    "rg_comm_barrier": (ctypes.c_int, [vp]),
+    "rg_comm_max_f64": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), u32]),
     # kvstore apply (include/rabia_kv.h)
     "rg_kv_create": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.POINTER(RgKvConfig)]),
     "rg_kv_destroy": (ctypes.c_int, [vp]),

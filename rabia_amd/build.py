@@ -15,8 +15,8 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB_DIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIB_DIR, "librabia_gpu.so")
-SOURCES = [os.path.join(CSRC, f) for f in ("rabia_gpu.hip", "rg_shard.hip", "rg_kv.hip", "rg_ingest.hip")]
-DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("rg_common.h", "rg_kernels.h")] + [
+SOURCES = [os.path.join(CSRC, f) for f in ("rabia_gpu.hip", "rg_shard.hip", "rg_kv.hip", "rg_ingest.hip", "rg_comm.hip")]
+DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("rg_common.h", "rg_kernels.h", "rg_ctx.h")] + [
     os.path.join(ROOT, "include", "rabia_gpu.h"), os.path.join(ROOT, "include", "rabia_gpu_debug.h"),
     os.path.join(ROOT, "include", "rabia_kv.h"), os.path.join(ROOT, "include", "rabia_ingest.h")]
 ARCH = "gfx950"

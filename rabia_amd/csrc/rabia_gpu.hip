@@ -15,6 +15,7 @@
 #include <new>
 #include <string>
 
+#include "rg_ctx.h"
 #include "rg_kernels.h"
 
 using namespace rg;
@@ -22,49 +23,6 @@ using namespace rg;
 namespace rg {
 void launch_ref_shard(int n, int block, int words, uint32_t grid, hipStream_t s, const StepParams& p);
 }
-
-struct rg_ctx {
-  rg_config cfg{};
-  uint32_t q = 0, fp1 = 0;
-  Key ref_key{}, coin_key{};
-  uint64_t coin_stream = 0;
-  hipStream_t stream = nullptr;
-  Record* rec = nullptr;
-  DevState* state = nullptr;
-  DevResult* result = nullptr;
-  unsigned long long* lookback = nullptr;
-  unsigned long long* stats = nullptr;
-  uint64_t tile_cap = 0;
-  uint32_t seq = 0;
-  uint32_t* d_votes = nullptr;
-  uint32_t* d_out = nullptr;
-  DevResult* d_user_result = nullptr;
-  uint64_t stage_votes_words = 0, stage_out_words = 0;
-  uint32_t diag = 0;
-  unsigned long long* dbg = nullptr;
-  uint64_t dbg_cap = 0;
-  uint32_t* r1v_cells = nullptr;   // round-1 votes: per-slot claim cells (0xFFFFFFFF)
-  uint64_t r1v_cells_cap = 0;
-  uint32_t* r1v_blocks = nullptr;  // per-block draw counts / offsets
-  uint64_t r1v_blocks_cap = 0;
-  unsigned long long* r1v_base = nullptr;
-  uint32_t* cluster_coins = nullptr;            // [phases][n_words] common-coin table
-  uint64_t cluster_coins_cap = 0;               // words
-  unsigned long long* cluster_part = nullptr;  // [blocks][kClusterStats]
-  uint64_t cluster_part_cap = 0;                // blocks
-  unsigned long long* cluster_stats = nullptr;  // [kClusterStats]
-  unsigned long long* fix_acc = nullptr;        // sharded REF fix-up accumulators [4][windows]
-  uint64_t fix_acc_cap = 4;
-  unsigned long long* follow_acc = nullptr;     // follower commit partials [kFollowGrid][4]
-  // results of the shard fix-up / shard commit / follower commit: each stage writes
-  // its own (a fix-up may run on another stream than the next window's step, whose
-  // result is ctx->result, the one rg_last_result reads)
-  DevResult* stage_result = nullptr;            // [3]
-  uint32_t n_cu = 256;                          // compute units (persistent lag-kernel grid)
-  bool chained = false;                         // counted in g_chain[device].live
-  uint32_t last_launch[6] = {};                 // rg_debug_last_launch: kind, shard, block, words, grid, windows
-  std::string err;
-};
 
 namespace {
 
@@ -104,16 +62,18 @@ int hip_fail(rg_ctx* ctx, hipError_t e, const char* what) {
   } while (0)
 
 constexpr int wmax_for(int n) { return n <= 5 ? 4 : (n <= 10 ? 2 : 1); }
-// persistent lag kernel: one workgroup per CU with tiles of kLagBlock x lag_words(n)
-// words (launches of >= 2 such tiles per CU), else two 512-thread workgroups per CU
-// with tiles of 512 x lag_words(n). The one-per-CU tile runs as lag_one_block(n)
-// threads x lag_one_words(n) words: n <= 5 as 512 x 4 (16-byte plane loads per lane:
-// 662.6 vs 668.2 us per 2^30 slots against 1024 x 2, interleaved A/B,
-// profiles/r04_ab_lag_w4_2e30.json), n > 5 as 1024 x 1.
+// persistent lag kernel: one workgroup per CU with 2048-word tiles (launches of >= 2
+// 1024 x lag_words(n)-word tiles per CU), else two 512-thread workgroups per CU with
+// tiles of 512 x lag_words(n) words. The one-per-CU tile runs as 512 threads x 4 words
+// (16-byte plane loads per lane) at every n <= 10: n = 5, 662.6 vs 668.2 us per 2^30
+// slots against 1024 x 2 (profiles/r04_ab_lag_w4_2e30.json); n = 9, 259.5 vs 298.8 us
+// per 2^28 slots against 1024 x 1 (profiles/r05/c5_probe_n9_k32_shapes.json). No
+// scratch up to n = 10 (256 VGPRs at 8 waves per CU).
 constexpr int kLagBlock = 1024, kLagBlockSmall = 512;
 constexpr int lag_words(int n) { return n <= 5 ? 2 : 1; }
-constexpr int lag_one_block(int n) { return n <= 5 ? 512 : 1024; }
-constexpr int lag_one_words(int n) { return kLagBlock * lag_words(n) / lag_one_block(n); }
+constexpr int lag_one_block(int) { return 512; }
+constexpr int lag_one_words(int) { return 4; }
+constexpr uint64_t kLagOneTileWords = 2048;
 
 // Tile shapes of the tiled kernel: {threads, words per thread}. Big tiles keep the
 // per-launch count of tiles and look-back hand-offs low on large windows; small
@@ -142,11 +102,8 @@ struct Disp {
   }
   // persistent lag kernel (large launches): grid = resident workgroups, tiles by ticket
   static void ref_lag(uint32_t grid, hipStream_t s, const StepParams& p) {  // n <= 10 (step_impl)
-    if constexpr (N <= 5)  // 8 waves per CU, up to 256 VGPRs each
+    if constexpr (N <= 10)  // 8 waves per CU, up to 256 VGPRs each
       hipLaunchKernelGGL((ref_lag_kernel<N, lag_one_words(N), lag_one_block(N), false, 2>), dim3(grid),
-                         dim3(lag_one_block(N)), 0, s, p);
-    else if constexpr (N <= 10)
-      hipLaunchKernelGGL((ref_lag_kernel<N, lag_one_words(N), lag_one_block(N), false>), dim3(grid),
                          dim3(lag_one_block(N)), 0, s, p);
   }
   static void ref_lag512(uint32_t grid, hipStream_t s, const StepParams& p) {
@@ -270,6 +227,8 @@ bool windows_disjoint(const rg_ctx* ctx, uint32_t planes, uint64_t n_words, uint
 
 }  // namespace
 
+int rg_set_error(rg_ctx* ctx, int code, const std::string& msg) { return fail(ctx, code, msg); }
+
 extern "C" {
 
 int rg_abi_version(void) { return RG_ABI_VERSION; }
@@ -370,6 +329,7 @@ int rg_destroy(rg_ctx* ctx) {
   if (!ctx) return RG_OK;
   (void)hipSetDevice(ctx->cfg.device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  rg_comm_release(ctx);
   if (ctx->chained) {
     DevChain& dc = g_chain[ctx->cfg.device];
     std::lock_guard<std::mutex> lk(dc.mu);
@@ -488,8 +448,8 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
   const bool mw = shard && win.n > 1;
   const uint64_t launch_words = n_words * (mw ? win.n : 1u);
   const bool lag_big = launch_words >= 32ull * ctx->n_cu * kLagBlock * (uint64_t)lag_words(n);
-  const uint64_t tiles_1024 = (n_words + kLagBlock * lag_words(n) - 1) / (kLagBlock * lag_words(n));
-  const bool mw_fits = !mw || tiles_1024 * win.n < (1ull << 30);  // tickets and look-back indices are 31-bit
+  const uint64_t tiles_one = (n_words + kLagOneTileWords - 1) / kLagOneTileWords;
+  const bool mw_fits = !mw || tiles_one * win.n < (1ull << 30);  // tickets and look-back indices are 31-bit
   const bool lag = lag_fits && mw_fits && n <= 10 &&
                    ((ctx->diag & 0x200000u) ? !wmvc
                                             : (lag_ok && lag_big && !(ctx->diag & 0x100000u) &&
@@ -497,8 +457,8 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
   // multi-window launches run only the one-workgroup-per-CU shape
   const bool lag1024 = lag && (mw || (!(ctx->diag & 0x400000u) &&
                                       n_words >= 2ull * ctx->n_cu * kLagBlock * (uint64_t)lag_words(n)));
-  const uint64_t lag_block = lag1024 ? kLagBlock : kLagBlockSmall;
-  uint64_t tile_words = lag ? lag_block * lag_words(n) : (uint64_t)cfg_block(cfg) * cfg_words(cfg, n);
+  uint64_t tile_words = lag ? (lag1024 ? kLagOneTileWords : (uint64_t)kLagBlockSmall * lag_words(n))
+                            : (uint64_t)cfg_block(cfg) * cfg_words(cfg, n);
   uint64_t n_tiles = (n_words + tile_words - 1) / tile_words;  // per window
   const uint64_t launch_tiles = n_tiles * (mw ? win.n : 1u);
   const uint32_t grid_force = (ctx->diag >> 24) & 0xFFu;  // diagnostics: lag-kernel grid (tests: many tiles per WG)

@@ -11,18 +11,14 @@ template <int N>
 void launch_n(int block, int words, uint32_t grid, hipStream_t s, const StepParams& p) {
   const dim3 g(grid, p.n_win > 1 ? p.n_win : 1);  // grid.y: windows of a multi-window launch (tiled kernel)
   constexpr int WM = N <= 5 ? 4 : (N <= 10 ? 2 : 1);
-  if (block <= 0) {  // the lag kernel (n <= 10, step_impl): -1 one WG per CU (2048-word tiles at n <= 5 as
-                     // 512 x 4, 1024-word tiles at n > 5 as 1024 x 1), 0 two 512-thread WGs per CU,
-                     // -2 the one-WG-per-CU shape over the tickets of every window (multi-window launch)
-    if constexpr (N <= 5) {
+  if (block <= 0) {  // the lag kernel (n <= 10, step_impl): -1 one WG per CU (2048-word tiles as 512 x 4),
+                     // -2 the same over the tickets of every window (multi-window launch), 0 two 512-thread
+                     // WGs per CU (512 x (n <= 5 ? 2 : 1))
+    if constexpr (N <= 10) {
+      constexpr int W2 = N <= 5 ? 2 : 1;
       if (block == -2) hipLaunchKernelGGL((ref_lag_kernel<N, 4, 512, true, 2, true>), dim3(grid), dim3(512), 0, s, p);
       else if (block < 0) hipLaunchKernelGGL((ref_lag_kernel<N, 4, 512, true, 2>), dim3(grid), dim3(512), 0, s, p);
-      else hipLaunchKernelGGL((ref_lag_kernel<N, 2, 512, true>), dim3(grid), dim3(512), 0, s, p);
-    } else if constexpr (N <= 10) {
-      if (block == -2)
-        hipLaunchKernelGGL((ref_lag_kernel<N, 1, 1024, true, 4, true>), dim3(grid), dim3(1024), 0, s, p);
-      else if (block < 0) hipLaunchKernelGGL((ref_lag_kernel<N, 1, 1024, true>), dim3(grid), dim3(1024), 0, s, p);
-      else hipLaunchKernelGGL((ref_lag_kernel<N, 1, 512, true>), dim3(grid), dim3(512), 0, s, p);
+      else hipLaunchKernelGGL((ref_lag_kernel<N, W2, 512, true>), dim3(grid), dim3(512), 0, s, p);
     }
   } else if (block == 512) hipLaunchKernelGGL((ref_step_kernel<N, WM, 512, true>), g, dim3(512), 0, s, p);
   else if (block == 256) hipLaunchKernelGGL((ref_step_kernel<N, WM, 256, true>), g, dim3(256), 0, s, p);
@@ -37,7 +33,7 @@ const Launch kTable[17] = {nullptr,      &launch_n<1>,  &launch_n<2>,  &launch_n
 
 // block/words must be one of the shapes rabia_gpu.hip picks: {512, wmax}, {256, wmax}, {128, 1};
 // block <= 0 = the persistent lag kernel (tiles by ticket, grid = resident workgroups; -1: one workgroup
-// per CU, 512 x 4 at n <= 5 and 1024 x 1 above; 0: two 512-thread workgroups per CU, 512 x (n <= 5 ? 2 : 1)).
+// per CU, 512 x 4; -2: the same over several windows; 0: two 512-thread workgroups per CU, 512 x (n <= 5 ? 2 : 1)).
 void launch_ref_shard(int n, int block, int words, uint32_t grid, hipStream_t s, const StepParams& p) {
   kTable[n](block, words, grid, s, p);
 }

@@ -320,6 +320,52 @@ class PhaseEvaluator:
         N.check(self.lib.rg_shard_commit_async(self.ctx, rows_ptr, n_shards, window_base, window_slots,
                                                result_ptr or None, stream or None), self.ctx)
 
+    # -- multi-GPU exchange over RCCL (include/rabia_gpu.h, rabia_amd/csrc/rg_comm.hip) --
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        """Rank 0: a fresh 128-byte RCCL id, to be carried to every rank by the host."""
+        lib = N.load()
+        buf = (ctypes.c_uint8 * 128)()
+        N.check(lib.rg_comm_unique_id(buf))
+        return bytes(buf)
+
+    def comm_create(self, uid: bytes, rank: int, world: int):
+        """Collective over the `world` ranks: attach an RCCL communicator to this context."""
+        if len(uid) != 128:
+            raise ValueError("the RCCL id is 128 bytes")
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        N.check(self.lib.rg_comm_create(self.ctx, buf, rank, world), self.ctx)
+
+    def comm_destroy(self):
+        N.check(self.lib.rg_comm_destroy(self.ctx), self.ctx)
+
+    def comm_rank(self):
+        r, w = ctypes.c_int(), ctypes.c_int()
+        N.check(self.lib.rg_comm_rank(self.ctx, ctypes.byref(r), ctypes.byref(w)), self.ctx)
+        return r.value, w.value
+
+    def comm_allgather_async(self, send_ptr, recv_ptr, nbytes, stream=0):
+        N.check(self.lib.rg_comm_allgather_async(self.ctx, send_ptr, recv_ptr, nbytes, stream or None), self.ctx)
+
+    def shard_exchange_windows_async(self, n_windows, out_ptr, out_pitch, n_slots, stride, slot_base, window_base,
+                                     window_slots, records_ptr, records_cap, rows_ptr, results_ptr, bitmaps_all_ptr=0,
+                                     max_phase=0, stream=0):
+        """Stages 2-4 (+ bitmaps) of the sharded pipeline through the context's communicator:
+        rows all-gathered, fix-up, final rows all-gathered, commit into results_ptr[K]."""
+        N.check(self.lib.rg_shard_exchange_windows_async(self.ctx, n_windows, out_ptr, out_pitch, n_slots, stride,
+                                                         slot_base, window_base, window_slots, max_phase, records_ptr,
+                                                         records_cap, rows_ptr, results_ptr, bitmaps_all_ptr or None,
+                                                         stream or None), self.ctx)
+
+    def comm_barrier(self):
+        N.check(self.lib.rg_comm_barrier(self.ctx), self.ctx)
+
+    def comm_max(self, values):
+        """Element-wise max over ranks of a few host floats."""
+        arr = (ctypes.c_double * len(values))(*[float(v) for v in values])
+        N.check(self.lib.rg_comm_max_f64(self.ctx, arr, len(values)), self.ctx)
+        return list(arr)
+
     def follower_commit_async(self, out_ptr, n_slots, stride, slot_base, applied_ptr=0, gate_ptr=0, result_ptr=0,
                               max_phase=0, stream=0):
         """handle_decision over a decided window (engine.rs:708-746): applied = V1 slots

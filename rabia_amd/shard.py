@@ -131,11 +131,52 @@ def exchange_bitmap(plane_tensor, group=None):
     return out.view((world,) + tuple(plane_tensor.shape))
 
 
+def rendezvous_store(rank: int, world: int, timeout_s: float = 300.0):
+    """The host channel that carries rank 0's RCCL id to every rank: the TCP store of the
+    launcher (torch.distributed.run's agent store, TORCHELASTIC_USE_AGENT_STORE) or,
+    without one, a store rank 0 serves at MASTER_ADDR:MASTER_PORT. A key-value store,
+    not a collective: the data path runs through the C ABI's communicator."""
+    import datetime
+    import os
+    from torch.distributed import PrefixStore, TCPStore
+    host = os.environ.get("MASTER_ADDR", "127.0.0.1")
+    port = int(os.environ["MASTER_PORT"])
+    agent = os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "").lower() == "true"
+    store = TCPStore(host, port, world, is_master=(rank == 0 and not agent),
+                     timeout=datetime.timedelta(seconds=timeout_s), wait_for_workers=False)
+    return PrefixStore("rabia_rg_comm/", store)
+
+
+class RcclComm:
+    """Rank `rank` of `world`: the RCCL id (rank 0 makes it, the rendezvous store carries
+    it) to attach to this rank's evaluator contexts (rg_comm_create, a collective). World
+    1 needs no store."""
+
+    def __init__(self, rank: int, world: int, store=None, key: str = "uid"):
+        from .engine import PhaseEvaluator
+        self.rank, self.world = rank, world
+        if world == 1:
+            self.uid = PhaseEvaluator.comm_unique_id()
+            return
+        store = store if store is not None else rendezvous_store(rank, world)
+        if rank == 0:
+            self.uid = PhaseEvaluator.comm_unique_id()
+            store.set(key, self.uid)
+        else:
+            self.uid = bytes(store.get(key))
+
+    def attach(self, ev):
+        ev.comm_create(self.uid, self.rank, self.world)
+        return ev
+
+
 class ShardedRefStep:
     """One rank's driver of the sharded REF window (include/rabia_gpu.h): the four
-    stages of one window on this rank's evaluator, the two row exchanges going
-    through torch.distributed (all_gather_into_tensor on device rows for "nccl";
-    host copies for "gloo"). Synchronous per window; bench.py pipelines the same
+    stages of one window on this rank's evaluator. With an RCCL communicator attached
+    to the evaluator (RcclComm.attach, rccl=True) stages 2-4 are ONE C-ABI call
+    (rg_shard_exchange_windows_async: the all-gathers run on the device stream);
+    otherwise the two row exchanges go through torch.distributed (host copies for
+    "gloo": the CPU rehearsal). Synchronous per window; bench.py pipelines the same
     calls across windows.
 
     shared_gpu=True: the ranks share one GPU (a rehearsal: one process per rank on one
@@ -144,10 +185,12 @@ class ShardedRefStep:
     one GPU can wait on each other across kernels (include/rabia_gpu.h).
     The in-process chain of the C ABI cannot order launches of other processes."""
 
-    def __init__(self, ev, rank: int, world: int, n_slots_cap: int, group=None, shared_gpu: bool = False):
+    def __init__(self, ev, rank: int, world: int, n_slots_cap: int, group=None, shared_gpu: bool = False,
+                 rccl: bool = False):
         import torch
         self.ev, self.rank, self.world, self.group = ev, rank, world, group
         self.shared_gpu = shared_gpu
+        self.rccl = rccl
         self.cap = int(n_slots_cap)
         self.records = torch.empty(max(self.cap, 1), dtype=torch.int64, device="cuda")
         self.row = torch.zeros(10, dtype=torch.int64, device="cuda")
@@ -170,6 +213,14 @@ class ShardedRefStep:
         [window_base, window_base + window_slots); returns the global step result."""
         import torch
         ev = self.ev
+        if self.rccl:
+            ev.phase_step_shard_async(votes_ptr, out_ptr, n_slots, stride, shard_base, self.records.data_ptr(),
+                                      self.cap, self.row.data_ptr(), max_phase, stream)
+            ev.shard_exchange_windows_async(1, out_ptr, 0, n_slots, stride, shard_base, window_base, window_slots,
+                                            self.records.data_ptr(), self.cap, self.row.data_ptr(),
+                                            self.result.data_ptr(), max_phase=max_phase, stream=stream)
+            ev.sync(stream)
+            return row_result(self.result.cpu().numpy().view("uint64").tolist())
         for r in (range(self.world) if self.shared_gpu and self.world > 1 else [self.rank]):
             if r == self.rank:
                 ev.phase_step_shard_async(votes_ptr, out_ptr, n_slots, stride, shard_base, self.records.data_ptr(),

@@ -16,7 +16,7 @@ def test_header_symbols_exported():
     for s in syms:
         assert hasattr(lib, s), f"librabia_gpu.so does not export {s}"
         assert s in N._SIGS, f"binding lacks a signature for {s}"
-    assert lib.rg_abi_version() == 3
+    assert lib.rg_abi_version() == 4
 
 
 def test_plane_stride():

@@ -46,9 +46,9 @@ def lag_words(n):
 
 
 def one_shape(n):
-    """(threads, words per thread) of the one-workgroup-per-CU lag shape: the same
-    1024 x lag_words(n)-word tile as 512 x 4 at n <= 5 (16-byte plane loads), 1024 x 1 above."""
-    return (512, 4) if n <= 5 else (1024, 1)
+    """(threads, words per thread) of the one-workgroup-per-CU lag shape: 2048-word tiles as
+    512 x 4 (16-byte plane loads) at every n <= 10 (round 5; n > 5 ran 1024 x 1 before)."""
+    return (512, 4)
 
 
 def popc(torch, x):
@@ -228,7 +228,7 @@ def test_forced_lag1024_vs_full_oracle(oracle, n, kind):
 @pytest.mark.parametrize("n", [3, 7, 9])
 def test_default_dispatch_lag1024(oracle, n):
     """No switch: at the first size where every CU runs >= 32 lag tiles step_impl
-    picks the one-workgroup-per-CU lag shape (n = 3: 2^29 slots, 512 x 4; n = 7, 9: 2^28, 1024 x 1).
+    picks the one-workgroup-per-CU lag shape, 512 x 4 (n = 3: 2^29 slots; n = 7, 9: 2^28).
     Properties over every slot, oracle slices, the tiled kernel's output."""
     torch = torch_cuda()
     S = 32 * 32 * n_cu(torch) * 1024 * lag_words(n)
@@ -239,7 +239,7 @@ def test_default_dispatch_lag1024(oracle, n):
     nw = S // 32
     p = word_planes(out, nw, 0, stride)
     cvq = check_properties(torch, p, S, base, 0, res, 5, res["rng_next"], lc_in=0)
-    tw = 1024 * lag_words(n)
+    tw = 2048  # one workgroup tile of the lag kernel, in words
     check_slices(oracle, torch, p, cvq, n, kind, seed, base, 5, n - 1,
                  [0, S - 8192, 32 * (tw - 64), 32 * (nw // 3), 32 * (nw - 2 * tw - 32)])
     del p, cvq
@@ -509,7 +509,7 @@ def test_shard_lag_windows_default_dispatch_c5_shape(oracle):
     finally:
         for ev in ctxs:
             ev.close()
-    assert all(la == {"kernel": "lag", "shard": True, "block": 1024, "words": 1, "grid": n_cu(torch),
+    assert all(la == {"kernel": "lag", "shard": True, "block": 512, "words": 4, "grid": n_cu(torch),
                       "windows": K} for la in launches), launches
     rows_h = [x.cpu().numpy().view(np.uint64) for x in rows]
     assert all(int(x[:, 9].max()) == 0 for x in rows_h)

@@ -499,3 +499,73 @@ def test_pipelined_two_streams_equals_one_engine():
                 g = shard.row_result(got[t, r, k].tolist())
                 assert {f: g[f] for f in RES_CMP} == {f: res_1[t * K + k][f] for f in RES_CMP}, (t, r, k)
     assert all(st == st_1 for st in states)
+
+
+@pytest.mark.parametrize("n,K,S,kind", [(5, 3, 300_032, 1), (9, 4, 1 << 20, 2)])
+def test_rccl_exchange_world1_equals_one_evaluator(n, K, S, kind):
+    """The multi-GPU pipeline through the C ABI's RCCL communicator (rg_comm_create at
+    world 1, rg_shard_exchange_windows_async: rows all-gathered, fix-up, final rows
+    all-gathered, commit, bitmaps all-gathered, all on one device stream) equals one
+    evaluator window by window: outputs, results, engine state; the gathered bitmaps
+    equal rg_decision_bitmap_windows_async of the fixed outputs. Also the single-window
+    driver (ShardedRefStep(rccl=True)), the generic all-gather, max and barrier."""
+    torch = torch_cuda()
+    votes, stride, total = make_votes(n, [S] * K, kind, seed=41)
+    Sp = ((S + 127) // 128) * 128
+    nw = (S + 31) // 32
+    i64 = dict(dtype=torch.int64, device="cuda")
+    out = torch.zeros(8 * stride, dtype=torch.int32, device="cuda")
+    rows = torch.zeros((K, 10), **i64)
+    res = torch.zeros((K, 10), **i64)
+    rec = torch.zeros(K * S, **i64)
+    bm_all = torch.zeros((1, K, 2, nw), dtype=torch.int32, device="cuda")
+    state = {"rng_next": 55, "last_committed": 2, "commit_watermark": 1, "steps": 0}
+    mp = K * S * 2 // 3
+    torch.cuda.synchronize()
+    with PhaseEvaluator(n, self_lane=n // 2, seed=42) as ev:
+        with pytest.raises(N.RabiaGpuError, match="no communicator"):
+            ev.comm_barrier()
+        shard.RcclComm(0, 1).attach(ev)
+        assert ev.comm_rank() == (0, 1)
+        ev.set_state(**state)
+        ev.phase_step_shard_windows_async(K, votes.data_ptr(), Sp // 32, out.data_ptr(), Sp // 32, S, stride, 1, S,
+                                          rec.data_ptr(), S, rows.data_ptr(), max_phase=mp)
+        ev.shard_exchange_windows_async(K, out.data_ptr(), Sp // 32, S, stride, 1, 1, S, rec.data_ptr(), S,
+                                        rows.data_ptr(), res.data_ptr(), bm_all.data_ptr(), max_phase=mp)
+        ev.sync()
+        st = ev.get_state()
+        # generic all-gather (world 1: a copy), max over ranks, barrier
+        src = torch.arange(37, dtype=torch.int32, device="cuda")
+        dst = torch.zeros(37, dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        ev.comm_allgather_async(src.data_ptr(), dst.data_ptr(), 37 * 4)
+        ev.sync()
+        assert torch.equal(src, dst)
+        assert ev.comm_max([1.5, -2.0, 7.0]) == [1.5, -2.0, 7.0]
+        ev.comm_barrier()
+        ev.comm_destroy()
+        with pytest.raises(N.RabiaGpuError):
+            ev.comm_rank()
+    out_1 = torch.zeros(8 * stride, dtype=torch.int32, device="cuda")
+    res_1, st_1 = run_single(n, [S] * K, votes, out_1, stride, self_lane=n // 2, state=state, max_phase=mp)
+    assert torch.equal(out, out_1) and st == st_1
+    got = rows_of(res)
+    for w in range(K):
+        assert {k: got[w][k] for k in RES_CMP} == {k: res_1[w][k] for k in RES_CMP}, w
+    bm = torch.zeros((K, 2, nw), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    with PhaseEvaluator(n) as ev:
+        ev.decision_bitmap_windows_async(K, out.data_ptr(), Sp // 32, S, stride, bm[0, 0].data_ptr(),
+                                         bm[0, 1].data_ptr(), 2 * nw)
+        ev.sync()
+    assert torch.equal(bm_all[0], bm)
+    # the single-window driver over the first window through the communicator
+    out_d = torch.zeros(8 * stride, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    with PhaseEvaluator(n, self_lane=n // 2, seed=42) as ev:
+        shard.RcclComm(0, 1).attach(ev)
+        ev.set_state(**state)
+        drv = shard.ShardedRefStep(ev, 0, 1, S, rccl=True)
+        g = drv.step(votes.data_ptr(), out_d.data_ptr(), S, stride, 1, 1, S, max_phase=mp)
+    assert {k: g[k] for k in RES_CMP} == {k: res_1[0][k] for k in RES_CMP}
+    assert torch.equal(out_d[: Sp // 32], out_1[: Sp // 32])

@@ -1,0 +1,98 @@
+#!/bin/bash
+# One parameterised GPU-box recipe: runs the named steps in order, each under its own
+# time limit, and stops at the first failure (no step runs after a fault, abort or
+# time limit). Results under gpurun_out/$TAG/.
+#   usage: bash tools/gpu_run.sh TAG STEP [STEP ...]
+#   steps:
+#     tests[=EXPR]      python -m pytest tests -m gpu (-k EXPR)
+#     smoke             __graft_entry__.smoke()
+#     bench             bench.py (C2 headline, CPU leg included)
+#     bench_sharded     bench.py --sharded (the N > 1 per-GPU pipeline on one GPU, RCCL world 1)
+#     c3 | c5 | c5_sharded   bench.py --config ...
+#     c4                tools/bench_c4.py (kvstore apply)
+#     probe_c5[=K]      tools/c5_probe.py, n = 9, K windows of 2^23 (default 32)
+#     ab[=SLOTS]        tools/ab_variants.py (interleaved A/B, AB_DIAGS / RABIA_AB_LIBS from the env)
+#     stamps            tools/lag_stamps.py (per-phase lag-kernel stamps at 2^30)
+#     latency           tools/latency_1m.py (single 2^20 window)
+#     gloo2             bench.py --gpus 2 --backend gloo (two ranks on the one GPU, a rehearsal)
+#     prof[=ARGS]       rocprofv3 --kernel-trace --stats over bench.py ARGS (default: the C2 line)
+#     pmc[=ARGS]        two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) over bench.py ARGS
+#     sq[=ARGS]         one SQ/GRBM counter pass over bench.py ARGS
+#   ARGS use ':' for spaces, e.g. prof=--config:c5:--sharded
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=${1:?usage: gpu_run.sh TAG STEP...}
+shift
+OUT=$R/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd "$R"
+export PYTHONUNBUFFERED=1
+
+run() {  # name seconds command...
+  local name=$1 secs=$2
+  shift 2
+  echo "== $name"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err"
+  local rc=$?
+  if [ $rc -ne 0 ]; then
+    echo "$name failed (rc $rc)"
+    tail -30 "$OUT/$name.err"
+    tail -30 "$OUT/$name.out"
+    exit $rc
+  fi
+  tail -2 "$OUT/$name.out"
+}
+
+prof_run() {  # name seconds rocprof-args... -- bench args (rocprofv3 needs the program itself after --)
+  local name=$1 secs=$2
+  shift 2
+  echo "== $name"
+  (export TMPDIR=/tmp; cd /tmp && timeout -s KILL "$secs" rocprofv3 "$@" > "$OUT/$name.log" 2>&1)
+  local rc=$?
+  if [ $rc -ne 0 ]; then
+    echo "$name failed (rc $rc)"
+    tail -30 "$OUT/$name.log"
+    exit $rc
+  fi
+}
+
+for step in "$@"; do
+  name=${step%%=*}
+  arg=""
+  [ "$step" != "$name" ] && arg=${step#*=}
+  bargs=${arg//:/ }
+  case $name in
+    tests)
+      if [ -n "$arg" ]; then
+        run tests 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$arg"
+      else
+        run tests 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+      fi ;;
+    smoke) run smoke 200 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 400 python bench.py ;;
+    bench_sharded) run bench_sharded 300 python bench.py --sharded --steps 20 --warmup 10 --no-cpu-baseline ;;
+    c3) run c3 300 python bench.py --config c3 --steps 10 --warmup 3 --no-cpu-baseline ;;
+    c5) run c5 300 python bench.py --config c5 --steps 20 --warmup 10 ;;
+    c5_sharded) run c5_sharded 300 python bench.py --config c5 --sharded --steps 20 --warmup 10 ;;
+    c4) run c4 300 python tools/bench_c4.py ;;
+    probe_c5) run "probe_c5_${arg:-32}" 400 python tools/c5_probe.py --n 9 --window-log2 23 --k "${arg:-32}" --diags default:0 ;;
+    ab) AB_SLOTS=${arg:-1073741824} AB_ROUNDS=${AB_ROUNDS:-4} run "ab_${arg:-1073741824}" 700 python -u tools/ab_variants.py ;;
+    stamps) run stamps 300 python tools/lag_stamps.py ;;
+    latency) run latency 300 python tools/latency_1m.py ;;
+    gloo2) run gloo2 300 python bench.py --gpus 2 --backend gloo --steps 5 --warmup 2 --no-cpu-baseline ;;
+    prof)
+      prof_run "prof" 500 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
+        python3 "$R/bench.py" --no-cpu-baseline --steps 30 --warmup 10 $bargs ;;
+    pmc)
+      prof_run pmc_fetch 240 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o pmc --output-format csv -- \
+        python3 "$R/bench.py" --no-cpu-baseline --steps 6 --warmup 2 $bargs
+      prof_run pmc_write 240 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o pmc --output-format csv -- \
+        python3 "$R/bench.py" --no-cpu-baseline --steps 6 --warmup 2 $bargs ;;
+    sq)
+      prof_run sq 240 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+        SQ_INSTS_LDS GRBM_GUI_ACTIVE -d "$OUT/sq" -o sq --output-format csv -- \
+        python3 "$R/bench.py" --no-cpu-baseline --steps 3 --warmup 1 $bargs ;;
+    *) echo "unknown step $name"; exit 2 ;;
+  esac
+done
+echo "all steps ok"
