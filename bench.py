@@ -110,6 +110,9 @@ def parse():
                          "0.80 vs 0.81, 0.84 vs 0.86, 0.86 vs 0.88 ms per one-shard step in three round-4 "
                          "runs, profiles/r04_c2_sharded_n1*.json) or on the compute stream right behind step "
                          "t + 1's launch")
+    ap.add_argument("--fixup-eager", action="store_true",
+                    help="N > 1 / --sharded: enqueue step t's exchange right after step t's launch (default: after "
+                         "step t + 1's launch)")
     ap.add_argument("--diag", type=lambda x: int(x, 0), default=0,
                     help="rg_debug_set switches for experiments (include/rabia_gpu_debug.h); 0 = the product path")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
@@ -449,6 +452,11 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, comm, bitmaps):
     # the fix-up of step t: on the second stream, overlapping step t + 1's launch, or on the
     # compute stream right behind step t + 1's launch (no competition for the CUs)
     fix_on_comp = a.fixup_stream == "comp"
+    # submission order: the exchange of step t is enqueued after step t + 1's launch (the
+    # default), so step t + 1's kernel never sits behind step t's exchange in a hardware
+    # queue the two streams may share (GPU_MAX_HW_QUEUES = 4 for every stream of the process)
+    defer = fix_on_comp or not a.fixup_eager
+    fs_main = comp if fix_on_comp else fix
 
     def shard_step(votes, out, rec, base, t):
         if K == 1:
@@ -486,10 +494,10 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, comm, bitmaps):
                 fix.wait_event(e_main[t])
                 gather(g_rows[t], rows[t])
                 e_rows[t].record(fix)
-        if not fix_on_comp:
+        if not defer:
             later(t, fix)
-        elif chain and t >= 1:  # the previous step's fix-up behind this step's launch, on the compute stream
-            later(t - 1, comp)
+        elif chain and t >= 1:  # the previous step's exchange behind this step's launch
+            later(t - 1, fs_main)
 
     def later(t, fs_stream):
         """Stages 3-4 of step t (+ C5 bitmaps): the fix-up on fs_stream, the final rows'
@@ -528,8 +536,8 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, comm, bitmaps):
 
     for t in range(a.warmup):
         step(t)
-    if fix_on_comp and a.warmup:
-        later(a.warmup - 1, comp)
+    if defer and a.warmup:
+        later(a.warmup - 1, fs_main)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -538,8 +546,8 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, comm, bitmaps):
     t_begin.record(comp)
     for k in range(a.steps):  # (the warm-up's last fix-up is done: the timed chain starts afresh)
         step(a.warmup + k, evs[k], chain=k > 0)
-    if fix_on_comp:
-        later(n_total - 1, comp)
+    if defer:
+        later(n_total - 1, fs_main)
     comp.wait_event(e_done[n_total - 1])
     t_end.record(comp)
     torch.cuda.synchronize()

@@ -1505,11 +1505,46 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
     prev_tile = park_tile;
     prev_incl = excl + park_total;
     const unsigned long long k_tile = k_base + excl;
-    unsigned long long* const vq_rec = p.vq_rec + (MW ? (uint64_t)park_l.w * p.vq_cap : 0ull);
-    // VQ slots whose draw gave V1 (engine.rs:523-537, 567-611)
 #pragma unroll
     for (int i = 0; i < W; i++) own[i] = 0;
-    if (park_total) {
+    if constexpr (SHARD) {
+      // Sharded step: no draws here. Every VQ slot is re-drawn at its global stream
+      // position by the fix-up (a provisional draw at this shard's position would be
+      // redrawn anyway), so the step takes the LIKELY outcome of the draw as its
+      // provisional own vote, deterministically: c1 > c0 -> V1 (the draw gives V1 with
+      // p = 0.9), c1 < c0 -> V0 (0.9), tie -> V1 (0.8) (engine.rs:567-611), i.e. own = e0.
+      // The fix-up then patches the 10-20 % of VQ slots whose draw disagrees. One record
+      // per VQ slot (index = local draw number, ascending slot order): offset, class,
+      // the decision under each own vote, the provisional own vote. No ChaCha12 pass and
+      // no barrier in the sharded step.
+      if (park_total) {
+        unsigned long long* const vq_rec = p.vq_rec + (MW ? (uint64_t)park_l.w * p.vq_cap : 0ull);
+        unsigned long long k = k_tile + park_thr;
+#pragma unroll
+        for (int i = 0; i < W; i++) {
+          const uint32_t e0 = pp[2][tid][i], e1 = pp[3][tid][i];
+          uint32_t m = e0 | e1;
+          own[i] = e0;
+          if (!m) continue;
+          uint32_t dv[4];
+#pragma unroll
+          for (int j = 0; j < 4; j++) dv[j] = pp[4 + j][tid][i];
+          while (m) {
+            const int b = __builtin_ctz(m);
+            m &= m - 1;
+            const bool x0 = (e0 >> b) & 1u, x1 = (e1 >> b) & 1u;  // gt: 1/0, lt: 0/1, tie: 1/1
+            const uint32_t cls = (x0 && !x1) ? kRecGt : ((x1 && !x0) ? kRecLt : 0u);
+            const uint32_t d4 = ((dv[0] >> b) & 1u) | (((dv[1] >> b) & 1u) << 1) | (((dv[2] >> b) & 1u) << 2) |
+                                (((dv[3] >> b) & 1u) << 3);
+            const uint32_t info = cls | (d4 << 2) | ((uint32_t)x0 << 6);
+            const unsigned long long kr = k - k_base;
+            const uint32_t off = 32u * (park_l.c * kTW + (uint32_t)tid * W + i) + b;  // window-relative
+            if (kr < p.vq_cap) vq_rec[kr] = ((unsigned long long)info << 32) | off;
+            k++;
+          }
+        }
+      }
+    } else if (park_total) {  // VQ slots whose draw gave V1 (engine.rs:523-537, 567-611)
       uint32_t mq[W];
       {
         uint32_t e0[W], e1[W];
@@ -1530,15 +1565,6 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
         for (int i = 0; i < W; i++) {
           if (!mq[i] || k >= k_lim) continue;
           const uint32_t e0 = pp[2][tid][i], e1 = pp[3][tid][i];
-          // SHARD: the draw record of each VQ slot, written as it is drawn (index = local
-          // draw number, ascending slot order): offset, class, the decision under each
-          // own vote, the provisional own vote (built in a loop of its own: 765 vs 697 us
-          // per 2^30 slots against no records at all)
-          uint32_t dv[4] = {0u, 0u, 0u, 0u};
-          if constexpr (SHARD) {
-#pragma unroll
-            for (int j = 0; j < 4; j++) dv[j] = pp[4 + j][tid][i];
-          }
           while (mq[i] && k < k_lim) {
             const int b = __builtin_ctz(mq[i]);
             mq[i] &= mq[i] - 1;
@@ -1548,15 +1574,6 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
             const bool x0 = (e0 >> b) & 1u, x1 = (e1 >> b) & 1u;  // gt: 1/0, lt: 0/1, tie: 1/1
             const bool v1 = (x0 && !x1) ? (u < kP90) : ((x1 && !x0) ? (u >= kP90) : (u < kP80));
             own[i] |= (uint32_t)v1 << b;
-            if constexpr (SHARD) {
-              const uint32_t cls = (x0 && !x1) ? kRecGt : ((x1 && !x0) ? kRecLt : 0u);
-              const uint32_t d4 = ((dv[0] >> b) & 1u) | (((dv[1] >> b) & 1u) << 1) | (((dv[2] >> b) & 1u) << 2) |
-                                  (((dv[3] >> b) & 1u) << 3);
-              const uint32_t info = cls | (d4 << 2) | ((uint32_t)v1 << 6);
-              const unsigned long long kr = k - k_base;
-              const uint32_t off = 32u * (park_l.c * kTW + (uint32_t)tid * W + i) + b;  // window-relative
-              if (kr < p.vq_cap) vq_rec[kr] = ((unsigned long long)info << 32) | off;
-            }
             k++;
           }
         }
@@ -1709,6 +1726,11 @@ __global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  //
     const bool any = c < n_tix;  // (cl: the tile of c, or tile 0 without one)
     const uint32_t voff0 = any ? in_off(cl) : 0u;
     buf_ld_planes<N, W>(in_rsrc(cl), voff0, in_pb, 0, r1lo, r1hi);
+    // every round-1 load before the first round-2 load, as the loop issues them: the
+    // compiler's vmcnt wait at the loop head is the minimum over the paths into it, and
+    // with the two groups interleaved here the tally waited for the round-2 planes too
+    // (vmcnt(7) instead of vmcnt(16) at n = 5)
+    __builtin_amdgcn_sched_barrier(0);
     buf_ld_planes<N, W>(in_rsrc(cl), voff0, in_pb, 2 * N, r2lo, r2hi);
     const uint32_t z[W] = {};
     const __amdgpu_buffer_rsrc_t orr = out_rsrc(TileLoc{0u, 0u});
@@ -2841,6 +2863,56 @@ __device__ __forceinline__ uint32_t heard_mask_k(uint32_t ck, uint32_t s32, int 
   return mask;
 }
 
+// The same heard set from a per-workgroup LDS table: the set depends only on the
+// receiver r and the pick ranks k_i = ((chunk i of h) * span_i) >> 6 (span_i = N - 1 - i),
+// so it is tabulated once per launch over (r, k_0, .., k_{q-2}) (N * (N-1)!/(N-q)!
+// entries: 60 at n = 5, 840 at 7, 15,120 at 9) and a lookup replaces the q - 1 branch-free
+// k-th-bit selections (heard_mask_k, which fills the table: bit-identical by construction).
+// Picks past the fifth re-mix h (heard_mask_k); tables are used only for q - 1 <= 5 picks.
+constexpr uint32_t kHeardTabMax = 16384;  // entries (u16): 32 KB of LDS
+template <int N>
+__host__ __device__ constexpr uint32_t heard_tab_size(uint32_t q) {
+  if (q < 1 || q > 6) return 0;
+  uint32_t n = N;
+  for (uint32_t i = 0; i + 1 < q; i++) {
+    n *= (uint32_t)N - 1 - i;
+    if (n > kHeardTabMax) return 0;
+  }
+  return n;
+}
+// Entry e of the table: (r, k_0, .., k_{q-2}) in mixed radix (r most significant).
+template <int N>
+__device__ __forceinline__ uint32_t heard_tab_entry(uint32_t e, uint32_t q) {
+  uint32_t k[6] = {0, 0, 0, 0, 0, 0};
+  for (int i = (int)q - 2; i >= 0; i--) {
+    const uint32_t span = (uint32_t)N - 1 - (uint32_t)i;
+    k[i] = e % span;
+    e /= span;
+  }
+  const uint32_t r = e;
+  uint32_t avail = ((1u << N) - 1u) & ~(1u << r), mask = 1u << r;
+  for (uint32_t i = 0; i + 1 < q; i++) {
+    uint32_t a = avail;
+    for (uint32_t t = 0; t < k[i]; t++) a &= a - 1;
+    const uint32_t pick = a & (~a + 1u);
+    mask |= pick;
+    avail &= ~pick;
+  }
+  return mask;
+}
+template <int N>
+__device__ __forceinline__ uint32_t heard_mask_tab(const uint16_t* tab, uint32_t ck, uint32_t s32, int r, uint32_t q) {
+  const uint32_t h = fmix32(ck ^ s32);
+  uint32_t idx = (uint32_t)r;
+#pragma unroll
+  for (uint32_t i = 0; i + 1 < (uint32_t)N && i < 5; i++) {
+    if (i + 1 >= q) break;
+    const uint32_t span = N - 1 - i;
+    idx = idx * span + ((((h >> (6 * i)) & 63u) * span) >> 6);
+  }
+  return tab[idx];
+}
+
 constexpr int kClusterStats = 8;  // all_decided, v1, sum_phases, max_phases, sum_coin_phases, sum_first, slots, -
 
 // Common-coin table for the cluster kernel: coin bits of phases 1..P for the
@@ -2892,6 +2964,10 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
   __shared__ unsigned long long s_next;
   __shared__ uint32_t s_ck[kKeyPhases][2][N];
   __shared__ uint32_t s_st[N][kStageWords];  // the chunk's initial-state words
+  constexpr uint32_t kTabCap = heard_tab_size<N>((uint32_t)N / 2 + 1) ? heard_tab_size<N>((uint32_t)N / 2 + 1) : 1;
+  __shared__ uint16_t s_heard[kTabCap];     // heard sets at the majority quorum (heard_mask_tab)
+  const uint32_t tab_n = heard_tab_size<N>(q);
+  const bool use_tab = tab_n != 0 && tab_n <= kTabCap;  // (uniform)
   const uint64_t n_words = (n_slots + 31) / 32;
   const uint64_t c0 = (uint64_t)blockIdx.x * chunk;
   const uint64_t c1 = c0 + chunk < n_slots ? c0 + chunk : n_slots;
@@ -2901,6 +2977,8 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
     const uint32_t ph = e / (2 * N), rd = (e / N) % 2, rr = e % N;
     s_ck[ph][rd][rr] = (uint32_t)cluster_key(dseed, ph + 1, rd + 1, (int)rr);
   }
+  if (use_tab)
+    for (uint32_t e = threadIdx.x; e < tab_n; e += blockDim.x) s_heard[e] = (uint16_t)heard_tab_entry<N>(e, q);
   if (c1 > c0) {
     const uint32_t nw = (uint32_t)((c1 - 1) / 32 - w0 + 1);  // <= kStageWords (chunk <= kClusterChunk)
     for (uint32_t e = threadIdx.x; e < N * nw; e += blockDim.x) {
@@ -2947,7 +3025,7 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
 #pragma unroll
     for (int r = 0; r < N; r++) {
       const uint32_t ck = tab ? s_ck[p - 1][0][r] : (uint32_t)cluster_key(dseed, p, 1, r);
-      const uint32_t h = heard_mask_k<N>(ck, s32, r, q);
+      const uint32_t h = use_tab ? heard_mask_tab<N>(s_heard, ck, s32, r, q) : heard_mask_k<N>(ck, s32, r, q);
       const uint32_t c1r = __builtin_popcount(h & st), c0r = __builtin_popcount(h & ~st);
       if (c1r >= q) v1 |= 1u << r;
       else if (c0r < q) vq |= 1u << r;
@@ -2957,7 +3035,7 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
 #pragma unroll
     for (int r = 0; r < N; r++) {
       const uint32_t ck = tab ? s_ck[p - 1][1][r] : (uint32_t)cluster_key(dseed, p, 2, r);
-      const uint32_t h = heard_mask_k<N>(ck, s32, r, q);
+      const uint32_t h = use_tab ? heard_mask_tab<N>(s_heard, ck, s32, r, q) : heard_mask_k<N>(ck, s32, r, q);
       const uint32_t c1r = __builtin_popcount(h & v1), cq = __builtin_popcount(h & vq);
       const uint32_t c0r = q - c1r - cq;
       int nv = c0r >= fp1 ? 0 : (c1r >= fp1 ? 1 : -1);

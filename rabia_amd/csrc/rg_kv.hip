@@ -120,6 +120,7 @@ enum : uint32_t { kRecNew = 1, kRecValue = 2, kRecInPlace = 4, kRecVersion = 8, 
 constexpr int kWalkPerLane = 4;                              // sorted positions per walker lane
 constexpr int kWalkSpan = 64 * kWalkPerLane;                 // positions per wave
 constexpr int kWalkBlockSpan = kBlock * kWalkPerLane;        // positions per block
+constexpr uint32_t kDecGroup = 64;                           // walk blocks per decide workgroup
 
 __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
   k ^= k >> 33; k *= 0xff51afd7ed558ccdull;
@@ -452,7 +453,8 @@ struct BatchView {
   uint8_t* results;
   uint8_t* done;          // per sorted position: handled by an earlier key of its run (multi-key runs)
   uint64_t* need;         // per sorted position: plan bytes (run heads only)
-  uint64_t* block_base;   // per walk block: heap offset of its first byte (decide's scan)
+  uint64_t* block_base;   // per walk block: heap offset of its first byte inside its decide group
+  uint64_t* group_base;   // per decide group (kDecGroup walk blocks): heap offset of its first byte
   KeyRec* recs;           // per sorted position: plan -> commit records (run head + key rank)
   uint32_t invalid_bucket;  // sort key of the commands that are not applied (sorted last)
   unsigned long long* part;  // [blocks][kPCount]
@@ -758,7 +760,8 @@ __global__ __launch_bounds__(kBlock) void kv_commit_kernel(BatchView b, StoreVie
   __syncthreads();
   unsigned long long before = 0;
   for (int w = 0; w < wave; w++) before += s_wsum[w];
-  uint64_t heap_pos = st.ctr->batch_base + b.block_base[blockIdx.x] + before + incl - mine;
+  uint64_t heap_pos = st.ctr->batch_base + b.group_base[blockIdx.x / kDecGroup] + b.block_base[blockIdx.x] + before +
+                      incl - mine;
   for (uint32_t h = lane; h < nh; h += 64) {
     const uint64_t i = wbase + s_heads[wave][h];
     // a run holds at most kMaxRunKeys records (more sends the batch to the ordered
@@ -855,36 +858,119 @@ __device__ __forceinline__ void fold_block(unsigned long long (&v)[sizeof...(F)]
   for (int k = 0; k < K; k++) v[k] = red[0][k];
 }
 
-__global__ __launch_bounds__(kFoldBlock) void kv_decide_kernel(StoreView st, const unsigned long long* part,
-                                                               uint32_t walk_blocks,
-                                                               const unsigned long long* set_part, uint32_t blocks,
-                                                               uint64_t* block_base) {
-  unsigned long long v[3] = {0, 0, 0};
-  fold_block<kPCreated, kPNewSlots, kPOverflow>(v, part, walk_blocks, kPCount);
-  unsigned long long w[2] = {0, 0};
-  fold_block<0, 1>(w, set_part, blocks, 2);
-  // exclusive scan of the walk blocks' plan bytes -> block_base; total = the batch's bytes
-  __shared__ unsigned long long s_scan[kFoldBlock];
-  const uint32_t per = (walk_blocks + kFoldBlock - 1) / kFoldBlock;
-  const uint32_t lo = threadIdx.x * per, hi = lo + per < walk_blocks ? lo + per : walk_blocks;
-  unsigned long long run = 0;
-  for (uint32_t q = lo; q < hi; q++) run += part[(uint64_t)q * kPCount + kPNeed];
-  s_scan[threadIdx.x] = run;
+// Multi-workgroup: workgroup g owns walk blocks [64g, 64g + 64) and a share of the
+// decode partials. It folds them (every load in flight at once), scans its walk blocks'
+// plan bytes (block_base = the offset inside the group) and publishes one row of
+// dpart; the last workgroup to arrive folds the rows, scans the group totals into
+// group_base (the commit adds both), picks the path and, on the keyed path, applies
+// the counter deltas (live, version, total_operations: nothing reads them between here
+// and the next batch's decide). Round 4 ran this as one 1024-thread workgroup (20 us
+// per 2^22 commands: a chain of dependent loads on one CU) plus a second fold in the
+// close kernel.
+constexpr int kDecBlock = 256;
+enum { kDCreated = 0, kDNewSlots, kDOverflow, kDSets, kDSetBytes, kDNeed, kDLive, kDVersion, kDOps, kDCount };
+
+__device__ __forceinline__ void dec_store(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long dec_load(const unsigned long long* p) {
+  return __hip_atomic_load(const_cast<unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(kDecBlock) void kv_decide_kernel(StoreView st, const unsigned long long* part,
+                                                              uint32_t walk_blocks, const unsigned long long* set_part,
+                                                              uint32_t blocks, uint64_t* block_base,
+                                                              uint64_t* group_base, unsigned long long* dpart,
+                                                              unsigned long long* arrivals) {
+  __shared__ unsigned long long red[kDecBlock / 64][kDCount];
+  __shared__ uint32_t s_last;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t g = blockIdx.x, D = gridDim.x;
+  unsigned long long v[kDCount] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  if (wave == 0) {  // this group's walk blocks, one per lane: folds + the in-group scan of plan bytes
+    const uint32_t wb = g * kDecGroup + (uint32_t)lane;
+    unsigned long long x[kPCount] = {0, 0, 0, 0, 0, 0, 0};
+    if (wb < walk_blocks)
+#pragma unroll
+      for (int k = 0; k < kPCount; k++) x[k] = part[(uint64_t)wb * kPCount + k];
+    v[kDCreated] = x[kPCreated];
+    v[kDNewSlots] = x[kPNewSlots];
+    v[kDOverflow] = x[kPOverflow];
+    v[kDLive] = x[kPLiveDelta];
+    v[kDVersion] = x[kPVersion];
+    v[kDOps] = x[kPOps];
+    unsigned long long incl = x[kPNeed];  // inclusive scan over the 64 lanes
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned long long t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
+    }
+    if (wb < walk_blocks) block_base[wb] = incl - x[kPNeed];
+    v[kDNeed] = x[kPNeed];
+  }
+  {  // this group's share of the decode partials (pending SETs, their worst-case bytes)
+    const uint32_t per = (blocks + D - 1) / D, r0 = g * per, r1 = r0 + per < blocks ? r0 + per : blocks;
+    for (uint32_t r = r0 + (uint32_t)tid; r < r1; r += kDecBlock) {
+      v[kDSets] += set_part[(uint64_t)r * 2];
+      v[kDSetBytes] += set_part[(uint64_t)r * 2 + 1];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kDCount; k++) {  // (overflow: any nonzero sum)
+    unsigned long long t = v[k];
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+    if (lane == 0) red[wave][k] = t;
+  }
   __syncthreads();
-  for (int o = 1; o < kFoldBlock; o <<= 1) {  // inclusive Hillis-Steele over the thread sums
-    const unsigned long long t = threadIdx.x >= (uint32_t)o ? s_scan[threadIdx.x - o] : 0ull;
+  if (tid < kDCount) {
+    unsigned long long t = 0;
+    for (int w = 0; w < kDecBlock / 64; w++) t += red[w][tid];
+    dec_store(dpart + (uint64_t)g * kDCount + tid, t);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    __threadfence();
+    s_last = atomicAdd(arrivals, 1ull) == D - 1 ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  // the last workgroup: fold every group's row; exclusive scan of the groups' plan bytes
+  const uint32_t per = (D + kDecBlock - 1) / kDecBlock;
+  const uint32_t lo = (uint32_t)tid * per, hi = lo + per < D ? lo + per : D;
+  unsigned long long f[kDCount] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (uint32_t q = lo; q < hi; q++)
+#pragma unroll
+    for (int k = 0; k < kDCount; k++) f[k] += dec_load(dpart + (uint64_t)q * kDCount + k);
+  __shared__ unsigned long long s_scan[kDecBlock];
+  s_scan[tid] = f[kDNeed];
+  __syncthreads();
+  for (int o = 1; o < kDecBlock; o <<= 1) {  // inclusive Hillis-Steele over the thread sums
+    const unsigned long long t = tid >= o ? s_scan[tid - o] : 0ull;
     __syncthreads();
-    s_scan[threadIdx.x] += t;
+    s_scan[tid] += t;
     __syncthreads();
   }
-  unsigned long long off = s_scan[threadIdx.x] - run;
+  unsigned long long off = s_scan[tid] - f[kDNeed];
   for (uint32_t q = lo; q < hi; q++) {
-    block_base[q] = off;
-    off += part[(uint64_t)q * kPCount + kPNeed];
+    group_base[q] = off;
+    off += dec_load(dpart + (uint64_t)q * kDCount + kDNeed);
   }
-  const uint64_t bytes = s_scan[kFoldBlock - 1];
-  if (threadIdx.x != 0) return;
-  const unsigned long long c = v[0], ns = v[1], ov = v[2], sets = w[0], set_bytes = w[1];
+#pragma unroll
+  for (int k = 0; k < kDCount; k++) {
+    unsigned long long t = f[k];
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+    if (lane == 0) red[wave][k] = t;
+  }
+  __syncthreads();
+  if (tid != 0) return;
+  unsigned long long tot[kDCount];
+  for (int k = 0; k < kDCount; k++) {
+    tot[k] = 0;
+    for (int w = 0; w < kDecBlock / 64; w++) tot[k] += red[w][k];
+  }
+  *arrivals = 0;  // for the next batch (stream order)
+  const unsigned long long c = tot[kDCreated], ns = tot[kDNewSlots], ov = tot[kDOverflow], sets = tot[kDSets],
+                           set_bytes = tot[kDSetBytes], bytes = tot[kDNeed];
   KvCounters* k = st.ctr;
   unsigned long long mode = 0;
   // StoreFull unreachable iff live + created <= max_keys (size never exceeds it).
@@ -903,8 +989,11 @@ __global__ __launch_bounds__(kFoldBlock) void kv_decide_kernel(StoreView st, con
   k->batches += 1;
   if (mode == 0) {
     k->occupied += ns;
-    k->batch_base = k->heap_top;  // commit writes [batch_base + block_base[b] + ..., ...)
+    k->batch_base = k->heap_top;  // commit writes [batch_base + group_base + block_base + ..., ...)
     k->heap_top += bytes;
+    k->live += tot[kDLive];  // two's-complement sum of +-1 deltas
+    k->version += tot[kDVersion];
+    k->total_ops += tot[kDOps];
   } else if (mode == 2 && !lost) {
     const bool table = mode == 2 && (k->occupied + (ov || k->live + c > st.max_keys ? sets : ns) > slot_cap);
     k->flags |= table ? kFaultTable : kFaultHeap;
@@ -992,13 +1081,8 @@ __global__ __launch_bounds__(kFoldBlock) void kv_close_kernel(const uint8_t* dat
       if (ops[c].status == kPending) results[c] = RG_KV_E_CAPACITY;
     return;
   }
-  if (mode != 0) return;
-  unsigned long long v[3] = {0, 0, 0};
-  fold_block<kPLiveDelta, kPVersion, kPOps>(v, part, blocks, kPCount);
-  if (threadIdx.x != 0) return;
-  k->live += v[0];  // two's-complement sum of +-1 deltas
-  k->version += v[1];
-  k->total_ops += v[2];
+  (void)part;  // mode 0: the decide kernel applied the keyed path's counter deltas
+  (void)blocks;
 }
 
 // ---- mark applied commands from the phase step's decision plane -----------------
@@ -1479,7 +1563,9 @@ struct rg_kv {
   // per-batch scratch
   uint64_t cap_cmds = 0;
   KvOp* ops = nullptr;
-  uint64_t *need = nullptr, *block_base = nullptr;
+  uint64_t *need = nullptr, *block_base = nullptr, *group_base = nullptr;
+  unsigned long long* dpart = nullptr;     // [decide groups][kDCount] decide rows
+  unsigned long long* arrivals = nullptr;  // decide workgroups arrived (0 between batches)
   uint32_t *key_a = nullptr, *key_b = nullptr, *idx_a = nullptr, *idx_b = nullptr;
   uint32_t* sort_hist = nullptr;           // [L1 chunks][256] digit counts -> offsets
   uint32_t* bin_lo = nullptr;              // [256] L1 bin sizes
@@ -1516,6 +1602,8 @@ void free_scratch(rg_kv* kv) {
   (void)hipFree(kv->need); (void)hipFree(kv->block_base); (void)hipFree(kv->idx_a);
   (void)hipFree(kv->idx_b); (void)hipFree(kv->done); (void)hipFree(kv->part);
   (void)hipFree(kv->set_part); (void)hipFree(kv->recs);
+  (void)hipFree(kv->group_base); (void)hipFree(kv->dpart); (void)hipFree(kv->arrivals);
+  kv->group_base = nullptr; kv->dpart = nullptr; kv->arrivals = nullptr;
   (void)hipFree(kv->sort_hist); (void)hipFree(kv->bin_lo); (void)hipFree(kv->scan_sums);
   kv->set_part = nullptr; kv->recs = nullptr;
   kv->sort_hist = kv->bin_lo = nullptr; kv->scan_sums = nullptr;
@@ -1537,6 +1625,11 @@ int ensure_scratch(rg_kv* kv, uint64_t n) {
   KV_HIP(kv, hipMalloc(&kv->recs, cap * sizeof(KeyRec)));
   KV_HIP(kv, hipMalloc(&kv->need, cap * 8));
   KV_HIP(kv, hipMalloc(&kv->block_base, (cap / kWalkBlockSpan + 1) * 8));
+  const uint64_t groups = cap / kWalkBlockSpan / kDecGroup + 2;
+  KV_HIP(kv, hipMalloc(&kv->group_base, groups * 8));
+  KV_HIP(kv, hipMalloc(&kv->dpart, groups * kDCount * 8));
+  KV_HIP(kv, hipMalloc(&kv->arrivals, 8));
+  KV_HIP(kv, hipMemset(kv->arrivals, 0, 8));
   KV_HIP(kv, hipMalloc(&kv->idx_a, cap * 4));
   KV_HIP(kv, hipMalloc(&kv->idx_b, cap * 4));
   KV_HIP(kv, hipMalloc(&kv->done, cap));
@@ -1678,13 +1771,14 @@ int rg_kv_apply_async(rg_kv* kv, const uint8_t* data_dev, const uint64_t* cmd_of
   KV_HIP(kv, hipGetLastError());
   const bool fin_a = (sa.passes2 & 1u) != 0;
   BatchView b{data_dev, kv->ops, fin_a ? kv->key_a : kv->key_b, fin_a ? kv->idx_a : kv->idx_b, n_cmds, results_dev,
-              kv->done, kv->need, kv->block_base, kv->recs, invalid_bucket, kv->part};
+              kv->done, kv->need, kv->block_base, kv->group_base, kv->recs, invalid_bucket, kv->part};
   const StoreView st = view(kv);
   const uint32_t walk_blocks = (uint32_t)((n_cmds + kWalkBlockSpan - 1) / kWalkBlockSpan);
   hipLaunchKernelGGL(kv_plan_kernel, dim3(walk_blocks), dim3(kBlock), 0, s, b, st);
   KV_HIP(kv, hipGetLastError());
-  hipLaunchKernelGGL(kv_decide_kernel, dim3(1), dim3(kFoldBlock), 0, s, st, kv->part, walk_blocks, kv->set_part,
-                     blocks, kv->block_base);
+  const uint32_t groups = (walk_blocks + kDecGroup - 1) / kDecGroup;
+  hipLaunchKernelGGL(kv_decide_kernel, dim3(groups), dim3(kDecBlock), 0, s, st, kv->part, walk_blocks, kv->set_part,
+                     blocks, kv->block_base, kv->group_base, kv->dpart, kv->arrivals);
   hipLaunchKernelGGL(kv_commit_kernel, dim3(walk_blocks), dim3(kBlock), 0, s, b, st);
   hipLaunchKernelGGL(kv_close_kernel, dim3(1), dim3(kFoldBlock), 0, s, data_dev, kv->ops, n_cmds, results_dev, st,
                      kv->part, walk_blocks);

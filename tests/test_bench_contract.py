@@ -28,7 +28,7 @@ def test_bytes_per_slot():
 
 
 @pytest.mark.parametrize("name,n,slots", [("pmc_c2.json", 5, 1 << 30), ("pmc_c2_sharded.json", 5, 1 << 30),
-                                          ("pmc_c5.json", 9, 1 << 26), ("pmc_c5_sharded.json", 9, 1 << 26)])
+                                          ("pmc_c5.json", 9, 1 << 31), ("pmc_c5_sharded.json", 9, 1 << 31)])
 def test_pmc_records(name, n, slots):
     path = os.path.join(ROOT, "profiles", name)
     with open(path) as f:

@@ -13,11 +13,16 @@
 #     probe_c5[=K]      tools/c5_probe.py, n = 9, K windows of 2^23 (default 32)
 #     ab[=SLOTS]        tools/ab_variants.py (interleaved A/B, AB_DIAGS / RABIA_AB_LIBS from the env)
 #     stamps            tools/lag_stamps.py (per-phase lag-kernel stamps at 2^30)
+#     stamps_shard      the same for the sharded step
+#     shard_probe       tools/shard_step_probe.py (plain vs sharded step alone, 2^30 slots)
 #     latency           tools/latency_1m.py (single 2^20 window)
 #     gloo2             bench.py --gpus 2 --backend gloo (two ranks on the one GPU, a rehearsal)
 #     prof[=ARGS]       rocprofv3 --kernel-trace --stats over bench.py ARGS (default: the C2 line)
 #     pmc[=ARGS]        two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) over bench.py ARGS
 #     sq[=ARGS]         one SQ/GRBM counter pass over bench.py ARGS
+#     pmc_c3            tools/pmc_c3.sh (the C3 cluster kernel's VALU counters, two passes)
+#     prof_c4           rocprofv3 kernel trace over tools/bench_c4.py
+#     bench_sharded_eager   bench_sharded with the exchange enqueued right behind its own step
 #   ARGS use ':' for spaces, e.g. prof=--config:c5:--sharded
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -27,6 +32,9 @@ OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd "$R"
 export PYTHONUNBUFFERED=1
+# the snapshot's prebuilt library as it is (through the /root/repo symlink, so the loader's
+# staleness check against the sources, which may be newer mid-edit, does not rebuild it)
+export RABIA_GPU_LIB=/root/repo/rabia_amd/lib/librabia_gpu.so
 
 run() {  # name seconds command...
   local name=$1 secs=$2
@@ -61,6 +69,7 @@ for step in "$@"; do
   arg=""
   [ "$step" != "$name" ] && arg=${step#*=}
   bargs=${arg//:/ }
+  sfx=$(echo "$arg" | tr -c 'a-zA-Z0-9\n' '_')  # per-argument output names
   case $name in
     tests)
       if [ -n "$arg" ]; then
@@ -78,20 +87,28 @@ for step in "$@"; do
     probe_c5) run "probe_c5_${arg:-32}" 400 python tools/c5_probe.py --n 9 --window-log2 23 --k "${arg:-32}" --diags default:0 ;;
     ab) AB_SLOTS=${arg:-1073741824} AB_ROUNDS=${AB_ROUNDS:-4} run "ab_${arg:-1073741824}" 700 python -u tools/ab_variants.py ;;
     stamps) run stamps 300 python tools/lag_stamps.py ;;
+    stamps_shard) STAMP_SHARD=1 run stamps_shard 300 python tools/lag_stamps.py ;;
+    shard_probe) run shard_probe 300 python tools/shard_step_probe.py ;;
     latency) run latency 300 python tools/latency_1m.py ;;
     gloo2) run gloo2 300 python bench.py --gpus 2 --backend gloo --steps 5 --warmup 2 --no-cpu-baseline ;;
     prof)
-      prof_run "prof" 500 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
+      prof_run "prof$sfx" 500 --kernel-trace --stats -d "$OUT/prof$sfx" -o run --output-format csv -- \
         python3 "$R/bench.py" --no-cpu-baseline --steps 30 --warmup 10 $bargs ;;
     pmc)
-      prof_run pmc_fetch 240 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o pmc --output-format csv -- \
+      prof_run "pmc_fetch$sfx" 240 --pmc FETCH_SIZE -d "$OUT/pmc_fetch$sfx" -o pmc --output-format csv -- \
         python3 "$R/bench.py" --no-cpu-baseline --steps 6 --warmup 2 $bargs
-      prof_run pmc_write 240 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o pmc --output-format csv -- \
+      prof_run "pmc_write$sfx" 240 --pmc WRITE_SIZE -d "$OUT/pmc_write$sfx" -o pmc --output-format csv -- \
         python3 "$R/bench.py" --no-cpu-baseline --steps 6 --warmup 2 $bargs ;;
     sq)
-      prof_run sq 240 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
-        SQ_INSTS_LDS GRBM_GUI_ACTIVE -d "$OUT/sq" -o sq --output-format csv -- \
+      prof_run "sq$sfx" 240 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+        SQ_INSTS_LDS GRBM_GUI_ACTIVE -d "$OUT/sq$sfx" -o sq --output-format csv -- \
         python3 "$R/bench.py" --no-cpu-baseline --steps 3 --warmup 1 $bargs ;;
+    pmc_c3) run pmc_c3 500 bash tools/pmc_c3.sh "$TAG" ;;
+    prof_c4)
+      prof_run prof_c4 500 --kernel-trace --stats -d "$OUT/prof_c4" -o run --output-format csv -- \
+        python3 "$R/tools/bench_c4.py" --no-cpu ;;
+    bench_sharded_eager) run bench_sharded_eager 300 python bench.py --sharded --fixup-eager --steps 20 --warmup 10 \
+      --no-cpu-baseline ;;
     *) echo "unknown step $name"; exit 2 ;;
   esac
 done

@@ -1,6 +1,7 @@
 """Per-phase timing of the persistent lag REF kernel (rg_debug_set bit 4 stamps):
 per workgroup, the time in each phase of its iterations and its start/end times.
-Run on the GPU box: python tools/lag_stamps.py [extra_diag] > gpurun_out/lag_stamps.json"""
+Run on the GPU box: python tools/lag_stamps.py [extra_diag] > gpurun_out/lag_stamps.json
+STAMP_SHARD=1: the sharded step (rg_phase_step_shard_async, draw records) instead."""
 import json
 import os
 import sys
@@ -28,15 +29,23 @@ def main():
     v = torch.empty(((nw + T - 1) // T) * (4 * n + 1) * T, dtype=torch.int32, device="cuda")
     o = torch.empty(((nw + T - 1) // T) * 8 * T, dtype=torch.int32, device="cuda")
     ev.trace_generate_async(N.RG_TRACE_AGREE90, 1, 1, S, T, v.data_ptr(), sp)
+    shard = os.environ.get("STAMP_SHARD", "0") == "1"
+    cap = S // 8
+    rec = torch.empty(cap if shard else 1, dtype=torch.int64, device="cuda")
+    row = torch.zeros(10, dtype=torch.int64, device="cuda")
     torch.cuda.synchronize()
-    out = {}
+    out = {"shard": shard}
     for diag, name in ((extra, "plain"), (extra | 4, "stamped")):
         N.check(ev.lib.rg_debug_set(ev.ctx, diag), ev.ctx)
         ts = []
         for k in range(8):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            ev.phase_step_async(v.data_ptr(), o.data_ptr(), S, T, slot_base=1 + k * S, stream=sp)
+            if shard:
+                ev.phase_step_shard_async(v.data_ptr(), o.data_ptr(), S, T, 1 + k * S, rec.data_ptr(), cap,
+                                          row.data_ptr(), stream=sp)
+            else:
+                ev.phase_step_async(v.data_ptr(), o.data_ptr(), S, T, slot_base=1 + k * S, stream=sp)
             e1.record(stream)
             e1.synchronize()
             ts.append(e0.elapsed_time(e1) * 1000.0)
