@@ -56,7 +56,7 @@ def bytes_per_slot_ref(n: int) -> float:
 def c3_roofline(r, bytes_slot):
     """C3 is VALU-issue bound (per phase 2n keyed scheduler picks per slot + the coin),
     not HBM bound. achieved = VALU wave-instructions per launch (per-slot count from the
-    SQ_INSTS_VALU pass of THIS round's kernel, profiles/r04_pmc_c3.json, tools/pmc_c3.sh)
+    SQ_INSTS_VALU pass of THIS round's kernel, profiles/pmc_c3.json, tools/pmc_c3.sh)
     / the live kernel time; peak = 256 CUs x 4 SIMDs x 1/2 wave64 instruction per cycle
     (a SIMD-32 issues a wave64 VALU instruction over 2 cycles, MI355X_MICROARCH.md "Wave
     scheduling") = 512 per cycle at the 2.4 GHz peak engine clock. The HBM fraction is
@@ -65,12 +65,12 @@ def c3_roofline(r, bytes_slot):
     hbm = r["S"] * bytes_slot / kern_s / 1e9
     out = {"bound": "valu", "achieved": None, "peak": 512 * 2.4, "unit": "G VALU wave-instr/s", "frac": None,
            "traffic": None, "kernel_avg_us": r["kern_ms"] * 1000.0, "hbm_gbs": hbm, "hbm_frac": hbm / HBM_PEAK_GBS}
-    path = os.path.join(ROOT, "profiles", "r04_pmc_c3.json")
+    path = os.path.join(ROOT, "profiles", "pmc_c3.json")
     if os.path.exists(path):
         pmc = json.load(open(path))
         achieved = pmc["valu_wave_instr_per_slot"] * r["S"] / kern_s / 1e9
         out.update(achieved=achieved, frac=achieved / out["peak"], counter_issue_util=pmc["valu_issue_util"],
-                   counter_file="profiles/r04_pmc_c3.json",
+                   counter_file="profiles/pmc_c3.json",
                    note="counter_issue_util = SQ_INSTS_VALU / (512 x GRBM_GUI_ACTIVE/8 cycles): the same ratio at "
                         "the clock the chip actually ran (DVFS); mix_per_slot in the counter file")
     return out
@@ -86,6 +86,8 @@ def parse():
     ap.add_argument("--windows", type=int, default=1024)
     ap.add_argument("--replicas", type=int, default=5)
     ap.add_argument("--sets", type=int, default=3)
+    ap.add_argument("--launch-events", action="store_true",
+                    help="an event pair around every timed launch (costs the stream 6-10 us per step)")
     ap.add_argument("--tile-words", type=int, default=1024,
                     help="slot-tiled plane layout (include/rabia_gpu.h); 0 = planar")
     ap.add_argument("--cpu-threads", type=int, default=0,
@@ -306,6 +308,24 @@ def load_pmc(path: str, n: int, slots: int):
     return None
 
 
+def launch_events(a):
+    """Per-launch timing events inside the timed region, with --launch-events only. An event
+    recorded between two step kernels puts a barrier packet in the stream: 6-10 us per step
+    between back-to-back 2^30-slot steps (tools/gap_probe.py, profiles/r05/gap_probe*). By
+    default the K launches run back to back between the two bracketing events, and the
+    average launch duration is their span / K (it includes the launch gaps: an upper bound
+    on the kernel time, which the committed rocprofv3 summaries sit just below)."""
+    if not a.launch_events:
+        return None
+    return [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+
+
+def launch_ms(evs, total_ms, steps):
+    if evs:
+        return float(np.mean([b.elapsed_time(e) for b, e in evs]))
+    return total_ms / steps
+
+
 def layout(n, S, T):
     nw = (S + 31) // 32
     if T:  # slot-tiled: the planes of each T-word slot tile are contiguous
@@ -348,15 +368,15 @@ def run_single(a, n, S, label):
     for t in range(a.warmup):
         step(t)
     torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    evs = launch_events(a)
     t_begin, t_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t_begin.record(stream)
     for k in range(a.steps):
-        step(a.warmup + k, evs[k])
+        step(a.warmup + k, evs[k] if evs else None)
     t_end.record(stream)
     torch.cuda.synchronize()
     total_ms = t_begin.elapsed_time(t_end)
-    kern_ms = float(np.mean([b.elapsed_time(e) for b, e in evs]))
+    kern_ms = launch_ms(evs, total_ms, a.steps)
     res = res_dev.cpu().numpy().view(np.uint64)
     if int(res[:, 9].max()) != 0:
         raise RuntimeError("device-side protocol fault flagged in a step result")
@@ -467,11 +487,21 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, comm, bitmaps):
                                               base + start, window_slots, rec.data_ptr(), cap, rows[t].data_ptr(),
                                               stream=comp.cuda_stream)
 
+    # comm (the product path): no event in the compute stream. Step t's exchange waits for the
+    # step on the device (a one-thread signal kernel behind the step, a one-thread wait kernel
+    # ahead of the exchange: rg_stream_signal_async / rg_stream_wait_async), and the host waits
+    # for step t - sets' exchange before it reuses that step's buffers (the host runs ahead of
+    # the device by less than `sets` steps; the device queue never waits).
+    flag = torch.zeros(2, dtype=torch.int64, device="cuda")  # [steps signalled, wait fault]
+
     def step(t, evs=None, chain=True):
         votes, out, rec = sets[t % a.sets]
         base = 1 + t * K * window_slots
         if t >= a.sets:  # the output buffers and records of step t - sets must be fixed up first
-            comp.wait_event(e_done[t - a.sets])
+            if comm is not None:
+                e_done[t - a.sets].synchronize()
+            else:
+                comp.wait_event(e_done[t - a.sets])
         if evs is not None:
             evs[0].record(comp)
         if a.backend == "gloo" and world > 1:
@@ -488,7 +518,10 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, comm, bitmaps):
             shard_step(votes, out, rec, base, t)
         if evs is not None:
             evs[1].record(comp)
-        e_main[t].record(comp)
+        if comm is not None:
+            ev.stream_signal_async(flag.data_ptr(), t + 1, comp.cuda_stream)
+        else:
+            e_main[t].record(comp)
         if comm is None:
             with torch.cuda.stream(fix):  # the rows' all-gather
                 fix.wait_event(e_main[t])
@@ -505,7 +538,10 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, comm, bitmaps):
         votes, out, rec = sets[t % a.sets]
         base = 1 + t * K * window_slots
         if comm is not None:  # stages 2-4 + bitmaps: one C-ABI call, RCCL on the device stream
-            fs_stream.wait_event(e_main[t])
+            if fs_stream is comp:
+                pass  # stream order
+            else:
+                ev.stream_wait_async(flag.data_ptr(), t + 1, flag.data_ptr() + 8, fs_stream.cuda_stream)
             ev.shard_exchange_windows_async(K, out.data_ptr(), out_words, S, stride, base + start, base, window_slots,
                                             rec.data_ptr(), cap, rows[t].data_ptr(), result[t].data_ptr(),
                                             bm_all[t].data_ptr() if bitmaps else 0, stream=fs_stream.cuda_stream)
@@ -541,11 +577,11 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, comm, bitmaps):
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    evs = launch_events(a)
     t_begin, t_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t_begin.record(comp)
     for k in range(a.steps):  # (the warm-up's last fix-up is done: the timed chain starts afresh)
-        step(a.warmup + k, evs[k], chain=k > 0)
+        step(a.warmup + k, evs[k] if evs else None, chain=k > 0)
     if defer:
         later(n_total - 1, fs_main)
     comp.wait_event(e_done[n_total - 1])
@@ -554,7 +590,9 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, comm, bitmaps):
     barrier()
     torch.cuda.synchronize()
     total_ms = t_begin.elapsed_time(t_end)
-    kern_ms = float(np.mean([b.elapsed_time(e) for b, e in evs]))
+    kern_ms = launch_ms(evs, total_ms, a.steps)
+    if int(flag[1]) != 0:
+        raise RuntimeError("a device-side stream wait (rg_stream_wait_async) timed out")
     res = result.reshape(-1, 10).cpu().numpy().view(np.uint64)
     fx = fixed.reshape(-1, 10).cpu().numpy().view(np.uint64)
     if int(res[:, 9].max()) != 0 or int(fx[:, 9].max()) != 0:
@@ -637,16 +675,16 @@ def run_c3(a, world, rank, dist, comm):
         step(t)
     torch.cuda.synchronize()
     barrier()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    evs = launch_events(a)
     t_begin, t_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t_begin.record(stream)
     for k in range(a.steps):
-        step(a.warmup + k, evs[k])
+        step(a.warmup + k, evs[k] if evs else None)
     t_end.record(stream)
     torch.cuda.synchronize()
     barrier()
     total_ms = t_begin.elapsed_time(t_end)
-    kern_ms = float(np.mean([b.elapsed_time(e) for b, e in evs]))
+    kern_ms = launch_ms(evs, total_ms, a.steps)
     rows = (g_stats if world > 1 else stats[:, None, :]).cpu().numpy().view(np.uint64)
     decided = 0
     for t in range(a.warmup, n_total):

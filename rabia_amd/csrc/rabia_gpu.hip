@@ -127,8 +127,12 @@ struct Disp {
                          uint64_t base, uint32_t q, uint32_t fp1, Key key, uint64_t cs, uint64_t dseed,
                          uint32_t maxp, uint32_t* info, unsigned long long* part, const uint32_t* coins,
                          uint32_t coin_phases, uint64_t chunk) {
-    hipLaunchKernelGGL((wmvc_cluster_lc_kernel<N>), dim3(grid), dim3(256), 0, s, st, stride, n_slots, base, q, fp1,
-                       key, cs, dseed, maxp, info, part, coins, coin_phases, chunk);
+    if (q == (uint32_t)(N / 2 + 1))  // the majority quorum: the straight-line instantiation
+      hipLaunchKernelGGL((wmvc_cluster_lc_kernel<N, N / 2 + 1>), dim3(grid), dim3(256), 0, s, st, stride, n_slots,
+                         base, q, fp1, key, cs, dseed, maxp, info, part, coins, coin_phases, chunk);
+    else
+      hipLaunchKernelGGL((wmvc_cluster_lc_kernel<N, 0>), dim3(grid), dim3(256), 0, s, st, stride, n_slots, base, q,
+                         fp1, key, cs, dseed, maxp, info, part, coins, coin_phases, chunk);
   }
 };
 
@@ -1007,6 +1011,28 @@ int rg_cluster_trace_async(rg_ctx* ctx, uint64_t seed, uint64_t slot_base, uint6
   hipLaunchKernelGGL(cluster_trace_kernel, dim3((uint32_t)((n_words + 255) / 256)), dim3(256), 0,
                      pick_stream(ctx, stream), (int)ctx->cfg.n_replicas, seed, slot_base, n_slots, stride_words,
                      states_dev);
+  RG_HIP(ctx, hipGetLastError());
+  return RG_OK;
+}
+
+int rg_stream_signal_async(rg_ctx* ctx, uint64_t* flag_dev, uint64_t value, void* stream) {
+  if (!ctx || !flag_dev || (reinterpret_cast<uintptr_t>(flag_dev) & 7u))
+    return fail(ctx, RG_EINVAL, "rg_stream_signal: null context or flag not 8-byte aligned");
+  RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
+  hipLaunchKernelGGL(stream_signal_kernel, dim3(1), dim3(1), 0, pick_stream(ctx, stream),
+                     reinterpret_cast<unsigned long long*>(flag_dev), (unsigned long long)value);
+  RG_HIP(ctx, hipGetLastError());
+  return RG_OK;
+}
+
+int rg_stream_wait_async(rg_ctx* ctx, const uint64_t* flag_dev, uint64_t value, uint64_t* fault_dev, void* stream) {
+  if (!ctx || !flag_dev || (reinterpret_cast<uintptr_t>(flag_dev) & 7u) ||
+      (reinterpret_cast<uintptr_t>(fault_dev) & 7u))
+    return fail(ctx, RG_EINVAL, "rg_stream_wait: null context or flag/fault not 8-byte aligned");
+  RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
+  hipLaunchKernelGGL(stream_wait_kernel, dim3(1), dim3(1), 0, pick_stream(ctx, stream),
+                     reinterpret_cast<const unsigned long long*>(flag_dev), (unsigned long long)value,
+                     reinterpret_cast<unsigned long long*>(fault_dev));
   RG_HIP(ctx, hipGetLastError());
   return RG_OK;
 }

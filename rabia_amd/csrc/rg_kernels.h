@@ -308,6 +308,27 @@ struct SpinBound {
   }
 };
 
+// Stream ordering without events (rg_stream_signal_async / rg_stream_wait_async): an
+// event recorded behind a step kernel puts a barrier packet in the step's queue (6-10 us
+// per step between back-to-back 2^30-slot steps, tools/gap_probe.py); a one-thread
+// kernel that stores a sequence number is dispatched like any other kernel, and the
+// consumer stream spins on the value in a one-thread kernel of its own (bounded).
+static __global__ void stream_signal_kernel(unsigned long long* flag, unsigned long long value) {
+  __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+static __global__ void stream_wait_kernel(const unsigned long long* flag, unsigned long long value,
+                                          unsigned long long* fault) {
+  SpinBound bound;
+  while (__hip_atomic_load(const_cast<unsigned long long*>(flag), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) <
+         value) {
+    if (bound.expired()) {
+      if (fault) atomicOr(fault, 1ull);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(8);
+  }
+}
+
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
@@ -2950,10 +2971,16 @@ static __global__ void coin_table_kernel(Key key, uint64_t stream, uint64_t slot
 // 1..max). Coins come from coin_table_kernel for phases <= coin_phases. The chunk's
 // initial-state words are staged in LDS first (<= kClusterChunk slots: the host sizes
 // the grid for it), so a refill reads LDS instead of waiting on global loads.
+// Q: the quorum as a compile-time constant (the host picks Q = N / 2 + 1, the majority,
+// when the context's quorum is that, else Q = 0 and q at run time). With Q fixed the
+// phase body is straight-line: the 2N heard sets of a phase are independent of each other
+// and of the votes, so the keys' LDS reads, the hashes and the table reads of both rounds
+// are all issued before the first popcount (round 4's body was one dependent LDS round
+// trip after another, per receiver, behind uniform branches on q).
 constexpr uint32_t kClusterChunk = 8192;
-template <int N>
+template <int N, int Q>
 __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* states, uint64_t stride,
-                                                              uint64_t n_slots, uint64_t slot_base, uint32_t q,
+                                                              uint64_t n_slots, uint64_t slot_base, uint32_t q_rt,
                                                               uint32_t fp1, Key ckey, uint64_t coin_stream,
                                                               uint64_t dseed, uint32_t max_phases, uint32_t* info,
                                                               unsigned long long* partials, const uint32_t* coin_tab,
@@ -2966,8 +2993,9 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
   __shared__ uint32_t s_st[N][kStageWords];  // the chunk's initial-state words
   constexpr uint32_t kTabCap = heard_tab_size<N>((uint32_t)N / 2 + 1) ? heard_tab_size<N>((uint32_t)N / 2 + 1) : 1;
   __shared__ uint16_t s_heard[kTabCap];     // heard sets at the majority quorum (heard_mask_tab)
+  const uint32_t q = Q ? (uint32_t)Q : q_rt;
   const uint32_t tab_n = heard_tab_size<N>(q);
-  const bool use_tab = tab_n != 0 && tab_n <= kTabCap;  // (uniform)
+  const bool use_tab = tab_n != 0 && tab_n <= kTabCap;  // (uniform; a constant when Q is)
   const uint64_t n_words = (n_slots + 31) / 32;
   const uint64_t c0 = (uint64_t)blockIdx.x * chunk;
   const uint64_t c1 = c0 + chunk < n_slots ? c0 + chunk : n_slots;
@@ -3020,51 +3048,64 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
     if (!__ballot(active)) break;
     if (!active) continue;
     // ---- one phase of every replica of slot s (same rules as wmvc_cluster_kernel)
+    // the coin word of this phase, loaded ahead (its latency hides behind the heard sets)
+    const bool coin_tabbed = p <= coin_phases;
+    const uint32_t coin_w = coin_tabbed ? coin_tab[(uint64_t)(p - 1) * n_words + s / 32] : 0u;
+    uint32_t ck[2][N];
+    if (p <= kKeyPhases) {
+#pragma unroll
+      for (int rd = 0; rd < 2; rd++)
+#pragma unroll
+        for (int r = 0; r < N; r++) ck[rd][r] = s_ck[p - 1][rd][r];
+    } else {
+#pragma unroll
+      for (int rd = 0; rd < 2; rd++)
+#pragma unroll
+        for (int r = 0; r < N; r++) ck[rd][r] = (uint32_t)cluster_key(dseed, p, (uint32_t)rd + 1, r);
+    }
+    uint32_t hm[2][N];  // heard sets of both rounds: independent of the votes
+#pragma unroll
+    for (int rd = 0; rd < 2; rd++)
+#pragma unroll
+      for (int r = 0; r < N; r++)
+        hm[rd][r] = use_tab ? heard_mask_tab<N>(s_heard, ck[rd][r], s32, r, q) : heard_mask_k<N>(ck[rd][r], s32, r, q);
     uint32_t v1 = 0, vq = 0;
-    const bool tab = p <= kKeyPhases;
 #pragma unroll
     for (int r = 0; r < N; r++) {
-      const uint32_t ck = tab ? s_ck[p - 1][0][r] : (uint32_t)cluster_key(dseed, p, 1, r);
-      const uint32_t h = use_tab ? heard_mask_tab<N>(s_heard, ck, s32, r, q) : heard_mask_k<N>(ck, s32, r, q);
-      const uint32_t c1r = __builtin_popcount(h & st), c0r = __builtin_popcount(h & ~st);
-      if (c1r >= q) v1 |= 1u << r;
-      else if (c0r < q) vq |= 1u << r;
+      const uint32_t c1r = __builtin_popcount(hm[0][r] & st), c0r = __builtin_popcount(hm[0][r] & ~st);
+      v1 |= (uint32_t)(c1r >= q) << r;
+      vq |= (uint32_t)(c1r < q && c0r < q) << r;
     }
-    uint32_t nst = 0;
-    int coin = -1;
+    uint32_t nv1 = 0, need_coin = 0, newly = 0, newv = 0;  // per replica: round-2 vote 1, coin, decides now
 #pragma unroll
     for (int r = 0; r < N; r++) {
-      const uint32_t ck = tab ? s_ck[p - 1][1][r] : (uint32_t)cluster_key(dseed, p, 2, r);
-      const uint32_t h = use_tab ? heard_mask_tab<N>(s_heard, ck, s32, r, q) : heard_mask_k<N>(ck, s32, r, q);
-      const uint32_t c1r = __builtin_popcount(h & v1), cq = __builtin_popcount(h & vq);
+      const uint32_t c1r = __builtin_popcount(hm[1][r] & v1), cq = __builtin_popcount(hm[1][r] & vq);
       const uint32_t c0r = q - c1r - cq;
-      int nv = c0r >= fp1 ? 0 : (c1r >= fp1 ? 1 : -1);
-      if (nv >= 0 && !((decided >> r) & 1u)) {
-        decided |= 1u << r;
-        decv |= (uint32_t)nv << r;
-        if (!first) first = p;
-      }
-      if (nv < 0) {
-        if (c0r > 0) nv = 0;
-        else if (c1r > 0) nv = 1;
-        else {
-          if (coin < 0) {
-            if (p <= coin_phases) {
-              coin = (int)((coin_tab[(uint64_t)(p - 1) * n_words + s / 32] >> (s & 31)) & 1u);
-            } else {
-              uint32_t blk[16];
-              chacha_block<12>(ckey, ((uint64_t)(p - 1) << 40) | (id >> 9), coin_stream, blk);
-              coin = (int)((select16(blk, (uint32_t)(id >> 5) & 15u) >> (id & 31)) & 1u);
-            }
-            coins++;
-          }
-          nv = coin;
-        }
-      }
-      if ((decided >> r) & 1u) nv = (int)((decv >> r) & 1u);
-      nst |= (uint32_t)nv << r;
+      const bool d0 = c0r >= fp1, d1 = !d0 && c1r >= fp1;
+      newly |= (uint32_t)(d0 || d1) << r;
+      newv |= (uint32_t)d1 << r;
+      // undecided this phase: 0 if any 0 was heard, else 1 if any 1, else the coin
+      nv1 |= (uint32_t)(d1 || (!d0 && c0r == 0 && c1r > 0)) << r;
+      need_coin |= (uint32_t)(!d0 && !d1 && c0r == 0 && c1r == 0) << r;
     }
-    st = nst;
+    newly &= ~decided;
+    if (newly && !first) first = p;
+    decided |= newly;
+    decv |= newv & newly;
+    uint32_t nst = nv1;
+    if (need_coin) {  // one coin per slot and phase, counted whenever a replica needs it
+      uint32_t coin;
+      if (coin_tabbed) {
+        coin = (coin_w >> (s & 31)) & 1u;
+      } else {
+        uint32_t blk[16];
+        chacha_block<12>(ckey, ((uint64_t)(p - 1) << 40) | (id >> 9), coin_stream, blk);
+        coin = (select16(blk, (uint32_t)(id >> 5) & 15u) >> (id & 31)) & 1u;
+      }
+      coins++;
+      nst |= coin ? need_coin : 0u;
+    }
+    st = (nst & ~decided) | (decv & decided);
     const bool all = decided == kAll;
     if (all || p >= max_phases) {
       const uint32_t phases = all ? p : 0u;

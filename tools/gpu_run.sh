@@ -23,6 +23,8 @@
 #     pmc_c3            tools/pmc_c3.sh (the C3 cluster kernel's VALU counters, two passes)
 #     prof_c4           rocprofv3 kernel trace over tools/bench_c4.py
 #     bench_sharded_eager   bench_sharded with the exchange enqueued right behind its own step
+#     line=ARGS         bench.py --steps 20 --warmup 10 ARGS (one bench line)
+#     gap | prof_gap    tools/gap_probe.py (gaps between step kernels by stream traffic), plain / under rocprofv3
 #   ARGS use ':' for spaces, e.g. prof=--config:c5:--sharded
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -109,6 +111,11 @@ for step in "$@"; do
         python3 "$R/tools/bench_c4.py" --no-cpu ;;
     bench_sharded_eager) run bench_sharded_eager 300 python bench.py --sharded --fixup-eager --steps 20 --warmup 10 \
       --no-cpu-baseline ;;
+    line) run "line$sfx" 300 python bench.py --steps 20 --warmup 10 $bargs ;;
+    gap) run gap 300 python tools/gap_probe.py ;;
+    prof_gap)
+      prof_run prof_gap 300 --kernel-trace --stats -d "$OUT/prof_gap" -o run --output-format csv -- \
+        python3 "$R/tools/gap_probe.py" ;;
     *) echo "unknown step $name"; exit 2 ;;
   esac
 done
