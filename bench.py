@@ -487,12 +487,12 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, comm, bitmaps):
                                               base + start, window_slots, rec.data_ptr(), cap, rows[t].data_ptr(),
                                               stream=comp.cuda_stream)
 
-    # comm (the product path): no event in the compute stream. Step t's exchange waits for the
-    # step on the device (a one-thread signal kernel behind the step, a one-thread wait kernel
-    # ahead of the exchange: rg_stream_signal_async / rg_stream_wait_async), and the host waits
-    # for step t - sets' exchange before it reuses that step's buffers (the host runs ahead of
-    # the device by less than `sets` steps; the device queue never waits).
-    flag = torch.zeros(2, dtype=torch.int64, device="cuda")  # [steps signalled, wait fault]
+    # comm (the product path): the compute stream carries the step kernels and one event per
+    # step (the exchange's dependency); the host waits for step t - sets' exchange before it
+    # reuses that step's buffers (the host runs ahead of the device by less than `sets` steps),
+    # so the compute queue holds no cross-stream wait. Every packet between two step kernels
+    # costs the stream 6-10 us (an event record 7, a one-thread kernel 6, a wait 5-6:
+    # tools/gap_probe.py, profiles/r05/gap_probe.json); back-to-back step kernels cost 0.
 
     def step(t, evs=None, chain=True):
         votes, out, rec = sets[t % a.sets]
@@ -518,10 +518,7 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, comm, bitmaps):
             shard_step(votes, out, rec, base, t)
         if evs is not None:
             evs[1].record(comp)
-        if comm is not None:
-            ev.stream_signal_async(flag.data_ptr(), t + 1, comp.cuda_stream)
-        else:
-            e_main[t].record(comp)
+        e_main[t].record(comp)
         if comm is None:
             with torch.cuda.stream(fix):  # the rows' all-gather
                 fix.wait_event(e_main[t])
@@ -538,10 +535,7 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, comm, bitmaps):
         votes, out, rec = sets[t % a.sets]
         base = 1 + t * K * window_slots
         if comm is not None:  # stages 2-4 + bitmaps: one C-ABI call, RCCL on the device stream
-            if fs_stream is comp:
-                pass  # stream order
-            else:
-                ev.stream_wait_async(flag.data_ptr(), t + 1, flag.data_ptr() + 8, fs_stream.cuda_stream)
+            fs_stream.wait_event(e_main[t])
             ev.shard_exchange_windows_async(K, out.data_ptr(), out_words, S, stride, base + start, base, window_slots,
                                             rec.data_ptr(), cap, rows[t].data_ptr(), result[t].data_ptr(),
                                             bm_all[t].data_ptr() if bitmaps else 0, stream=fs_stream.cuda_stream)
@@ -591,8 +585,6 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, comm, bitmaps):
     torch.cuda.synchronize()
     total_ms = t_begin.elapsed_time(t_end)
     kern_ms = launch_ms(evs, total_ms, a.steps)
-    if int(flag[1]) != 0:
-        raise RuntimeError("a device-side stream wait (rg_stream_wait_async) timed out")
     res = result.reshape(-1, 10).cpu().numpy().view(np.uint64)
     fx = fixed.reshape(-1, 10).cpu().numpy().view(np.uint64)
     if int(res[:, 9].max()) != 0 or int(fx[:, 9].max()) != 0:

@@ -372,21 +372,6 @@ int rg_cluster_bitmap_async(rg_ctx* ctx, const uint32_t* info_dev, uint64_t n_sl
 int rg_cluster_trace_async(rg_ctx* ctx, uint64_t seed, uint64_t slot_base, uint64_t n_slots,
                            uint64_t stride_words, uint32_t* states_dev, void* stream);
 
-/* Device-side stream ordering for the sharded pipeline's second stream (no reference
- * counterpart: the reference orders its handlers on one task). An event recorded behind a
- * step kernel costs the step's stream a barrier packet, 6-10 us per step between
- * back-to-back 2^30-slot steps; these are one-thread kernels dispatched like any other.
- * rg_stream_signal_async: once the stream's earlier work has completed, stores `value` to
- *   *flag_dev (release, device scope).
- * rg_stream_wait_async: later work on `stream` starts once *flag_dev >= value (acquire),
- *   and sees everything the signalling stream wrote before its signal. Enqueue the wait
- *   after its signal in host order (two streams may share one hardware queue). Bounded:
- *   after 4 s it sets bit 0 of *fault_dev (when not NULL) and returns.
- * flag_dev / fault_dev: 8-byte aligned device words; values should grow monotonically. */
-int rg_stream_signal_async(rg_ctx* ctx, uint64_t* flag_dev, uint64_t value, void* stream);
-int rg_stream_wait_async(rg_ctx* ctx, const uint64_t* flag_dev, uint64_t value, uint64_t* fault_dev,
-                         void* stream);
-
 int rg_stream_sync(rg_ctx* ctx, void* stream);
 
 /* Host-side layout helpers (no device work). */

@@ -106,8 +106,6 @@ _SIGS = {
     "rg_wmvc_cluster_async": (ctypes.c_int, [vp, vp, u64, u64, u64, u64, u32, vp, vp, vp]),
     "rg_cluster_trace_async": (ctypes.c_int, [vp, u64, u64, u64, u64, vp, vp]),
     "rg_cluster_bitmap_async": (ctypes.c_int, [vp, vp, u64, vp, vp, vp]),
-    "rg_stream_signal_async": (ctypes.c_int, [vp, vp, u64, vp]),
-    "rg_stream_wait_async": (ctypes.c_int, [vp, vp, u64, vp, vp]),
     "rg_stream_sync": (ctypes.c_int, [vp, vp]),
     "rg_pack_codes": (ctypes.c_int, [vp, u32, u64, u64, vp]),
     "rg_unpack_planes": (ctypes.c_int, [vp, u32, u64, u64, vp]),

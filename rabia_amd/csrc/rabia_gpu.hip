@@ -1015,28 +1015,6 @@ int rg_cluster_trace_async(rg_ctx* ctx, uint64_t seed, uint64_t slot_base, uint6
   return RG_OK;
 }
 
-int rg_stream_signal_async(rg_ctx* ctx, uint64_t* flag_dev, uint64_t value, void* stream) {
-  if (!ctx || !flag_dev || (reinterpret_cast<uintptr_t>(flag_dev) & 7u))
-    return fail(ctx, RG_EINVAL, "rg_stream_signal: null context or flag not 8-byte aligned");
-  RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
-  hipLaunchKernelGGL(stream_signal_kernel, dim3(1), dim3(1), 0, pick_stream(ctx, stream),
-                     reinterpret_cast<unsigned long long*>(flag_dev), (unsigned long long)value);
-  RG_HIP(ctx, hipGetLastError());
-  return RG_OK;
-}
-
-int rg_stream_wait_async(rg_ctx* ctx, const uint64_t* flag_dev, uint64_t value, uint64_t* fault_dev, void* stream) {
-  if (!ctx || !flag_dev || (reinterpret_cast<uintptr_t>(flag_dev) & 7u) ||
-      (reinterpret_cast<uintptr_t>(fault_dev) & 7u))
-    return fail(ctx, RG_EINVAL, "rg_stream_wait: null context or flag/fault not 8-byte aligned");
-  RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
-  hipLaunchKernelGGL(stream_wait_kernel, dim3(1), dim3(1), 0, pick_stream(ctx, stream),
-                     reinterpret_cast<const unsigned long long*>(flag_dev), (unsigned long long)value,
-                     reinterpret_cast<unsigned long long*>(fault_dev));
-  RG_HIP(ctx, hipGetLastError());
-  return RG_OK;
-}
-
 int rg_stream_sync(rg_ctx* ctx, void* stream) {
   if (!ctx) return fail(nullptr, RG_EINVAL, "rg_stream_sync: null context");
   RG_HIP(ctx, hipSetDevice(ctx->cfg.device));

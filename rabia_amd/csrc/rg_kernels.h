@@ -308,27 +308,6 @@ struct SpinBound {
   }
 };
 
-// Stream ordering without events (rg_stream_signal_async / rg_stream_wait_async): an
-// event recorded behind a step kernel puts a barrier packet in the step's queue (6-10 us
-// per step between back-to-back 2^30-slot steps, tools/gap_probe.py); a one-thread
-// kernel that stores a sequence number is dispatched like any other kernel, and the
-// consumer stream spins on the value in a one-thread kernel of its own (bounded).
-static __global__ void stream_signal_kernel(unsigned long long* flag, unsigned long long value) {
-  __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-}
-static __global__ void stream_wait_kernel(const unsigned long long* flag, unsigned long long value,
-                                          unsigned long long* fault) {
-  SpinBound bound;
-  while (__hip_atomic_load(const_cast<unsigned long long*>(flag), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) <
-         value) {
-    if (bound.expired()) {
-      if (fault) atomicOr(fault, 1ull);
-      return;
-    }
-    __builtin_amdgcn_s_sleep(8);
-  }
-}
-
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }

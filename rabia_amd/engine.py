@@ -435,13 +435,5 @@ class PhaseEvaluator:
         return {"kernel": kind, "shard": bool(buf[1]), "block": buf[2], "words": buf[3], "grid": buf[4],
                 "windows": buf[5]}
 
-    def stream_signal_async(self, flag_ptr: int, value: int, stream=0):
-        """rg_stream_signal_async: *flag = value once `stream`'s earlier work is done."""
-        N.check(self.lib.rg_stream_signal_async(self.ctx, flag_ptr, value, stream or None), self.ctx)
-
-    def stream_wait_async(self, flag_ptr: int, value: int, fault_ptr: int = 0, stream=0):
-        """rg_stream_wait_async: later work on `stream` waits (on the device) for *flag >= value."""
-        N.check(self.lib.rg_stream_wait_async(self.ctx, flag_ptr, value, fault_ptr or None, stream or None), self.ctx)
-
     def sync(self, stream=0):
         N.check(self.lib.rg_stream_sync(self.ctx, stream or None), self.ctx)

@@ -569,3 +569,4 @@ def test_rccl_exchange_world1_equals_one_evaluator(n, K, S, kind):
         g = drv.step(votes.data_ptr(), out_d.data_ptr(), S, stride, 1, 1, S, max_phase=mp)
     assert {k: g[k] for k in RES_CMP} == {k: res_1[0][k] for k in RES_CMP}
     assert torch.equal(out_d[: Sp // 32], out_1[: Sp // 32])
+

@@ -10,11 +10,9 @@ of the sharded pipeline's stream traffic at a time:
             of the step before (the output-buffer reuse dependency)
   shard   the sharded step kernel alone (draw records), no exchange
   evt     plain + a timing event pair around every step (torch events)
-  xkern   xrec with the dependency carried by one-thread kernels instead of events
-            (rg_stream_signal_async behind the step, rg_stream_wait_async on the second stream)
-  xkern_host  xkern + the host waiting, before every step, for the second stream's event
-            of the step before last (the buffer-reuse dependency kept off the device queue)
-  *_dev   the same with events recorded at device scope (rabia_amd.hip_events)
+  xrec_host  xrec + the host waiting, before every step, for the second stream's event of
+            the step before last (the buffer-reuse dependency kept off the device queue:
+            bench.py's sharded pipeline)
 Prints one JSON object."""
 import json
 import os
@@ -27,7 +25,6 @@ import torch  # noqa: E402
 
 from rabia_amd import _native as N  # noqa: E402
 from rabia_amd.engine import PhaseEvaluator  # noqa: E402
-from rabia_amd.hip_events import DevEvent  # noqa: E402
 
 n, T = 5, 1024
 S = int(os.environ.get("PROBE_SLOTS", 1 << 30))
@@ -52,9 +49,7 @@ src = torch.zeros(10, dtype=torch.int64, device="cuda")
 dst = torch.zeros(10, dtype=torch.int64, device="cuda")
 torch.cuda.synchronize()
 out = {"lib": os.environ.get("RABIA_GPU_LIB", "default"), "slots": S, "steps": K}
-MODES = ("plain", "xrec", "xkern", "xboth", "xkern_host", "evt", "shard")
-flag = torch.zeros(2, dtype=torch.int64, device="cuda")  # [sequence, fault]
-seq = 0
+MODES = ("plain", "xrec", "xboth", "xrec_host", "evt", "shard")
 
 
 class TorchEvent:
@@ -70,9 +65,7 @@ class TorchEvent:
 
 for mode in MODES * 2:
     ev = PhaseEvaluator(n, self_lane=n - 1, seed=42, tile_words=T)
-    dev = mode.endswith("_dev")
-    mk = DevEvent if dev else TorchEvent
-    base_mode = mode[:-4] if dev else mode
+    mk, base_mode = TorchEvent, mode
     e_main = [mk() for _ in range(K + 4)]
     e_fix = [mk() for _ in range(K + 4)]
     e_t = [(mk(True), mk(True)) for _ in range(K + 4)]
@@ -84,7 +77,7 @@ for mode in MODES * 2:
         v, o = sets[r % 2]
         if base_mode == "xboth" and r >= 2 and r != 4:
             e_fix[r - 2].wait(comp)
-        if base_mode == "xkern_host" and r >= 2:
+        if base_mode == "xrec_host" and r >= 2:
             e_fix[r - 2].e.synchronize()
         if base_mode == "evt":
             e_t[r][0].record(comp)
@@ -95,14 +88,7 @@ for mode in MODES * 2:
             ev.phase_step_async(v.data_ptr(), o.data_ptr(), S, T, slot_base=1 + r * S, stream=sp)
         if base_mode == "evt":
             e_t[r][1].record(comp)
-        if base_mode in ("xkern", "xkern_host"):
-            seq += 1
-            ev.stream_signal_async(flag.data_ptr(), seq, sp)
-            with torch.cuda.stream(fix):
-                ev.stream_wait_async(flag.data_ptr(), seq, flag.data_ptr() + 8, fix.cuda_stream)
-                dst.copy_(src)
-                e_fix[r].record(fix)
-        if base_mode in ("xrec", "xboth"):
+        if base_mode in ("xrec", "xboth", "xrec_host"):
             e_main[r].record(comp)
             with torch.cuda.stream(fix):
                 e_main[r].wait(fix)
@@ -112,5 +98,4 @@ for mode in MODES * 2:
     torch.cuda.synchronize()
     ev.close()
     out.setdefault(mode, []).append(round(t0.elapsed_time(t1) / K, 5))
-assert int(flag[1]) == 0, "a stream wait timed out"
 print(json.dumps(out))

@@ -24,7 +24,9 @@
 #     prof_c4           rocprofv3 kernel trace over tools/bench_c4.py
 #     bench_sharded_eager   bench_sharded with the exchange enqueued right behind its own step
 #     line=ARGS         bench.py --steps 20 --warmup 10 ARGS (one bench line)
-#     gap | prof_gap    tools/gap_probe.py (gaps between step kernels by stream traffic), plain / under rocprofv3
+#     lib[=PATH]        later steps load another build (repo-relative; no PATH: the in-tree library)
+#     gap[=LIB] | prof_gap    tools/gap_probe.py (gaps between step kernels by stream traffic; LIB: another
+#                       build, repo-relative), plain / under rocprofv3
 #   ARGS use ':' for spaces, e.g. prof=--config:c5:--sharded
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -111,11 +113,16 @@ for step in "$@"; do
         python3 "$R/tools/bench_c4.py" --no-cpu ;;
     bench_sharded_eager) run bench_sharded_eager 300 python bench.py --sharded --fixup-eager --steps 20 --warmup 10 \
       --no-cpu-baseline ;;
+    lib) export RABIA_GPU_LIB="$R/${arg:-rabia_amd/lib/librabia_gpu.so}"; echo "== lib $RABIA_GPU_LIB" ;;
     line) run "line$sfx" 300 python bench.py --steps 20 --warmup 10 $bargs ;;
-    gap) run gap 300 python tools/gap_probe.py ;;
+    gap)
+      if [ -n "$arg" ]; then RABIA_GPU_LIB="$R/$arg" run "gap$sfx" 300 python tools/gap_probe.py
+      else run gap 300 python tools/gap_probe.py; fi ;;
     prof_gap)
-      prof_run prof_gap 300 --kernel-trace --stats -d "$OUT/prof_gap" -o run --output-format csv -- \
-        python3 "$R/tools/gap_probe.py" ;;
+      if [ -n "$arg" ]; then export RABIA_GPU_LIB="$R/$arg"; fi
+      prof_run "prof_gap$sfx" 300 --kernel-trace --stats -d "$OUT/prof_gap$sfx" -o run --output-format csv -- \
+        python3 "$R/tools/gap_probe.py"
+      export RABIA_GPU_LIB=/root/repo/rabia_amd/lib/librabia_gpu.so ;;
     *) echo "unknown step $name"; exit 2 ;;
   esac
 done
