@@ -298,11 +298,14 @@ def cpu_baseline(a, n: int, r: dict) -> dict:
 
 
 def load_pmc(path: str, n: int, slots: int):
+    """HBM bytes per launch from a committed PMC record of this launch size: the file holds
+    one record, or {"records": [...]} for several launch sizes."""
     try:
         with open(path) as f:
             d = json.load(f)
-        if d.get("replicas") == n and d.get("slots_per_launch") == slots:
-            return d.get("hbm_bytes_per_launch")
+        for rec in d.get("records", [d]):
+            if rec.get("replicas") == n and rec.get("slots_per_launch") == slots:
+                return rec.get("hbm_bytes_per_launch")
     except Exception:
         pass
     return None

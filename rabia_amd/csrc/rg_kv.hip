@@ -117,7 +117,7 @@ struct KeyRec {
   uint32_t flags, pad;
 };
 enum : uint32_t { kRecNew = 1, kRecValue = 2, kRecInPlace = 4, kRecVersion = 8, kRecLast = 16 };
-constexpr int kWalkPerLane = 4;                              // sorted positions per walker lane
+constexpr int kWalkPerLane = 2;                              // sorted positions per walker lane
 constexpr int kWalkSpan = 64 * kWalkPerLane;                 // positions per wave
 constexpr int kWalkBlockSpan = kBlock * kWalkPerLane;        // positions per block
 constexpr uint32_t kDecGroup = 64;                           // walk blocks per decide workgroup

@@ -27,23 +27,27 @@ def test_bytes_per_slot():
     assert bench.bytes_per_slot_ref(9) == 5.5
 
 
-@pytest.mark.parametrize("name,n,slots", [("pmc_c2.json", 5, 1 << 30), ("pmc_c2_sharded.json", 5, 1 << 30),
-                                          ("pmc_c5.json", 9, 1 << 31), ("pmc_c5_sharded.json", 9, 1 << 31)])
-def test_pmc_records(name, n, slots):
+@pytest.mark.parametrize("name,n,sizes", [("pmc_c2.json", 5, [1 << 30]), ("pmc_c2_sharded.json", 5, [1 << 30]),
+                                          ("pmc_c5.json", 9, [1 << 31]), ("pmc_c5_sharded.json", 9, [1 << 31, 1 << 28])])
+def test_pmc_records(name, n, sizes):
     path = os.path.join(ROOT, "profiles", name)
     with open(path) as f:
-        d = json.load(f)
-    assert d["replicas"] == n and d["slots_per_launch"] == slots
-    assert d["alg_bytes_per_launch"] == slots * bench.bytes_per_slot_ref(n)
-    # FETCH_SIZE doubled (the gfx950 correction) + WRITE_SIZE, both in KB
-    assert d["hbm_bytes_per_launch"] == 2 * d["fetch_size_kb_median"] * 1024 + d["write_size_kb_median"] * 1024
-    assert d["traffic_over_alg"] == pytest.approx(d["hbm_bytes_per_launch"] / d["alg_bytes_per_launch"])
-    assert 1.0 <= d["traffic_over_alg"] < 1.05
-    assert min(d["dispatches"]) >= 5
-    assert bench.load_pmc(path, n, slots) == d["hbm_bytes_per_launch"]
-    assert bench.load_pmc(path, n + 2, slots) is None
-    assert bench.load_pmc(path, n, slots // 2) is None
-    assert bench.load_pmc(path + ".missing", n, slots) is None
+        recs = json.load(f)
+    recs = recs.get("records", [recs])
+    assert sorted(d["slots_per_launch"] for d in recs) == sorted(sizes)
+    for d in recs:
+        slots = d["slots_per_launch"]
+        assert d["replicas"] == n
+        assert d["alg_bytes_per_launch"] == slots * bench.bytes_per_slot_ref(n)
+        # FETCH_SIZE doubled (the gfx950 correction) + WRITE_SIZE, both in KB
+        assert d["hbm_bytes_per_launch"] == 2 * d["fetch_size_kb_median"] * 1024 + d["write_size_kb_median"] * 1024
+        assert d["traffic_over_alg"] == pytest.approx(d["hbm_bytes_per_launch"] / d["alg_bytes_per_launch"])
+        assert 1.0 <= d["traffic_over_alg"] < 1.05
+        assert min(d["dispatches"]) >= 5
+        assert bench.load_pmc(path, n, slots) == d["hbm_bytes_per_launch"]
+        assert bench.load_pmc(path, n + 2, slots) is None
+        assert bench.load_pmc(path, n, slots // 2) is None
+        assert bench.load_pmc(path + ".missing", n, slots) is None
 
 
 def test_layout():

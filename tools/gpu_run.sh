@@ -9,7 +9,7 @@
 #     bench             bench.py (C2 headline, CPU leg included)
 #     bench_sharded     bench.py --sharded (the N > 1 per-GPU pipeline on one GPU, RCCL world 1)
 #     c3 | c5 | c5_sharded   bench.py --config ...
-#     c4                tools/bench_c4.py (kvstore apply)
+#     c4[=NAME]         tools/bench_c4.py (kvstore apply; NAME: an A/B label, no CPU leg)
 #     probe_c5[=K]      tools/c5_probe.py, n = 9, K windows of 2^23 (default 32)
 #     ab[=SLOTS]        tools/ab_variants.py (interleaved A/B, AB_DIAGS / RABIA_AB_LIBS from the env)
 #     stamps            tools/lag_stamps.py (per-phase lag-kernel stamps at 2^30)
@@ -87,7 +87,9 @@ for step in "$@"; do
     c3) run c3 300 python bench.py --config c3 --steps 10 --warmup 3 --no-cpu-baseline ;;
     c5) run c5 300 python bench.py --config c5 --steps 20 --warmup 10 ;;
     c5_sharded) run c5_sharded 300 python bench.py --config c5 --sharded --steps 20 --warmup 10 ;;
-    c4) run c4 300 python tools/bench_c4.py ;;
+    c4)
+      if [ -n "$arg" ]; then run "c4_$sfx" 300 python tools/bench_c4.py --no-cpu
+      else run c4 300 python tools/bench_c4.py; fi ;;
     probe_c5) run "probe_c5_${arg:-32}" 400 python tools/c5_probe.py --n 9 --window-log2 23 --k "${arg:-32}" --diags default:0 ;;
     ab) AB_SLOTS=${arg:-1073741824} AB_ROUNDS=${AB_ROUNDS:-4} run "ab_${arg:-1073741824}" 700 python -u tools/ab_variants.py ;;
     stamps) run stamps 300 python tools/lag_stamps.py ;;
