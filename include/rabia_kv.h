@@ -26,6 +26,13 @@
  * Value bytes are allocated in size classes (powers of two >= 16): a SET whose value
  * fits its key's current allocation overwrites it in place, so updates of existing
  * keys never grow the heap; only new keys and outgrown values take heap bytes.
+ *
+ * Paths of a batch (rg_kv_stats.last_path), all exact: 0 keyed (StoreFull cannot
+ * fire: live + keys created <= max_keys); 3 keyed with the creates ranked (StoreFull
+ * can fire, no DELETE meets a live key: the live count only grows, so a create
+ * succeeds iff fewer than max_keys - live creates precede it in command order); 1
+ * ordered replay, one thread (StoreFull can fire and a DELETE frees a key mid-batch,
+ * or a hash run holds more than 8 keys); 2 refused (capacity).
  */
 #ifndef RABIA_KV_H
 #define RABIA_KV_H
@@ -82,7 +89,8 @@ typedef struct rg_kv_stats {
                                 treat the store as lost; the bit stays set and every
                                 later batch is refused (results RG_KV_E_CAPACITY)      */
   uint64_t last_path;        /* the last batch: 0 keyed replay, 1 ordered replay,
-                                2 refused (capacity fault, results RG_KV_E_CAPACITY)     */
+                                2 refused (capacity fault, results RG_KV_E_CAPACITY),
+                                3 keyed replay with the creates ranked (StoreFull)     */
 } rg_kv_stats;
 
 int rg_kv_create(rg_kv** out, const rg_kv_config* cfg);

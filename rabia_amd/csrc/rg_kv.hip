@@ -10,21 +10,22 @@
 //   2 sort      stable sort of the applied commands by bucket (two levels of 8-bit
 //               counting passes, hand-written): each key's commands become one
 //               contiguous run, still in total order; the rest sort last
-//   3 plan      wave per 1024 sorted positions, decoded fields staged in LDS; run
+//   3 plan      workgroup per 512 sorted positions, decoded fields staged in LDS; run
 //               heads compacted per wave, each lane replays one key's commands in
 //               order (one table lookup per key), writes the result bytes and a
 //               per-key commit record (slot, version, key/value sources, in-place or
 //               new allocation); multi-key runs (bucket or hash collisions) take a
 //               general path over global memory
-//   4 decide    one 1024-thread block folds the plan partials: can StoreFull (the
-//               only cross-key dependency: store.rs:153-158 reads data.len()) occur?
-//               live + keys created <= max_keys => no, the keyed replay is exact;
-//               capacity refusal; exclusive scan of the heap bytes
+//   4 decide    workgroups of 64 walk blocks fold the plan partials, the last to
+//               arrive folds theirs: can StoreFull (the only cross-key dependency:
+//               store.rs:153-158 reads data.len()) occur? live + keys created <=
+//               max_keys => no, the keyed replay is exact; capacity refusal; scan of
+//               the heap bytes (group and block bases); the keyed path's counters
 //   5 commit    lookup-free write pass over the commit records: table claims for new
-//               keys, key/value bytes at the scanned heap offsets, entry fields
-//   6 close     one launch: the ordered replay (one thread, only when StoreFull can
-//               fire: exact, slow, counted in rg_kv_stats.ordered_batches), the
-//               counter fold, or the refusal results
+//               keys, key/value bytes at the scanned heap offsets, entry fields; the
+//               same launch runs the ordered replay instead (one thread, only when
+//               StoreFull can fire: exact, slow, counted in
+//               rg_kv_stats.ordered_batches) or writes the refusal results
 // Key equality is byte equality (hash runs are split by comparing key bytes).
 // Deleted keys keep their table slot (version 0 = not live) so probe chains stay
 // intact; a later SET of the same key reuses it with a fresh ValueEntry (version 1).
@@ -97,12 +98,15 @@ __device__ __forceinline__ uint64_t kv_val_off(const KvOp& op) { return op.key_o
 struct KvCounters {
   unsigned long long live, version, total_ops, occupied, heap_top;
   unsigned long long batches, ordered, flags;
-  unsigned long long mode;        // per batch: 0 keyed commit, 1 ordered replay, 2 fault
+  unsigned long long mode;        // per batch: 0 keyed commit, 1 ordered replay, 2 fault, 3 capacity-ranked
   unsigned long long batch_base;  // heap top before the batch (keyed commit offsets)
+  unsigned long long cut;         // mode 3: command index of the first create StoreFull refuses
 };
 
-// Per-block partials of the plan walk.
-enum { kPCreated = 0, kPNewSlots, kPOverflow, kPLiveDelta, kPVersion, kPOps, kPNeed, kPCount };
+// Per-block partials of the plan walk. kPLiveDel: DELETEs that hit a live key (the
+// all-succeed replay); none in a batch => the live count only grows (mode 3).
+enum { kPCreated = 0, kPNewSlots, kPOverflow, kPLiveDelta, kPVersion, kPOps, kPNeed, kPLiveDel, kPCount };
+constexpr uint32_t kNoCreate = 0xFFFFFFFFu;
 
 // What the commit writes for one key, decided by the plan (one record per distinct
 // key of a hash run, at the run head's sorted position + the key's rank in the run).
@@ -114,13 +118,14 @@ struct KeyRec {
   uint64_t val_src;     // batch data offset of the final value
   uint64_t val_dst;     // heap offset of the slot's current value (in-place write)
   uint32_t key_len, val_len;
-  uint32_t flags, pad;
+  uint32_t flags;
+  uint32_t create;      // command index of the SET that creates the key (kNoCreate: none)
 };
 enum : uint32_t { kRecNew = 1, kRecValue = 2, kRecInPlace = 4, kRecVersion = 8, kRecLast = 16 };
 constexpr int kWalkPerLane = 2;                              // sorted positions per walker lane
 constexpr int kWalkSpan = 64 * kWalkPerLane;                 // positions per wave
 constexpr int kWalkBlockSpan = kBlock * kWalkPerLane;        // positions per block
-constexpr uint32_t kDecGroup = 64;                           // walk blocks per decide workgroup
+constexpr uint32_t kDecGroup = 256;                          // walk blocks per decide workgroup (one per thread)
 
 __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
   k ^= k >> 33; k *= 0xff51afd7ed558ccdull;
@@ -282,13 +287,15 @@ __device__ __forceinline__ bool eq_fast(const uint8_t* a, const uint8_t* b, uint
 constexpr uint32_t kFastKey = 16, kFastVal = 64;  // decode fast path: key <= 16 B, value region <= 64 B
 
 // ---- 1 decode ----------------------------------------------------------------
+constexpr int kSetPart = 3;  // decode partials per block: pending SETs, their worst-case bytes, pending DELETEs
 __global__ __launch_bounds__(kBlock) void kv_decode_kernel(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ off, uint64_t n, const uint8_t* __restrict__ mask,
     uint64_t max_value, uint64_t hmask, uint64_t bmask, uint32_t invalid_bucket, KvOp* __restrict__ ops,
     uint32_t* __restrict__ sort_key, uint8_t* __restrict__ results,
-    unsigned long long* __restrict__ set_part, uint8_t* __restrict__ done) {
+    unsigned long long* __restrict__ set_part, uint8_t* __restrict__ done, uint32_t* __restrict__ cbits,
+    unsigned long long* __restrict__ cbytes) {
   const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  unsigned long long sets = 0, set_bytes = 0;  // worst-case growth of the batch (the refusal check)
+  unsigned long long sets = 0, set_bytes = 0, dels = 0;  // worst-case growth of the batch (the refusal check)
   if (c < n) {
   KvOp op{0, kInvalidKey, 0, 0, 0, kPending};
   uint64_t key = kInvalidKey;
@@ -368,24 +375,30 @@ __global__ __launch_bounds__(kBlock) void kv_decode_kernel(
   ops[c] = op;
   sort_key[c] = key == kInvalidKey ? invalid_bucket : (uint32_t)hash_bucket(key, bmask);
   done[c] = 0;  // the plan's per-sorted-position marks (multi-key runs), cleared here: no memset launch
+  if (cbits) {  // the create bitmap and reservations (when StoreFull can fire), likewise
+    if ((c & 31u) == 0) cbits[c >> 5] = 0;
+    cbytes[c] = 0;
+  }
   if (op.status != kPending) results[c] = (uint8_t)op.status;
   if (op.status == kPending && op.kind == 0) {
     sets = 1;
     set_bytes = op.key_len + val_class(op.val_len);
   }
+  dels = op.status == kPending && op.kind == 2;
   }
-  __shared__ unsigned long long red[kBlock / 64][2];
+  __shared__ unsigned long long red[kBlock / 64][3];
   for (int o = 32; o > 0; o >>= 1) {
     sets += __shfl_xor(sets, o, 64);
     set_bytes += __shfl_xor(set_bytes, o, 64);
+    dels += __shfl_xor(dels, o, 64);
   }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) { red[wave][0] = sets; red[wave][1] = set_bytes; }
+  if (lane == 0) { red[wave][0] = sets; red[wave][1] = set_bytes; red[wave][2] = dels; }
   __syncthreads();
-  if (threadIdx.x < 2) {
+  if (threadIdx.x < kSetPart) {
     unsigned long long t = 0;
     for (int w = 0; w < kBlock / 64; w++) t += red[w][threadIdx.x];
-    set_part[(uint64_t)blockIdx.x * 2 + threadIdx.x] = t;
+    set_part[(uint64_t)blockIdx.x * kSetPart + threadIdx.x] = t;
   }
 }
 
@@ -458,6 +471,8 @@ struct BatchView {
   KeyRec* recs;           // per sorted position: plan -> commit records (run head + key rank)
   uint32_t invalid_bucket;  // sort key of the commands that are not applied (sorted last)
   unsigned long long* part;  // [blocks][kPCount]
+  uint32_t* cbits;           // creates by command index (one bit each), NULL when StoreFull cannot fire
+  unsigned long long* cbytes;  // per command: heap bytes its key reserves when it is the key's create
 };
 
 __device__ __forceinline__ bool same_key(const BatchView& b, const KvOp& x, const KvOp& y) {
@@ -469,13 +484,15 @@ struct KeyOutcome {
   bool live0, live1, wrote_value, any_set;
   uint64_t ver0, ver1;
   uint32_t last_set;     // command index of the final value's SET
-  uint64_t n_ops, n_version;
+  uint32_t first_create; // command index of the first SET on a non-live key (kNoCreate: none)
+  uint64_t n_ops, n_version, n_live_del;
 };
 
 __device__ __forceinline__ KeyOutcome key_start(int64_t slot, const KvEntry& e) {
   KeyOutcome o{};
   o.live0 = o.live1 = slot >= 0 && e.version > 0;
   o.ver0 = o.ver1 = o.live0 ? e.version : 0;
+  o.first_create = kNoCreate;
   return o;
 }
 
@@ -483,6 +500,7 @@ __device__ __forceinline__ KeyOutcome key_start(int64_t slot, const KvEntry& e) 
 __device__ __forceinline__ uint8_t key_step(KeyOutcome& o, uint32_t kind, uint32_t c, uint32_t notify) {
   uint8_t r;
   if (kind == 0) {                    // SET: update or insert (store.rs:151-163)
+    if (!o.live1 && o.first_create == kNoCreate) o.first_create = c;
     o.ver1 = o.live1 ? o.ver1 + 1 : 1;
     o.live1 = true;
     o.wrote_value = true;
@@ -495,6 +513,7 @@ __device__ __forceinline__ uint8_t key_step(KeyOutcome& o, uint32_t kind, uint32
     if (o.live1) {
       o.n_version += notify;
       o.wrote_value = false;
+      o.n_live_del++;
     }
     o.live1 = false;
     o.ver1 = 0;
@@ -508,9 +527,13 @@ __device__ __forceinline__ uint8_t key_step(KeyOutcome& o, uint32_t kind, uint32
 // Folds a replayed key into the block partials and its commit record; returns the
 // heap bytes the commit will take for it (new key bytes + a new value allocation).
 // (vsrc, vlen: the final value's bytes, from the SET the replay recorded in last_set.)
+// (create: the command index of the key's first create, o.first_create translated by
+// the caller; its bit goes to the create bitmap when StoreFull can fire.)
 __device__ uint64_t plan_key(const KeyOutcome& o, int64_t slot, const KvEntry& e, uint64_t key_off,
-                             uint32_t key_len, uint64_t vsrc, uint32_t vlen, uint64_t hl,
-                             unsigned long long (&acc)[kPCount], KeyRec& r) {
+                             uint32_t key_len, uint64_t vsrc, uint32_t vlen, uint64_t hl, uint32_t create,
+                             uint32_t* cbits, unsigned long long* cbytes, unsigned long long (&acc)[kPCount],
+                             KeyRec& r) {
+  acc[kPLiveDel] += o.n_live_del;
   acc[kPOps] += o.n_ops;
   acc[kPVersion] += o.n_version;
   acc[kPLiveDelta] += (unsigned long long)((int64_t)o.live1 - (int64_t)o.live0);
@@ -534,8 +557,13 @@ __device__ uint64_t plan_key(const KeyOutcome& o, int64_t slot, const KvEntry& e
   r.val_len = vlen;
   r.flags = (new_slot ? kRecNew : 0u) | (value ? kRecValue : 0u) | (in_place ? kRecInPlace : 0u) |
             ((slot >= 0 || new_slot) && (o.any_set || o.live0 != o.live1) ? kRecVersion : 0u);
-  r.pad = 0;
-  return (new_slot ? key_len : 0) + (value && !in_place ? val_class(vlen) : 0);
+  r.create = create;
+  const uint64_t need = (new_slot ? key_len : 0) + (value && !in_place ? val_class(vlen) : 0);
+  if (cbits && create != kNoCreate) {  // StoreFull reachable: the create's bit and the key's reservation
+    atomicOr(cbits + (create >> 5), 1u << (create & 31u));
+    cbytes[create] = need;
+  }
+  return need;
 }
 
 __device__ __forceinline__ void block_add_partials(unsigned long long (&v)[kPCount],
@@ -607,7 +635,7 @@ __global__ __launch_bounds__(kBlock) void kv_plan_kernel(BatchView b, StoreView 
   __shared__ uint32_t s_klen[kWalkBlockSpan];
   __shared__ uint32_t s_vlen[kWalkBlockSpan];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  unsigned long long acc[kPCount] = {0, 0, 0, 0, 0, 0, 0};
+  unsigned long long acc[kPCount] = {0, 0, 0, 0, 0, 0, 0, 0};
   const uint64_t bbase = (uint64_t)blockIdx.x * kWalkBlockSpan;
   const uint32_t wl = (uint32_t)wave * kWalkSpan;
   if (b.skey[bbase] == b.invalid_bucket) {  // the sorted tail of commands not applied: nothing to plan
@@ -691,7 +719,8 @@ __global__ __launch_bounds__(kBlock) void kv_plan_kernel(BatchView b, StoreView 
         b.results[s_c[q]] = key_step(o, s_inf[q] & 3u, q, st.notify);
       const uint32_t ls = o.last_set;
       KeyRec r;
-      need = plan_key(o, slot, e, koff, klen, s_koff[ls] + s_klen[ls] + 8, s_vlen[ls], hl, acc, r);
+      need = plan_key(o, slot, e, koff, klen, s_koff[ls] + s_klen[ls] + 8, s_vlen[ls], hl,
+                      o.first_create == kNoCreate ? kNoCreate : s_c[o.first_create], b.cbits, b.cbytes, acc, r);
       r.flags |= kRecLast;
       b.recs[i] = r;
     } else {       // general: split the bucket run into keys by their bytes
@@ -727,7 +756,8 @@ __global__ __launch_bounds__(kBlock) void kv_plan_kernel(BatchView b, StoreView 
           vsrc = kv_val_off(v);
           vlen = v.val_len;
         }
-        need += plan_key(o, slot, e, lead.key_off, lead.key_len, vsrc, vlen, hl, acc, r);
+        need += plan_key(o, slot, e, lead.key_off, lead.key_len, vsrc, vlen, hl, o.first_create, b.cbits, b.cbytes,
+                         acc, r);
       }
       if (keys) {
         r.flags |= kRecLast;
@@ -740,17 +770,79 @@ __global__ __launch_bounds__(kBlock) void kv_plan_kernel(BatchView b, StoreView 
   block_add_partials(acc, b.part);
 }
 
+__device__ void kv_ordered(const uint8_t* data, const KvOp* ops, uint64_t n, uint8_t* results, StoreView st);
+
+// Mode 3, a key whose create StoreFull refuses (its create's command index >= the cut):
+// from the create on, the key stays absent (store.rs:153-158: the SET fails, no later
+// command of the batch deletes a live key), so its SETs answer StoreFull and its GETs /
+// EXISTS NotFound. Its commands are the bucket run's (one key) or, in a run of several
+// keys, those with its hash and key bytes. The counters lose what the all-succeed
+// replay counted for it: the live key, the slot of a new key, and per refused SET one
+// operation and (notifications on) one version.
+struct RefuseCorr {
+  unsigned long long live, occupied, ops, version;
+};
+__device__ void refuse_key(const BatchView& b, uint64_t i, const KeyRec& r, bool one_key, uint32_t notify,
+                           RefuseCorr& corr) {
+  const uint32_t bucket = b.skey[i];
+  for (uint64_t q = i; q < b.n && b.skey[q] == bucket; q++) {
+    const uint32_t c = b.sidx[q];
+    if (c < r.create) continue;  // before the create the key is absent either way
+    const KvOp op = b.ops[c];
+    if (!one_key && !(op.hash == r.hash && op.key_len == r.key_len &&
+                      bytes_eq(b.data + op.key_off, b.data + r.key_src, r.key_len)))
+      continue;
+    if (op.kind == 0) {
+      b.results[c] = RG_KV_E_FULL;
+      corr.ops++;
+      corr.version += notify;
+    } else {
+      b.results[c] = RG_KV_NOT_FOUND;
+    }
+  }
+  corr.live++;
+  corr.occupied += (r.flags & kRecNew) ? 1u : 0u;
+}
+
+// The commit launch also closes the batch on the other two paths decide may pick (one
+// launch fewer per batch than a separate close kernel): mode 1, the exact in-order
+// replay (one thread); mode 2, the refusal (every pending command gets
+// RG_KV_E_CAPACITY, grid-stride). Mode 3 is mode 0 with the keys whose create is
+// refused left out (refuse_key).
 __global__ __launch_bounds__(kBlock) void kv_commit_kernel(BatchView b, StoreView st) {
   __shared__ uint16_t s_heads[kBlock / 64][kWalkSpan];
   __shared__ unsigned long long s_wsum[kBlock / 64];
-  if (st.ctr->mode != 0) return;  // uniform over the grid
+  const unsigned long long mode = st.ctr->mode;  // uniform over the grid
+  if (mode == 1) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) kv_ordered(b.data, b.ops, b.n, b.results, st);
+    return;
+  }
+  if (mode == 2) {
+    for (uint64_t c = (uint64_t)blockIdx.x * kBlock + threadIdx.x; c < b.n; c += (uint64_t)gridDim.x * kBlock)
+      if (b.ops[c].status == kPending) b.results[c] = RG_KV_E_CAPACITY;
+    return;
+  }
   if (b.skey[(uint64_t)blockIdx.x * kWalkBlockSpan] == b.invalid_bucket) return;  // no heads in the tail
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t wbase = (uint64_t)blockIdx.x * kWalkBlockSpan + (uint64_t)wave * kWalkSpan;
   const uint32_t nh = collect_heads(b, wbase, lane, true, s_heads[wave]);
+  const unsigned long long cut = mode == 3 ? st.ctr->cut : ~0ull;
   // this lane's heap offset: block base + exclusive prefix of plan sizes over (wave, lane)
+  // (mode 3: the sizes of the keys that are not refused, and the workgroup's base from
+  // one atomic on the heap top: the decide scan counted the refused keys too)
   unsigned long long mine = 0;
-  for (uint32_t h = lane; h < nh; h += 64) mine += b.need[wbase + s_heads[wave][h]];
+  if (mode == 3) {
+    for (uint32_t h = lane; h < nh; h += 64)
+      for (uint64_t k = wbase + s_heads[wave][h]; k < b.n; k++) {
+        const KeyRec r = b.recs[k];
+        if (!(r.create != kNoCreate && r.create >= cut))
+          mine += (r.flags & kRecNew) ? r.key_len + val_class(r.val_len)
+                                      : ((r.flags & kRecValue) && !(r.flags & kRecInPlace) ? val_class(r.val_len) : 0);
+        if (r.flags & kRecLast) break;
+      }
+  } else {
+    for (uint32_t h = lane; h < nh; h += 64) mine += b.need[wbase + s_heads[wave][h]];
+  }
   unsigned long long incl = mine;
   for (int o = 1; o < 64; o <<= 1) {
     const unsigned long long t = __shfl_up(incl, o, 64);
@@ -760,8 +852,19 @@ __global__ __launch_bounds__(kBlock) void kv_commit_kernel(BatchView b, StoreVie
   __syncthreads();
   unsigned long long before = 0;
   for (int w = 0; w < wave; w++) before += s_wsum[w];
-  uint64_t heap_pos = st.ctr->batch_base + b.group_base[blockIdx.x / kDecGroup] + b.block_base[blockIdx.x] + before +
-                      incl - mine;
+  __shared__ unsigned long long s_base;
+  if (mode == 3) {
+    if (threadIdx.x == 0) {
+      unsigned long long tot = 0;
+      for (int w = 0; w < kBlock / 64; w++) tot += s_wsum[w];
+      s_base = tot ? atomicAdd(&st.ctr->heap_top, tot) : 0ull;
+    }
+    __syncthreads();
+  }
+  uint64_t heap_pos = (mode == 3 ? s_base
+                                 : st.ctr->batch_base + b.group_base[blockIdx.x / kDecGroup] + b.block_base[blockIdx.x]) +
+                      before + incl - mine;
+  RefuseCorr corr{0, 0, 0, 0};
   for (uint32_t h = lane; h < nh; h += 64) {
     const uint64_t i = wbase + s_heads[wave][h];
     // a run holds at most kMaxRunKeys records (more sends the batch to the ordered
@@ -769,6 +872,11 @@ __global__ __launch_bounds__(kBlock) void kv_commit_kernel(BatchView b, StoreVie
     for (uint64_t k = i; k < b.n && k < i + kMaxRunKeys; k++) {
       const KeyRec r = b.recs[k];
       int64_t s = r.slot;
+      if (r.create != kNoCreate && r.create >= cut) {  // mode 3: StoreFull refuses this key's create
+        refuse_key(b, i, r, k == i && (r.flags & kRecLast), st.notify, corr);
+        if (r.flags & kRecLast) break;
+        continue;
+      }
       if (r.flags & kRecNew) {  // a new key always ends live with a value: the whole entry at once
         s = table_claim(st.hashes, st.mask, r.hash);
         const uint64_t koff = heap_pos, voff = heap_pos + r.key_len;
@@ -811,64 +919,44 @@ __global__ __launch_bounds__(kBlock) void kv_commit_kernel(BatchView b, StoreVie
       if (r.flags & kRecLast) break;
     }
   }
+  if (mode != 3) return;  // (uniform)
+  unsigned long long v[4] = {corr.live, corr.occupied, corr.ops, corr.version};
+#pragma unroll
+  for (int q = 0; q < 4; q++)
+    for (int o = 32; o > 0; o >>= 1) v[q] += __shfl_xor(v[q], o, 64);
+  __shared__ unsigned long long s_corr[kBlock / 64][4];
+  if (lane == 0)
+    for (int q = 0; q < 4; q++) s_corr[wave][q] = v[q];
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    unsigned long long t = 0;
+    for (int w = 0; w < kBlock / 64; w++) t += s_corr[w][threadIdx.x];
+    unsigned long long* dst[4] = {&st.ctr->live, &st.ctr->occupied, &st.ctr->total_ops, &st.ctr->version};
+    if (t) atomicAdd(dst[threadIdx.x], ~t + 1ull);  // subtract (two's complement)
+  }
 }
 
 // ---- 4 decide ----------------------------------------------------------------
-// One 1024-thread block folds the per-block partials (8 loads per thread in
-// flight, wave shuffles, one LDS step) and picks the batch's path:
+// Folds the plan partials and picks the batch's path:
 //   0 keyed commit: StoreFull unreachable (live + keys created <= max_keys);
 //   1 ordered replay: exact in-order path;
 //   2 refused: a capacity (table slots or heap bytes) cannot hold the batch's
 //     worst case — nothing is written, every pending command gets RG_KV_E_CAPACITY.
-constexpr int kFoldBlock = 1024;
-template <int... F>
-__device__ __forceinline__ void fold_block(unsigned long long (&v)[sizeof...(F)], const unsigned long long* src,
-                                           uint32_t rows, uint32_t stride) {
-  constexpr int K = sizeof...(F);
-  constexpr int field[K] = {F...};
-  for (uint32_t r0 = threadIdx.x; r0 < rows; r0 += kFoldBlock * 8) {
-    unsigned long long x[8][K];
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-      const uint32_t r = r0 + (uint32_t)u * kFoldBlock;
-#pragma unroll
-      for (int k = 0; k < K; k++) x[u][k] = r < rows ? src[(uint64_t)r * stride + field[k]] : 0ull;
-    }
-#pragma unroll
-    for (int u = 0; u < 8; u++)
-#pragma unroll
-      for (int k = 0; k < K; k++) v[k] = field[k] == kPOverflow ? (v[k] | x[u][k]) : v[k] + x[u][k];
-  }
-  __shared__ unsigned long long red[kFoldBlock / 64][K];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int k = 0; k < K; k++) {
-    unsigned long long t = v[k];
-    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);  // overflow flags: any nonzero sum
-    if (lane == 0) red[wave][k] = t;
-  }
-  __syncthreads();
-  if (threadIdx.x < (uint32_t)K) {  // column k folded by thread k
-    unsigned long long t = 0;
-    for (int w = 0; w < kFoldBlock / 64; w++) t += red[w][threadIdx.x];
-    red[0][threadIdx.x] = t;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < K; k++) v[k] = red[0][k];
-}
-
-// Multi-workgroup: workgroup g owns walk blocks [64g, 64g + 64) and a share of the
+// Multi-workgroup: workgroup g owns walk blocks [256g, 256g + 256) and a share of the
 // decode partials. It folds them (every load in flight at once), scans its walk blocks'
 // plan bytes (block_base = the offset inside the group) and publishes one row of
 // dpart; the last workgroup to arrive folds the rows, scans the group totals into
 // group_base (the commit adds both), picks the path and, on the keyed path, applies
 // the counter deltas (live, version, total_operations: nothing reads them between here
 // and the next batch's decide). Round 4 ran this as one 1024-thread workgroup (20 us
-// per 2^22 commands: a chain of dependent loads on one CU) plus a second fold in the
+// per 2^22 commands: a chain of dependent loads on one CU) plus a second fold in a
 // close kernel.
 constexpr int kDecBlock = 256;
-enum { kDCreated = 0, kDNewSlots, kDOverflow, kDSets, kDSetBytes, kDNeed, kDLive, kDVersion, kDOps, kDCount };
+static_assert(kDecGroup == (uint32_t)kDecBlock, "decide: one walk block per thread");
+enum {
+  kDCreated = 0, kDNewSlots, kDOverflow, kDSets, kDSetBytes, kDNeed, kDLive, kDVersion, kDOps, kDLiveDel, kDDels,
+  kDCount
+};
 
 __device__ __forceinline__ void dec_store(unsigned long long* p, unsigned long long v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -881,15 +969,21 @@ __global__ __launch_bounds__(kDecBlock) void kv_decide_kernel(StoreView st, cons
                                                               uint32_t walk_blocks, const unsigned long long* set_part,
                                                               uint32_t blocks, uint64_t* block_base,
                                                               uint64_t* group_base, unsigned long long* dpart,
-                                                              unsigned long long* arrivals) {
+                                                              unsigned long long* arrivals, const uint32_t* cbits,
+                                                              const unsigned long long* cbytes, uint64_t n_cmds) {
   __shared__ unsigned long long red[kDecBlock / 64][kDCount];
   __shared__ uint32_t s_last;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t g = blockIdx.x, D = gridDim.x;
-  unsigned long long v[kDCount] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  if (wave == 0) {  // this group's walk blocks, one per lane: folds + the in-group scan of plan bytes
-    const uint32_t wb = g * kDecGroup + (uint32_t)lane;
-    unsigned long long x[kPCount] = {0, 0, 0, 0, 0, 0, 0};
+  // the store counters the last workgroup decides with, loaded now (the previous batch
+  // wrote them: stream order) so the load is not on the fold's dependent chain
+  KvCounters* k = st.ctr;
+  const unsigned long long live0 = k->live, occ0 = k->occupied, top0 = k->heap_top, flags0 = k->flags;
+  const unsigned long long batches0 = k->batches, ver0 = k->version, ops0 = k->total_ops;
+  unsigned long long v[kDCount] = {};
+  {  // this group's walk blocks, one per thread: folds + the in-group scan of plan bytes
+    const uint32_t wb = g * kDecGroup + (uint32_t)tid;
+    unsigned long long x[kPCount] = {};
     if (wb < walk_blocks)
 #pragma unroll
       for (int k = 0; k < kPCount; k++) x[k] = part[(uint64_t)wb * kPCount + k];
@@ -899,19 +993,25 @@ __global__ __launch_bounds__(kDecBlock) void kv_decide_kernel(StoreView st, cons
     v[kDLive] = x[kPLiveDelta];
     v[kDVersion] = x[kPVersion];
     v[kDOps] = x[kPOps];
-    unsigned long long incl = x[kPNeed];  // inclusive scan over the 64 lanes
+    v[kDLiveDel] = x[kPLiveDel];
+    unsigned long long incl = x[kPNeed];  // inclusive scan: over the wave, then the waves before
     for (int o = 1; o < 64; o <<= 1) {
       const unsigned long long t = __shfl_up(incl, o, 64);
       if (lane >= o) incl += t;
     }
+    __shared__ unsigned long long s_wtot[kDecBlock / 64];
+    if (lane == 63) s_wtot[wave] = incl;
+    __syncthreads();
+    for (int w = 0; w < wave; w++) incl += s_wtot[w];
     if (wb < walk_blocks) block_base[wb] = incl - x[kPNeed];
     v[kDNeed] = x[kPNeed];
   }
   {  // this group's share of the decode partials (pending SETs, their worst-case bytes)
     const uint32_t per = (blocks + D - 1) / D, r0 = g * per, r1 = r0 + per < blocks ? r0 + per : blocks;
     for (uint32_t r = r0 + (uint32_t)tid; r < r1; r += kDecBlock) {
-      v[kDSets] += set_part[(uint64_t)r * 2];
-      v[kDSetBytes] += set_part[(uint64_t)r * 2 + 1];
+      v[kDSets] += set_part[(uint64_t)r * kSetPart];
+      v[kDSetBytes] += set_part[(uint64_t)r * kSetPart + 1];
+      v[kDDels] += set_part[(uint64_t)r * kSetPart + 2];
     }
   }
 #pragma unroll
@@ -937,7 +1037,7 @@ __global__ __launch_bounds__(kDecBlock) void kv_decide_kernel(StoreView st, cons
   // the last workgroup: fold every group's row; exclusive scan of the groups' plan bytes
   const uint32_t per = (D + kDecBlock - 1) / kDecBlock;
   const uint32_t lo = (uint32_t)tid * per, hi = lo + per < D ? lo + per : D;
-  unsigned long long f[kDCount] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long f[kDCount] = {};
   for (uint32_t q = lo; q < hi; q++)
 #pragma unroll
     for (int k = 0; k < kDCount; k++) f[k] += dec_load(dpart + (uint64_t)q * kDCount + k);
@@ -962,41 +1062,98 @@ __global__ __launch_bounds__(kDecBlock) void kv_decide_kernel(StoreView st, cons
     if (lane == 0) red[wave][k] = t;
   }
   __syncthreads();
-  if (tid != 0) return;
-  unsigned long long tot[kDCount];
-  for (int k = 0; k < kDCount; k++) {
-    tot[k] = 0;
-    for (int w = 0; w < kDecBlock / 64; w++) tot[k] += red[w][k];
+  __shared__ unsigned long long s_tot[kDCount], s_path, s_cut, s_failed;
+  if (tid < kDCount) {
+    unsigned long long t = 0;
+    for (int w = 0; w < kDecBlock / 64; w++) t += red[w][tid];
+    s_tot[tid] = t;
   }
+  __syncthreads();
+  const unsigned long long c = s_tot[kDCreated], ov = s_tot[kDOverflow];
+  const unsigned long long free_keys = live0 < st.max_keys ? st.max_keys - live0 : 0;
+  // StoreFull unreachable iff live + created <= max_keys (size never exceeds it): the
+  // keyed commit (0). Reachable: if no DELETE meets a live key, the live count only
+  // grows through the batch, so a create succeeds iff fewer than max_keys - live
+  // creates precede it in command order: the keyed commit with the creates ranked
+  // (3, the cut below). Otherwise the ordered replay (1).
+  unsigned long long path = 0;
+  if (ov || live0 + c > st.max_keys) path = (!ov && s_tot[kDLiveDel] == 0 && cbits) ? 3 : 1;
+  if (path == 3) {
+    // the cut = command index of the create of rank max_keys - live (0-based) in
+    // command order, from the plan's create bitmap: each thread popcounts a contiguous
+    // range of words, a workgroup scan finds the range that holds it
+    const uint64_t W = (n_cmds + 31) / 32, per_w = (W + kDecBlock - 1) / kDecBlock;
+    const uint64_t w0 = (uint64_t)tid * per_w, w1 = w0 + per_w < W ? w0 + per_w : W;
+    unsigned long long cnt = 0;
+    for (uint64_t w = w0; w < w1; w++) cnt += __builtin_popcount(cbits[w]);
+    s_scan[tid] = cnt;
+    if (tid == 0) s_cut = n_cmds;  // (every create fits: not reached, c > free)
+    __syncthreads();
+    for (int o = 1; o < kDecBlock; o <<= 1) {
+      const unsigned long long t = tid >= o ? s_scan[tid - o] : 0ull;
+      __syncthreads();
+      s_scan[tid] += t;
+      __syncthreads();
+    }
+    const unsigned long long incl = s_scan[tid], excl = incl - cnt;
+    if (excl <= free_keys && free_keys < incl) {
+      unsigned long long r = free_keys - excl;
+      for (uint64_t w = w0; w < w1; w++) {
+        uint32_t x = cbits[w];
+        const unsigned long long pc = __builtin_popcount(x);
+        if (r < pc) {
+          for (; r; r--) x &= x - 1;  // drop the r lowest creates of the word
+          s_cut = w * 32 + (uint64_t)__builtin_ctz(x);
+          break;
+        }
+        r -= pc;
+      }
+    }
+    __syncthreads();
+    // heap bytes the refused keys reserved in the plan (cbytes at their creates)
+    unsigned long long fb = 0;
+    for (uint64_t q = s_cut + (uint64_t)tid; q < n_cmds; q += kDecBlock) fb += cbytes[q];
+    for (int o = 32; o > 0; o >>= 1) fb += __shfl_xor(fb, o, 64);
+    if (lane == 0) red[wave][0] = fb;
+    __syncthreads();
+    if (tid == 0) s_failed = red[0][0] + red[1][0] + red[2][0] + red[3][0];
+    __syncthreads();
+  }
+  if (tid != 0) return;
+  const unsigned long long ns = s_tot[kDNewSlots], sets = s_tot[kDSets], set_bytes = s_tot[kDSetBytes];
+  // mode 3: the accepted creates take at most max_keys - live new slots, and the heap
+  // bytes without the refused keys' reservations
+  const unsigned long long slots = path == 3 && ns > free_keys ? free_keys : ns;
+  // the ordered replay creates at most max_keys - live keys plus one per DELETE (each
+  // frees at most one), so it needs at most that many new slots
+  const unsigned long long room = free_keys + s_tot[kDDels];
+  const unsigned long long slots1 = room < sets ? room : sets;
+  const unsigned long long bytes = s_tot[kDNeed] - (path == 3 ? s_failed : 0ull);
   *arrivals = 0;  // for the next batch (stream order)
-  const unsigned long long c = tot[kDCreated], ns = tot[kDNewSlots], ov = tot[kDOverflow], sets = tot[kDSets],
-                           set_bytes = tot[kDSetBytes], bytes = tot[kDNeed];
-  KvCounters* k = st.ctr;
-  unsigned long long mode = 0;
-  // StoreFull unreachable iff live + created <= max_keys (size never exceeds it).
-  if (ov || k->live + c > st.max_keys) mode = 1;
   // an earlier commit pass faulted and left a batch partially written: the store is
   // lost, and every later batch is refused (the fault bit stays set)
   // capacities: at most 7/8 of the table occupied; heap bytes available. The ordered
   // replay is checked against its worst case (every pending SET a new key and a new
   // value allocation), so a batch either fits whole or is refused before any write.
   const uint64_t cap = st.mask + 1, slot_cap = cap - cap / 8;
-  if (mode == 0 && (k->occupied + ns > slot_cap || k->heap_top + bytes > st.heap_cap)) mode = 2;
-  if (mode == 1 && (k->occupied + sets > slot_cap || k->heap_top + set_bytes > st.heap_cap)) mode = 2;
-  const bool lost = (k->flags & kFaultPartial) != 0;
+  unsigned long long mode = path;
+  if (path != 1 && (occ0 + slots > slot_cap || top0 + bytes > st.heap_cap)) mode = 2;
+  if (path == 1 && (occ0 + slots1 > slot_cap || top0 + set_bytes > st.heap_cap)) mode = 2;
+  const bool lost = (flags0 & kFaultPartial) != 0;
   if (lost) mode = 2;
   k->mode = mode;
-  k->batches += 1;
-  if (mode == 0) {
-    k->occupied += ns;
-    k->batch_base = k->heap_top;  // commit writes [batch_base + group_base + block_base + ..., ...)
-    k->heap_top += bytes;
-    k->live += tot[kDLive];  // two's-complement sum of +-1 deltas
-    k->version += tot[kDVersion];
-    k->total_ops += tot[kDOps];
+  k->batches = batches0 + 1;
+  if (mode == 0 || mode == 3) {  // (mode 3: the commit subtracts what refused keys added)
+    k->occupied = occ0 + ns;
+    k->batch_base = top0;  // mode 0: commit writes [batch_base + group_base + block_base + ..., ...)
+    if (mode == 0) k->heap_top = top0 + bytes;  // (mode 3: the commit's workgroups bump heap_top)
+    k->live = live0 + s_tot[kDLive];  // two's-complement sum of +-1 deltas
+    k->version = ver0 + s_tot[kDVersion];
+    k->total_ops = ops0 + s_tot[kDOps];
+    k->cut = mode == 3 ? s_cut : ~0ull;
   } else if (mode == 2 && !lost) {
-    const bool table = mode == 2 && (k->occupied + (ov || k->live + c > st.max_keys ? sets : ns) > slot_cap);
-    k->flags |= table ? kFaultTable : kFaultHeap;
+    const bool table = occ0 + (path == 1 ? slots1 : slots) > slot_cap;
+    k->flags = flags0 | (table ? kFaultTable : kFaultHeap);
   }
 }
 
@@ -1061,28 +1218,6 @@ __device__ void kv_ordered(const uint8_t* data, const KvOp* ops, uint64_t n, uin
   }
   k->live = live; k->version = ver; k->total_ops = tops; k->occupied = occ; k->heap_top = top;
   k->ordered += 1;
-}
-
-// ---- 7 finish (keyed path counters) ----------------------------------------------
-// One launch closes the batch by its path (mode is uniform): 0 folds the keyed
-// path's counter deltas; 1 runs the ordered replay (one thread); 2 (refused) gives
-// every pending command RG_KV_E_CAPACITY (a block-stride loop: refusals are rare).
-__global__ __launch_bounds__(kFoldBlock) void kv_close_kernel(const uint8_t* data, const KvOp* ops, uint64_t n,
-                                                              uint8_t* results, StoreView st,
-                                                              const unsigned long long* part, uint32_t blocks) {
-  KvCounters* k = st.ctr;
-  const unsigned long long mode = k->mode;
-  if (mode == 1) {
-    if (threadIdx.x == 0) kv_ordered(data, ops, n, results, st);
-    return;
-  }
-  if (mode == 2) {
-    for (uint64_t c = threadIdx.x; c < n; c += blockDim.x)
-      if (ops[c].status == kPending) results[c] = RG_KV_E_CAPACITY;
-    return;
-  }
-  (void)part;  // mode 0: the decide kernel applied the keyed path's counter deltas
-  (void)blocks;
 }
 
 // ---- mark applied commands from the phase step's decision plane -----------------
@@ -1574,6 +1709,11 @@ struct rg_kv {
   uint8_t* done = nullptr;
   unsigned long long* part = nullptr;
   unsigned long long* set_part = nullptr;  // [blocks][2] decode partials: pending SETs, worst-case bytes
+  uint32_t* cbits = nullptr;               // [cap / 32] creates by command index (mode 3)
+  unsigned long long* cbytes = nullptr;    // [cap] heap bytes reserved at each create (mode 3)
+  // host-side upper bound of the live keys after every enqueued batch (exact after a
+  // synchronising call): a batch marks its creates only when it could meet StoreFull
+  uint64_t live_ub = 0;
   std::string err;
 };
 
@@ -1601,7 +1741,8 @@ void free_scratch(rg_kv* kv) {
   (void)hipFree(kv->ops); (void)hipFree(kv->key_a); (void)hipFree(kv->key_b);
   (void)hipFree(kv->need); (void)hipFree(kv->block_base); (void)hipFree(kv->idx_a);
   (void)hipFree(kv->idx_b); (void)hipFree(kv->done); (void)hipFree(kv->part);
-  (void)hipFree(kv->set_part); (void)hipFree(kv->recs);
+  (void)hipFree(kv->set_part); (void)hipFree(kv->recs); (void)hipFree(kv->cbits); (void)hipFree(kv->cbytes);
+  kv->cbits = nullptr; kv->cbytes = nullptr;
   (void)hipFree(kv->group_base); (void)hipFree(kv->dpart); (void)hipFree(kv->arrivals);
   kv->group_base = nullptr; kv->dpart = nullptr; kv->arrivals = nullptr;
   (void)hipFree(kv->sort_hist); (void)hipFree(kv->bin_lo); (void)hipFree(kv->scan_sums);
@@ -1634,7 +1775,9 @@ int ensure_scratch(rg_kv* kv, uint64_t n) {
   KV_HIP(kv, hipMalloc(&kv->idx_b, cap * 4));
   KV_HIP(kv, hipMalloc(&kv->done, cap));
   KV_HIP(kv, hipMalloc(&kv->part, blocks * kPCount * 8));
-  KV_HIP(kv, hipMalloc(&kv->set_part, blocks * 2 * 8));
+  KV_HIP(kv, hipMalloc(&kv->set_part, blocks * kSetPart * 8));
+  KV_HIP(kv, hipMalloc(&kv->cbits, (cap / 32 + 1) * 4));
+  KV_HIP(kv, hipMalloc(&kv->cbytes, cap * 8));
   KV_HIP(kv, hipMalloc(&kv->sort_hist, (cap / kL1Chunk + 1) * kRadix * 4));
   KV_HIP(kv, hipMalloc(&kv->bin_lo, (kRadix + 1) * 4));
   KV_HIP(kv, hipMalloc(&kv->scan_sums, (cap / kScanChunk + 2) * 8));
@@ -1743,11 +1886,17 @@ int rg_kv_apply_async(rg_kv* kv, const uint8_t* data_dev, const uint64_t* cmd_of
   while (vbits < 31 && (1ull << (vbits - 8)) < n_cmds) vbits++;
   if (kv->cfg.bucket_bits && (int)kv->cfg.bucket_bits < vbits) vbits = (int)kv->cfg.bucket_bits;
   const uint32_t invalid_bucket = 1u << vbits;
+  // StoreFull can fire only if live + keys created > max_keys; a batch creates at most
+  // n_cmds keys, so below the bound the plan keeps no create bitmap (mode 3 unneeded)
+  const bool may_fill = kv->live_ub + n_cmds > kv->cfg.max_keys;
+  kv->live_ub = kv->live_ub + n_cmds < kv->live_ub ? ~0ull : kv->live_ub + n_cmds;
+  uint32_t* cbits = may_fill ? kv->cbits : nullptr;
+  unsigned long long* cbytes = may_fill ? kv->cbytes : nullptr;
   hipLaunchKernelGGL(kv_decode_kernel, dim3(blocks), dim3(kBlock), 0, s, data_dev, cmd_off_dev, n_cmds,
                      apply_mask_dev, kv->cfg.max_value_size,
                      kv->cfg.hash_bits && kv->cfg.hash_bits < 64 ? (1ull << kv->cfg.hash_bits) - 1 : ~0ull,
                      (uint64_t)invalid_bucket - 1, invalid_bucket, kv->ops, kv->key_a, results_dev, kv->set_part,
-                     kv->done);
+                     kv->done, cbits, cbytes);
   KV_HIP(kv, hipGetLastError());
   // stable (bucket, index) sort of the applied commands (two levels of 8-bit digits)
   SortArgs sa;
@@ -1771,17 +1920,15 @@ int rg_kv_apply_async(rg_kv* kv, const uint8_t* data_dev, const uint64_t* cmd_of
   KV_HIP(kv, hipGetLastError());
   const bool fin_a = (sa.passes2 & 1u) != 0;
   BatchView b{data_dev, kv->ops, fin_a ? kv->key_a : kv->key_b, fin_a ? kv->idx_a : kv->idx_b, n_cmds, results_dev,
-              kv->done, kv->need, kv->block_base, kv->group_base, kv->recs, invalid_bucket, kv->part};
+              kv->done, kv->need, kv->block_base, kv->group_base, kv->recs, invalid_bucket, kv->part, cbits, cbytes};
   const StoreView st = view(kv);
   const uint32_t walk_blocks = (uint32_t)((n_cmds + kWalkBlockSpan - 1) / kWalkBlockSpan);
   hipLaunchKernelGGL(kv_plan_kernel, dim3(walk_blocks), dim3(kBlock), 0, s, b, st);
   KV_HIP(kv, hipGetLastError());
   const uint32_t groups = (walk_blocks + kDecGroup - 1) / kDecGroup;
   hipLaunchKernelGGL(kv_decide_kernel, dim3(groups), dim3(kDecBlock), 0, s, st, kv->part, walk_blocks, kv->set_part,
-                     blocks, kv->block_base, kv->group_base, kv->dpart, kv->arrivals);
+                     blocks, kv->block_base, kv->group_base, kv->dpart, kv->arrivals, cbits, cbytes, n_cmds);
   hipLaunchKernelGGL(kv_commit_kernel, dim3(walk_blocks), dim3(kBlock), 0, s, b, st);
-  hipLaunchKernelGGL(kv_close_kernel, dim3(1), dim3(kFoldBlock), 0, s, data_dev, kv->ops, n_cmds, results_dev, st,
-                     kv->part, walk_blocks);
   KV_HIP(kv, hipGetLastError());
   return 0;
 }
@@ -1791,6 +1938,7 @@ int rg_kv_get_stats(rg_kv* kv, rg_kv_stats* out) {
   KvCounters c;
   KV_HIP(kv, hipDeviceSynchronize());  // applies may sit on caller streams
   KV_HIP(kv, hipMemcpy(&c, kv->ctr, sizeof(c), hipMemcpyDeviceToHost));
+  kv->live_ub = c.live;  // exact: every apply has completed
   out->live_keys = c.live;
   out->version = c.version;
   out->total_operations = c.total_ops;

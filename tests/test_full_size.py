@@ -117,6 +117,45 @@ def test_c4_full_size_pipeline(oracle):
         assert got_state["data"] == exp_state["data"]
 
 
+def test_c4_full_size_store_full(oracle):
+    """StoreFull at full size (2^22 commands over 2^20 keys, max_keys 500,000, the
+    device trace with its DELETEs made GETs): the capacity-ranked keyed path (mode 3)
+    against the sequential C restatement, every result and the final store; then a
+    second batch on the full store (every create refused, updates in place)."""
+    torch = torch_cuda()
+    from rabia_amd.kvstore import DeviceKVStore, KVStoreConfig
+    S, ks, mk = 1 << 22, 1 << 20, 500_000
+    cmd_data = torch.zeros(68 * S, dtype=torch.uint8, device="cuda")
+    cmd_off = torch.zeros(S + 1, dtype=torch.int64, device="cuda")
+    res = torch.zeros(S, dtype=torch.uint8, device="cuda")
+    ref = oracle.KVStoreC(max_keys=mk)
+    torch.cuda.synchronize()
+    with DeviceKVStore(KVStoreConfig(max_keys=mk)) as kv:
+        for seed in (3, 4):
+            kv.trace_async(seed, S, ks, cmd_data.data_ptr(), cmd_data.numel(), cmd_off.data_ptr())
+            kv.sync()
+            first = cmd_off[:-1]
+            kind = cmd_data[first]
+            cmd_data[first[kind == 2]] = 1  # DELETE -> GET (first byte of the u32 variant)
+            torch.cuda.synchronize()
+            kv.apply_async(cmd_data.data_ptr(), cmd_off.data_ptr(), S, 0, res.data_ptr())
+            kv.sync()
+            stats = kv.stats()
+            assert stats["last_path"] == 3 and stats["ordered_batches"] == 0, stats
+            data = cmd_data.cpu().numpy()
+            offs = cmd_off.cpu().numpy().view(np.uint64)
+            exp_res = ref.apply(data[: int(offs[-1])], offs, np.ones(S, dtype=np.uint8))
+            got = res.cpu().numpy()
+            np.testing.assert_array_equal(got, exp_res)
+            assert (got == 5).any()  # RG_KV_E_FULL
+            rs = ref.stats()
+            assert stats["live_keys"] == rs["live_keys"] == mk and stats["version"] == rs["version"]
+            assert stats["total_operations"] == rs["total_operations"] and stats["flags"] == 0
+        got_state, exp_state = kv.get_state(), ref.state()
+        assert got_state["version"] == exp_state["version"]
+        assert got_state["data"] == exp_state["data"]
+
+
 def test_c5_full_size_step(oracle):
     torch = torch_cuda()
     n, S, T = 9, 1 << 26, 1024

@@ -167,6 +167,48 @@ def test_gpu_store_full_takes_ordered_path():
         assert dev.stats()["ordered_batches"] >= 1
 
 
+def no_delete(blobs):
+    """The same commands with every DELETE turned into a GET (a batch whose live count
+    only grows: the capacity-ranked path)."""
+    out = []
+    for b in blobs:
+        if len(b) >= 4 and b[:4] == b"\x02\x00\x00\x00":
+            b = b"\x01\x00\x00\x00" + b[4:]
+        out.append(b)
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,key_space,max_keys,bucket_bits,batches",
+                         [(3000, 2000, 500, 0, 2), (3000, 400, 100, 8, 3), (500, 100, 1, 0, 2), (4000, 900, 600, 0, 3)])
+def test_gpu_store_full_capacity_ranked(n, key_space, max_keys, bucket_bits, batches):
+    """StoreFull reachable in a batch with no DELETE of a live key: the live count only
+    grows, so a create succeeds iff fewer than max_keys - live creates precede it in
+    command order. The keyed path with the creates ranked (mode 3, the cut from the
+    plan's create bitmap) equals the in-order restatement: results (StoreFull for the
+    refused keys' SETs, NotFound for their GETs), the store and the counters, also in
+    runs of several keys (8-bit buckets) and once the store is full (free = 0)."""
+    rng = random.Random(n + max_keys)
+    with _store(max_keys=max_keys, max_value_size=64, bucket_bits=bucket_bits) as dev:
+        ref = R.KVStoreRef(max_keys=max_keys, max_value_size=64)
+        paths = []
+        for _ in range(batches):
+            blobs = no_delete(random_blobs(rng, n, key_space))
+            got = [int(x) for x in dev.apply_commands(blobs)]
+            assert got == ref.apply_commands(blobs)
+            paths.append(dev.stats()["last_path"])
+            _check_state(dev, ref)
+        assert R.E_FULL in got
+        assert 3 in paths and dev.stats()["ordered_batches"] == 0, paths
+        # a DELETE of a live key in a batch that meets StoreFull: the ordered replay
+        victim = next(iter(ref.data))
+        blobs = [R.encode_op(R.DELETE, victim)] + no_delete(random_blobs(rng, n, key_space))
+        got = [int(x) for x in dev.apply_commands(blobs)]
+        assert got == ref.apply_commands(blobs)
+        _check_state(dev, ref)
+        assert dev.stats()["last_path"] == 1 and dev.stats()["ordered_batches"] == 1
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("hash_bits", [2, 5, 12])
 def test_gpu_hash_collision_runs(hash_bits):
