@@ -8,7 +8,7 @@
 #     smoke             __graft_entry__.smoke()
 #     bench             bench.py (C2 headline, CPU leg included)
 #     bench_sharded     bench.py --sharded (the N > 1 per-GPU pipeline on one GPU, RCCL world 1)
-#     c3 | c5 | c5_sharded   bench.py --config ...
+#     c3[=NAME] | c5 | c5_sharded   bench.py --config ... (NAME: an A/B label)
 #     c4[=NAME]         tools/bench_c4.py (kvstore apply; NAME: an A/B label, no CPU leg)
 #     probe_c5[=K]      tools/c5_probe.py, n = 9, K windows of 2^23 (default 32)
 #     ab[=SLOTS]        tools/ab_variants.py (interleaved A/B, AB_DIAGS / RABIA_AB_LIBS from the env)
@@ -84,7 +84,7 @@ for step in "$@"; do
     smoke) run smoke 200 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 400 python bench.py ;;
     bench_sharded) run bench_sharded 300 python bench.py --sharded --steps 20 --warmup 10 --no-cpu-baseline ;;
-    c3) run c3 300 python bench.py --config c3 --steps 10 --warmup 3 --no-cpu-baseline ;;
+    c3) run "c3$sfx" 300 python bench.py --config c3 --steps 10 --warmup 3 --no-cpu-baseline ;;
     c5) run c5 300 python bench.py --config c5 --steps 20 --warmup 10 ;;
     c5_sharded) run c5_sharded 300 python bench.py --config c5 --sharded --steps 20 --warmup 10 ;;
     c4)
