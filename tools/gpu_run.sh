@@ -16,6 +16,8 @@
 #     stamps_shard      the same for the sharded step
 #     shard_probe       tools/shard_step_probe.py (plain vs sharded step alone, 2^30 slots)
 #     latency           tools/latency_1m.py (single 2^20 window)
+#     warm[=zero]       tools/warm_probe.py (launch-to-launch ramp; =zero: outputs zeroed first)
+#     driver[=NAME]     bench.py exactly as the round-end driver runs it (--steps 20 --warmup 5)
 #     gloo2             bench.py --gpus 2 --backend gloo (two ranks on the one GPU, a rehearsal)
 #     prof[=ARGS]       rocprofv3 --kernel-trace --stats over bench.py ARGS (default: the C2 line)
 #     pmc[=ARGS]        two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) over bench.py ARGS
@@ -96,6 +98,8 @@ for step in "$@"; do
     stamps_shard) STAMP_SHARD=1 run stamps_shard 300 python tools/lag_stamps.py ;;
     shard_probe) run shard_probe 300 python tools/shard_step_probe.py ;;
     latency) run latency 300 python tools/latency_1m.py ;;
+    warm) run "warm$sfx" 300 env ${arg:+PROBE_ZERO=1} python tools/warm_probe.py ;;
+    driver) run "driver$sfx" 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
     gloo2) run gloo2 300 python bench.py --gpus 2 --backend gloo --steps 5 --warmup 2 --no-cpu-baseline ;;
     prof)
       prof_run "prof$sfx" 500 --kernel-trace --stats -d "$OUT/prof$sfx" -o run --output-format csv -- \
