@@ -311,21 +311,28 @@ def load_pmc(path: str, n: int, slots: int):
     return None
 
 
-def launch_events(a):
-    """Per-launch timing events inside the timed region, with --launch-events only. An event
-    recorded between two step kernels puts a barrier packet in the stream: 6-10 us per step
-    between back-to-back 2^30-slot steps (tools/gap_probe.py, profiles/r05/gap_probe*). By
-    default the K launches run back to back between the two bracketing events, and the
-    average launch duration is their span / K (it includes the launch gaps: an upper bound
-    on the kernel time, which the committed rocprofv3 summaries sit just below)."""
-    if not a.launch_events:
-        return None
-    return [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+def launch_events(a, every=0):
+    """Per-launch timing events inside the timed region. An event recorded between two step
+    kernels puts a barrier packet in the stream: 6-10 us per step between back-to-back
+    2^30-slot steps (tools/gap_probe.py, profiles/r05/gap_probe.json). --launch-events: a
+    pair around every launch. Otherwise, every > 0 (the sharded pipeline, whose step time
+    also holds the exchange): a pair around every every-th launch only; every = 0 (the
+    single evaluator, steps back to back): none, and the average launch duration is the
+    span / K (it includes the launch gaps: an upper bound on the kernel time, which the
+    committed rocprofv3 summaries sit just below)."""
+    def pair():
+        return torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if a.launch_events:
+        return [pair() for _ in range(a.steps)]
+    if every:
+        return [pair() if k % every == 0 else None for k in range(a.steps)]
+    return None
 
 
 def launch_ms(evs, total_ms, steps):
-    if evs:
-        return float(np.mean([b.elapsed_time(e) for b, e in evs]))
+    timed = [p for p in (evs or []) if p is not None]
+    if timed:
+        return float(np.mean([b.elapsed_time(e) for b, e in timed]))
     return total_ms / steps
 
 
@@ -574,7 +581,7 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, comm, bitmaps):
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
-    evs = launch_events(a)
+    evs = launch_events(a, every=4)  # the step kernel alone, sampled: the step time holds the exchange too
     t_begin, t_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t_begin.record(comp)
     for k in range(a.steps):  # (the warm-up's last fix-up is done: the timed chain starts afresh)
@@ -670,7 +677,7 @@ def run_c3(a, world, rank, dist, comm):
         step(t)
     torch.cuda.synchronize()
     barrier()
-    evs = launch_events(a)
+    evs = launch_events(a, every=2)  # the cluster kernel alone, sampled: the step holds the gathers too
     t_begin, t_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t_begin.record(stream)
     for k in range(a.steps):
