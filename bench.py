@@ -71,8 +71,10 @@ def c3_roofline(r, bytes_slot):
         achieved = pmc["valu_wave_instr_per_slot"] * r["S"] / kern_s / 1e9
         out.update(achieved=achieved, frac=achieved / out["peak"], counter_issue_util=pmc["valu_issue_util"],
                    counter_file="profiles/pmc_c3.json",
-                   note="counter_issue_util = SQ_INSTS_VALU / (512 x GRBM_GUI_ACTIVE/8 cycles): the same ratio at "
-                        "the clock the chip actually ran (DVFS); mix_per_slot in the counter file")
+                   note="achieved = the cluster kernel's VALU wave-instructions over the rg_wmvc_cluster_async call's "
+                        "time (coin table + cluster kernel + statistics fold: a lower bound for the kernel); "
+                        "counter_issue_util = SQ_INSTS_VALU / (512 x GRBM_GUI_ACTIVE/8 cycles) of the cluster kernel "
+                        "alone, at the clock the chip actually ran (DVFS); mix_per_slot in the counter file")
     return out
 
 
@@ -677,7 +679,7 @@ def run_c3(a, world, rank, dist, comm):
         step(t)
     torch.cuda.synchronize()
     barrier()
-    evs = launch_events(a, every=2)  # the cluster kernel alone, sampled: the step holds the gathers too
+    evs = launch_events(a, every=2)  # the cluster call alone (coin table, cluster kernel, statistics fold), sampled
     t_begin, t_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t_begin.record(stream)
     for k in range(a.steps):

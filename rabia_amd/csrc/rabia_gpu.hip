@@ -968,7 +968,8 @@ int rg_wmvc_cluster_async(rg_ctx* ctx, const uint32_t* states_dev, uint64_t stri
   hipStream_t s = pick_stream(ctx, stream);
   // coin bits of the first phases precomputed (one ChaCha12 block per 512 slots and
   // phase instead of one per lane and phase); later phases (rare) compute inline
-  const uint32_t coin_phases = max_phases < 16 ? max_phases : 16;
+  constexpr uint32_t kCoinTablePhases = 8;  // 16: 0.498 ms per C3 step, 8: 0.465-0.468, 4: 0.475-0.478 (profiles/r05/c3_ab.json)
+  const uint32_t coin_phases = max_phases < kCoinTablePhases ? max_phases : kCoinTablePhases;
   const uint64_t n_words = (n_slots + 31) / 32;
   if (coin_phases * n_words > ctx->cluster_coins_cap) {
     RG_HIP(ctx, hipDeviceSynchronize());
@@ -986,7 +987,7 @@ int rg_wmvc_cluster_async(rg_ctx* ctx, const uint32_t* states_dev, uint64_t stri
                                         ctx->coin_key, ctx->coin_stream, delivery_seed, max_phases, info_dev,
                                         ctx->cluster_part, ctx->cluster_coins, coin_phases, chunk);
   unsigned long long* dst = stats_dev ? reinterpret_cast<unsigned long long*>(stats_dev) : ctx->cluster_stats;
-  hipLaunchKernelGGL(cluster_stats_kernel, dim3(1), dim3(256), 0, s, ctx->cluster_part, grid, dst);
+  hipLaunchKernelGGL(cluster_stats_kernel, dim3(1), dim3(kStatsBlock), 0, s, ctx->cluster_part, grid, dst);
   RG_HIP(ctx, hipGetLastError());
   return RG_OK;
 }
