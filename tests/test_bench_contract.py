@@ -56,3 +56,26 @@ def test_layout():
     assert stride == 1024 and in_w == tiles * 21 * 1024 and out_w == tiles * 8 * 1024
     stride, in_w, out_w = bench.layout(9, 1000, 0)  # planar: 16-byte aligned plane stride in words
     assert stride == 32 and in_w == 37 * 32 and out_w == 8 * 32
+
+
+class _Ev:  # stands in for a recorded torch.cuda.Event pair (elapsed_time in ms)
+    def __init__(self, t):
+        self.t = t
+
+    def elapsed_time(self, other):
+        return other.t - self.t
+
+
+def test_launch_timing_policy(monkeypatch):
+    """Per-launch events: none for the single evaluator (span / K), every `every`-th launch
+    for the pipelines (the kernel alone), every launch with --launch-events."""
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    a = bench.parse()
+    a.steps = 8
+    assert bench.launch_events(a) is None
+    assert bench.launch_ms(None, 10.0, 8) == pytest.approx(1.25)
+    if bench.torch.cuda.is_available():
+        evs = bench.launch_events(a, every=4)
+        assert [e is not None for e in evs] == [True, False, False, False, True, False, False, False]
+    timed = [(_Ev(0.0), _Ev(0.6)), None, None, None, (_Ev(1.0), _Ev(1.8)), None, None, None]
+    assert bench.launch_ms(timed, 10.0, 8) == pytest.approx(0.7)  # the sampled launches only
