@@ -365,6 +365,13 @@ int rg_digest_trace_async(rg_ctx* ctx, uint64_t seed, uint64_t slot_base, uint64
 int rg_wmvc_cluster_async(rg_ctx* ctx, const uint32_t* states_dev, uint64_t stride_words,
                           uint64_t n_slots, uint64_t slot_base, uint64_t delivery_seed,
                           uint32_t max_phases, uint32_t* info_dev, uint64_t* stats_dev, void* stream);
+/* rg_wmvc_cluster_async plus the run's decided and V1 bitmaps (as rg_cluster_bitmap_async
+ * makes them from info_dev, ceil(n_slots/32) words each), built inside the cluster
+ * kernel: one pass instead of two. */
+int rg_wmvc_cluster_bitmaps_async(rg_ctx* ctx, const uint32_t* states_dev, uint64_t stride_words,
+                                  uint64_t n_slots, uint64_t slot_base, uint64_t delivery_seed,
+                                  uint32_t max_phases, uint32_t* info_dev, uint64_t* stats_dev,
+                                  uint32_t* decided_dev, uint32_t* v1_dev, void* stream);
 /* Decided (all replicas decided) and V1 bitmaps of a cluster run's info words,
  * ceil(n_slots/32) words each: the per-shard payload of the C3 multi-GPU exchange. */
 int rg_cluster_bitmap_async(rg_ctx* ctx, const uint32_t* info_dev, uint64_t n_slots,

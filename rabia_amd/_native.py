@@ -105,6 +105,7 @@ _SIGS = {
     "rg_digest_trace_async": (ctypes.c_int, [vp, u64, u64, u64, u64, vp, vp]),
     "rg_wmvc_cluster_async": (ctypes.c_int, [vp, vp, u64, u64, u64, u64, u32, vp, vp, vp]),
     "rg_cluster_trace_async": (ctypes.c_int, [vp, u64, u64, u64, u64, vp, vp]),
+    "rg_wmvc_cluster_bitmaps_async": (ctypes.c_int, [vp, vp, u64, u64, u64, u64, u32, vp, vp, vp, vp, vp]),
     "rg_cluster_bitmap_async": (ctypes.c_int, [vp, vp, u64, vp, vp, vp]),
     "rg_stream_sync": (ctypes.c_int, [vp, vp]),
     "rg_pack_codes": (ctypes.c_int, [vp, u32, u64, u64, vp]),

@@ -126,13 +126,13 @@ struct Disp {
   static void cluster_lc(uint32_t grid, hipStream_t s, const uint32_t* st, uint64_t stride, uint64_t n_slots,
                          uint64_t base, uint32_t q, uint32_t fp1, Key key, uint64_t cs, uint64_t dseed,
                          uint32_t maxp, uint32_t* info, unsigned long long* part, const uint32_t* coins,
-                         uint32_t coin_phases, uint64_t chunk) {
+                         uint32_t coin_phases, uint64_t chunk, uint32_t* bm_dec, uint32_t* bm_v1) {
     if (q == (uint32_t)(N / 2 + 1))  // the majority quorum: the straight-line instantiation
       hipLaunchKernelGGL((wmvc_cluster_lc_kernel<N, N / 2 + 1>), dim3(grid), dim3(256), 0, s, st, stride, n_slots,
-                         base, q, fp1, key, cs, dseed, maxp, info, part, coins, coin_phases, chunk);
+                         base, q, fp1, key, cs, dseed, maxp, info, part, coins, coin_phases, chunk, bm_dec, bm_v1);
     else
       hipLaunchKernelGGL((wmvc_cluster_lc_kernel<N, 0>), dim3(grid), dim3(256), 0, s, st, stride, n_slots, base, q,
-                         fp1, key, cs, dseed, maxp, info, part, coins, coin_phases, chunk);
+                         fp1, key, cs, dseed, maxp, info, part, coins, coin_phases, chunk, bm_dec, bm_v1);
   }
 };
 
@@ -152,7 +152,7 @@ const StepLaunch kWmvcLaunch[17] = RG_TABLE(wmvc);
 const DigestLaunch kDigestLaunch[17] = RG_TABLE(digest);
 using ClusterLcLaunch = void (*)(uint32_t, hipStream_t, const uint32_t*, uint64_t, uint64_t, uint64_t, uint32_t,
                                  uint32_t, Key, uint64_t, uint64_t, uint32_t, uint32_t*, unsigned long long*,
-                                 const uint32_t*, uint32_t, uint64_t);
+                                 const uint32_t*, uint32_t, uint64_t, uint32_t*, uint32_t*);
 const ClusterLcLaunch kClusterLcLaunch[17] = RG_TABLE(cluster_lc);
 
 hipStream_t pick_stream(rg_ctx* ctx, void* stream) {
@@ -940,9 +940,9 @@ int rg_digest_trace_async(rg_ctx* ctx, uint64_t seed, uint64_t slot_base, uint64
   return RG_OK;
 }
 
-int rg_wmvc_cluster_async(rg_ctx* ctx, const uint32_t* states_dev, uint64_t stride_words, uint64_t n_slots,
-                          uint64_t slot_base, uint64_t delivery_seed, uint32_t max_phases, uint32_t* info_dev,
-                          uint64_t* stats_dev, void* stream) {
+static int cluster_run(rg_ctx* ctx, const uint32_t* states_dev, uint64_t stride_words, uint64_t n_slots,
+                       uint64_t slot_base, uint64_t delivery_seed, uint32_t max_phases, uint32_t* info_dev,
+                       uint64_t* stats_dev, uint32_t* decided_dev, uint32_t* v1_dev, void* stream) {
   if (!ctx || !states_dev || !info_dev || n_slots == 0) return fail(ctx, RG_EINVAL, "rg_wmvc_cluster: bad argument");
   if (stride_words < (n_slots + 31) / 32) return fail(ctx, RG_EINVAL, "rg_wmvc_cluster: stride too small");
   if (max_phases < 1 || max_phases > 255) return fail(ctx, RG_EINVAL, "rg_wmvc_cluster: max_phases must be 1..255");
@@ -982,14 +982,33 @@ int rg_wmvc_cluster_async(rg_ctx* ctx, const uint32_t* states_dev, uint64_t stri
   const uint64_t groups = ((n_words + 15) / 16) * coin_phases;
   hipLaunchKernelGGL(coin_table_kernel, dim3((uint32_t)((groups + 255) / 256)), dim3(256), 0, s, ctx->coin_key,
                      ctx->coin_stream, slot_base, n_slots, coin_phases, ctx->cluster_coins);
-  const uint64_t chunk = (n_slots + grid - 1) / grid;
+  // whole bitmap words per workgroup (<= kClusterChunk still: grid >= n_slots / kClusterChunk
+  // and kClusterChunk is a multiple of 32); trailing workgroups may get an empty chunk
+  const uint64_t chunk = ((n_slots + grid - 1) / grid + 31) / 32 * 32;
   kClusterLcLaunch[ctx->cfg.n_replicas](grid, s, states_dev, stride_words, n_slots, slot_base, ctx->q, ctx->fp1,
                                         ctx->coin_key, ctx->coin_stream, delivery_seed, max_phases, info_dev,
-                                        ctx->cluster_part, ctx->cluster_coins, coin_phases, chunk);
+                                        ctx->cluster_part, ctx->cluster_coins, coin_phases, chunk, decided_dev,
+                                        v1_dev);
   unsigned long long* dst = stats_dev ? reinterpret_cast<unsigned long long*>(stats_dev) : ctx->cluster_stats;
   hipLaunchKernelGGL(cluster_stats_kernel, dim3(1), dim3(kStatsBlock), 0, s, ctx->cluster_part, grid, dst);
   RG_HIP(ctx, hipGetLastError());
   return RG_OK;
+}
+
+int rg_wmvc_cluster_async(rg_ctx* ctx, const uint32_t* states_dev, uint64_t stride_words, uint64_t n_slots,
+                          uint64_t slot_base, uint64_t delivery_seed, uint32_t max_phases, uint32_t* info_dev,
+                          uint64_t* stats_dev, void* stream) {
+  return cluster_run(ctx, states_dev, stride_words, n_slots, slot_base, delivery_seed, max_phases, info_dev,
+                     stats_dev, nullptr, nullptr, stream);
+}
+
+int rg_wmvc_cluster_bitmaps_async(rg_ctx* ctx, const uint32_t* states_dev, uint64_t stride_words, uint64_t n_slots,
+                                  uint64_t slot_base, uint64_t delivery_seed, uint32_t max_phases,
+                                  uint32_t* info_dev, uint64_t* stats_dev, uint32_t* decided_dev, uint32_t* v1_dev,
+                                  void* stream) {
+  if (!decided_dev || !v1_dev) return fail(ctx, RG_EINVAL, "rg_wmvc_cluster_bitmaps: null bitmap");
+  return cluster_run(ctx, states_dev, stride_words, n_slots, slot_base, delivery_seed, max_phases, info_dev,
+                     stats_dev, decided_dev, v1_dev, stream);
 }
 
 int rg_cluster_bitmap_async(rg_ctx* ctx, const uint32_t* info_dev, uint64_t n_slots, uint32_t* decided_dev,

@@ -2950,6 +2950,9 @@ static __global__ void coin_table_kernel(Key key, uint64_t stream, uint64_t slot
 // 1..max). Coins come from coin_table_kernel for phases <= coin_phases. The chunk's
 // initial-state words are staged in LDS first (<= kClusterChunk slots: the host sizes
 // the grid for it), so a refill reads LDS instead of waiting on global loads.
+// bm_dec / bm_v1 (both or neither): the decided / V1 bitmaps of the run, built in LDS
+// as slots finish and written once per chunk word (what cluster_bitmap_kernel makes
+// from info in a second pass, 26 µs at C3's 2^24 slots).
 // Q: the quorum as a compile-time constant (the host picks Q = N / 2 + 1, the majority,
 // when the context's quorum is that, else Q = 0 and q at run time). With Q fixed the
 // phase body is straight-line: the 2N heard sets of a phase are independent of each other
@@ -2963,13 +2966,15 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
                                                               uint32_t fp1, Key ckey, uint64_t coin_stream,
                                                               uint64_t dseed, uint32_t max_phases, uint32_t* info,
                                                               unsigned long long* partials, const uint32_t* coin_tab,
-                                                              uint32_t coin_phases, uint64_t chunk) {
+                                                              uint32_t coin_phases, uint64_t chunk, uint32_t* bm_dec,
+                                                              uint32_t* bm_v1) {
   constexpr uint32_t kAll = (1u << N) - 1u;
   constexpr uint32_t kKeyPhases = 32;  // cluster_key table: phases 1..32 (later phases compute theirs)
   constexpr uint32_t kStageWords = kClusterChunk / 32 + 1;
   __shared__ unsigned long long s_next;
   __shared__ uint32_t s_ck[kKeyPhases][2][N];
   __shared__ uint32_t s_st[N][kStageWords];  // the chunk's initial-state words
+  __shared__ uint32_t s_bd[kStageWords], s_b1[kStageWords];  // the chunk's decided / V1 bitmap words
   constexpr uint32_t kTabCap = heard_tab_size<N>((uint32_t)N / 2 + 1) ? heard_tab_size<N>((uint32_t)N / 2 + 1) : 1;
   __shared__ uint16_t s_heard[kTabCap];     // heard sets at the majority quorum (heard_mask_tab)
   const uint32_t q = Q ? (uint32_t)Q : q_rt;
@@ -2986,13 +2991,13 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
   }
   if (use_tab)
     for (uint32_t e = threadIdx.x; e < tab_n; e += blockDim.x) s_heard[e] = (uint16_t)heard_tab_entry<N>(e, q);
-  if (c1 > c0) {
-    const uint32_t nw = (uint32_t)((c1 - 1) / 32 - w0 + 1);  // <= kStageWords (chunk <= kClusterChunk)
-    for (uint32_t e = threadIdx.x; e < N * nw; e += blockDim.x) {
-      const uint32_t r = e / nw, w = e % nw;
-      s_st[r][w] = states[(uint64_t)r * stride + w0 + w];
-    }
+  const uint32_t nw = c1 > c0 ? (uint32_t)((c1 - 1) / 32 - w0 + 1) : 0u;  // <= kStageWords (chunk <= kClusterChunk)
+  for (uint32_t e = threadIdx.x; e < N * nw; e += blockDim.x) {
+    const uint32_t r = e / nw, w = e % nw;
+    s_st[r][w] = states[(uint64_t)r * stride + w0 + w];
   }
+  if (bm_dec)
+    for (uint32_t w = threadIdx.x; w < nw; w += blockDim.x) s_bd[w] = s_b1[w] = 0;
   __syncthreads();
   const int lane = threadIdx.x & 63;
   uint32_t acc[kClusterStats] = {0, 0, 0, 0, 0, 0, 0, 0};  // per lane: <= chunk slots, sums < 2^32
@@ -3090,6 +3095,11 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
       const uint32_t phases = all ? p : 0u;
       const uint32_t dec = all ? ((decv == 0 || decv == kAll) ? (decv & 1u) : kCodeVQ) : kCodeNone;
       info[s] = dec | (phases << 8) | (first << 16) | (coins << 24);
+      if (bm_dec && dec <= kCodeV1) {
+        const uint32_t wl = (uint32_t)(s / 32 - w0), bit = 1u << (s & 31);
+        atomicOr(&s_bd[wl], bit);
+        if (dec == kCodeV1) atomicOr(&s_b1[wl], bit);
+      }
       acc[0] += all;
       acc[1] += dec == kCodeV1;
       acc[2] += phases;
@@ -3116,6 +3126,13 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
     for (int w = 0; w < 4; w++) v = k == 3 ? (red[w][k] > v ? red[w][k] : v) : v + red[w][k];
     partials[(uint64_t)blockIdx.x * kClusterStats + k] = v;
   }
+  // the chunk's bitmap words (the host makes chunk a multiple of 32: no word is shared
+  // with another workgroup; bits past n_slots stay 0)
+  if (bm_dec)
+    for (uint32_t w = threadIdx.x; w < nw; w += blockDim.x) {
+      bm_dec[w0 + w] = s_bd[w];
+      bm_v1[w0 + w] = s_b1[w];
+    }
 }
 
 // Decided / V1 bitmaps of a cluster run's info words (one wave ballot per 64 slots):

@@ -415,6 +415,12 @@ class PhaseEvaluator:
         N.check(self.lib.rg_wmvc_cluster_async(self.ctx, states_ptr, stride, n_slots, slot_base, delivery_seed,
                                                max_phases, info_ptr, stats_ptr or None, stream or None), self.ctx)
 
+    def wmvc_cluster_bitmaps_async(self, states_ptr, stride, n_slots, slot_base, delivery_seed, max_phases,
+                                   info_ptr, decided_ptr, v1_ptr, stats_ptr=0, stream=0):
+        N.check(self.lib.rg_wmvc_cluster_bitmaps_async(self.ctx, states_ptr, stride, n_slots, slot_base,
+                                                       delivery_seed, max_phases, info_ptr, stats_ptr or None,
+                                                       decided_ptr, v1_ptr, stream or None), self.ctx)
+
     def cluster_bitmap_async(self, info_ptr, n_slots, decided_ptr, v1_ptr, stream=0):
         N.check(self.lib.rg_cluster_bitmap_async(self.ctx, info_ptr, n_slots, decided_ptr, v1_ptr, stream or None),
                 self.ctx)

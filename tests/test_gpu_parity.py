@@ -374,3 +374,39 @@ def test_wmvc_cluster_vs_oracle(oracle, golden, n):
     if n in (3, 5, 7):
         g = golden(f"cluster_n{n}.npz")
         np.testing.assert_array_equal(got[: g["info"].shape[0]], g["info"])
+
+
+@pytest.mark.parametrize("S", [1, 33, 50_001, 1_000_003, (1 << 24) + 77])
+def test_wmvc_cluster_fused_bitmaps(S):
+    """rg_wmvc_cluster_bitmaps_async: the cluster run's decided / V1 bitmaps built in the
+    cluster kernel equal rg_cluster_bitmap_async's over the same info words, every word
+    written (buffers start as garbage), info and statistics unchanged. Sizes cover one
+    partial word, a chunk rounded up to whole words with empty trailing workgroups
+    (1,000,003) and the grid grown past 2,048 workgroups (2^24 + 77)."""
+    torch = torch_cuda()
+    n = 5
+    stride = ((S + 127) // 128) * 4
+    nw = (S + 31) // 32
+    states = torch.zeros(n * stride, dtype=torch.int32, device="cuda")
+    info_a = torch.zeros(S, dtype=torch.int32, device="cuda")
+    info_b = torch.full((S,), -1, dtype=torch.int32, device="cuda")
+    stats_a = torch.zeros(8, dtype=torch.int64, device="cuda")
+    stats_b = torch.zeros(8, dtype=torch.int64, device="cuda")
+    bm_a = torch.zeros((2, nw), dtype=torch.int32, device="cuda")
+    bm_b = torch.full((2, nw), -1, dtype=torch.int32, device="cuda")
+    with PhaseEvaluator(n, mode="wmvc", coin_seed=7, epoch=3) as ev:
+        ev.cluster_trace_async(42, 1, S, stride, states.data_ptr())
+        ev.wmvc_cluster_async(states.data_ptr(), stride, S, 1, 99, 32, info_a.data_ptr(), stats_a.data_ptr())
+        ev.cluster_bitmap_async(info_a.data_ptr(), S, bm_a[0].data_ptr(), bm_a[1].data_ptr())
+        ev.wmvc_cluster_bitmaps_async(states.data_ptr(), stride, S, 1, 99, 32, info_b.data_ptr(),
+                                      bm_b[0].data_ptr(), bm_b[1].data_ptr(), stats_b.data_ptr())
+        ev.sync()
+    torch.testing.assert_close(info_b, info_a, rtol=0, atol=0)
+    torch.testing.assert_close(stats_b, stats_a, rtol=0, atol=0)
+    torch.testing.assert_close(bm_b, bm_a, rtol=0, atol=0)
+    if S <= 50_001:  # the bitmaps against the info words directly
+        dec = info_a.cpu().numpy() & 255
+        bits = np.unpackbits(bm_b.cpu().numpy().view(np.uint8), axis=1, bitorder="little")
+        np.testing.assert_array_equal(bits[0, :S], dec <= 1)
+        np.testing.assert_array_equal(bits[1, :S], dec == 1)
+        assert not bits[:, S:].any()

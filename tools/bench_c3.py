@@ -2,7 +2,7 @@
 """C3 timing (BASELINE.json configs[2]): 5 replicas x 2^24 slots, adversarial initial
 states ((n-1)/2 replicas at V1 per slot) forcing multi-round common-coin Weak-MVC, run
 to termination (max 32 phases) for every replica of every slot on one GPU
-(rg_wmvc_cluster_async: each phase = round 1 + round 2 of all n replicas under the
+(rg_wmvc_cluster_bitmaps_async: each phase = round 1 + round 2 of all n replicas under the
 seeded quorum-delivery scheduler + the common coin). At 8 GPUs each rank takes a
 2^21-slot shard (coin keyed by the global slot id: shard-invariant); this tool runs
 the per-GPU shard sizes 2^21 and 2^24 on one GPU.
@@ -39,6 +39,7 @@ def main():
         states = torch.zeros(n * stride, dtype=torch.int32, device="cuda")
         info = torch.zeros(S, dtype=torch.int32, device="cuda")
         stats = torch.zeros(8, dtype=torch.int64, device="cuda")
+        bm = torch.zeros((2, (S + 31) // 32), dtype=torch.int32, device="cuda")
         with PhaseEvaluator(n, mode="wmvc", coin_seed=7, epoch=3) as ev:
             ev.cluster_trace_async(42, 1, S, stride, states.data_ptr(), sp)
             times = []
@@ -46,7 +47,8 @@ def main():
                 stats.zero_()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
-                ev.wmvc_cluster_async(states.data_ptr(), stride, S, 1, 99, 32, info.data_ptr(), stats.data_ptr(), sp)
+                ev.wmvc_cluster_bitmaps_async(states.data_ptr(), stride, S, 1, 99, 32, info.data_ptr(),
+                                              bm[0].data_ptr(), bm[1].data_ptr(), stats.data_ptr(), sp)
                 e1.record(stream)
                 e1.synchronize()
                 if r:
