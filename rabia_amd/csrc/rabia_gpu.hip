@@ -968,7 +968,10 @@ static int cluster_run(rg_ctx* ctx, const uint32_t* states_dev, uint64_t stride_
   hipStream_t s = pick_stream(ctx, stream);
   // coin bits of the first phases precomputed (one ChaCha12 block per 512 slots and
   // phase instead of one per lane and phase); later phases (rare) compute inline
-  constexpr uint32_t kCoinTablePhases = 8;  // 16: 0.498 ms per C3 step, 8: 0.465-0.468, 4: 0.475-0.478 (profiles/r05/c3_ab.json)
+#ifndef RG_COIN_TABLE_PHASES
+#define RG_COIN_TABLE_PHASES 8
+#endif
+  constexpr uint32_t kCoinTablePhases = RG_COIN_TABLE_PHASES;  // 16: 0.498 ms per C3 step, 8: 0.465-0.468, 4: 0.475-0.478 (profiles/r05/c3_ab.json)
   const uint32_t coin_phases = max_phases < kCoinTablePhases ? max_phases : kCoinTablePhases;
   const uint64_t n_words = (n_slots + 31) / 32;
   if (coin_phases * n_words > ctx->cluster_coins_cap) {
@@ -979,8 +982,8 @@ static int cluster_run(rg_ctx* ctx, const uint32_t* states_dev, uint64_t stride_
     RG_HIP(ctx, hipMalloc(&ctx->cluster_coins, coin_phases * n_words * 4));
     ctx->cluster_coins_cap = coin_phases * n_words;
   }
-  const uint64_t groups = ((n_words + 15) / 16) * coin_phases;
-  hipLaunchKernelGGL(coin_table_kernel, dim3((uint32_t)((groups + 255) / 256)), dim3(256), 0, s, ctx->coin_key,
+  const uint64_t coin_wgs = ((n_words + 15) / 16 + kCoinGroupsPerWg - 1) / kCoinGroupsPerWg;
+  hipLaunchKernelGGL(coin_table_kernel, dim3((uint32_t)coin_wgs, coin_phases), dim3(kCoinBlock), 0, s, ctx->coin_key,
                      ctx->coin_stream, slot_base, n_slots, coin_phases, ctx->cluster_coins);
   // whole bitmap words per workgroup (<= kClusterChunk still: grid >= n_slots / kClusterChunk
   // and kClusterChunk is a multiple of 32); trailing workgroups may get an empty chunk

@@ -2916,31 +2916,42 @@ __device__ __forceinline__ uint32_t heard_mask_tab(const uint16_t* tab, uint32_t
 constexpr int kClusterStats = 8;  // all_decided, v1, sum_phases, max_phases, sum_coin_phases, sum_first, slots, -
 
 // Common-coin table for the cluster kernel: coin bits of phases 1..P for the
-// window's slots, [P][n_words]; one thread per 512-slot group (16 words) computes
-// the one or two ChaCha12 blocks that cover it (the same bits as coin_kernel).
-static __global__ void coin_table_kernel(Key key, uint64_t stream, uint64_t slot_base, uint64_t n_slots,
-                                  uint32_t phases, uint32_t* tab) {
+// window's slots, [P][n_words] (the same bits as coin_kernel). A 512-slot group's 16
+// words start sh = slot_base mod 512 bits into one ChaCha12 block and end in the next,
+// the same sh for every group. One workgroup per (phase, 255 groups): each thread
+// computes ONE block into LDS (256 blocks: the 255 groups' and the one after), then
+// the workgroup writes the 255 x 16 words coalesced, each a funnel shift of two LDS
+// words. 8 phases of 2^24 slots: 13.5 µs (one lane quad per block, chacha_block_quad
+// in 1,024-thread workgroups: 15.3 µs); 30 µs with one thread per group computing both
+// of its blocks (2x the ChaCha work, and a run-time register select that put them in
+// scratch memory).
+constexpr uint32_t kCoinBlock = 256;  // one ChaCha block per thread
+constexpr uint32_t kCoinGroupsPerWg = kCoinBlock - 1;
+static __global__ __launch_bounds__(kCoinBlock) void coin_table_kernel(Key key, uint64_t stream, uint64_t slot_base,
+                                                                       uint64_t n_slots, uint32_t phases,
+                                                                       uint32_t* tab) {
+  __shared__ uint32_t s_blk[kCoinBlock][17];  // +1: conflict-free column reads
   const uint64_t n_words = (n_slots + 31) / 32, n_groups = (n_words + 15) / 16;
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n_groups * phases) return;
-  const uint64_t g = t % n_groups, phase = t / n_groups + 1;
-  const uint64_t id0 = slot_base + 512 * g;  // first slot id of the group
-  uint32_t a[16], b[16];
-  chacha_block<12>(key, ((phase - 1) << 40) | (id0 >> 9), stream, a);
-  const uint32_t sh = (uint32_t)(id0 & 511u);
-  if (sh) chacha_block<12>(key, ((phase - 1) << 40) | ((id0 >> 9) + 1), stream, b);
-  else
+  const uint64_t phase = blockIdx.y + 1, g0 = (uint64_t)blockIdx.x * kCoinGroupsPerWg;
+  const uint32_t sh = (uint32_t)(slot_base & 511u), ws = sh >> 5, bo = sh & 31u;  // grid-uniform
+  const uint64_t blk0 = (slot_base >> 9) + g0;  // the first group's first block
+  const uint32_t t = threadIdx.x;
+  {
+    uint32_t b[16];
+    chacha_block<12>(key, ((phase - 1) << 40) | (blk0 + t), stream, b);
 #pragma unroll
-    for (int k = 0; k < 16; k++) b[k] = 0;
-  for (uint32_t k = 0; k < 16; k++) {
-    const uint64_t w = 16 * g + k;
-    if (w >= n_words) break;
-    // bits [sh + 32k, sh + 32k + 32) of the 1024-bit concatenation a|b
-    const uint32_t bit = sh + 32 * k, wi = bit >> 5, bo = bit & 31u;
-    const uint32_t lo = wi < 16 ? select16(a, wi) : select16(b, wi - 16);
-    const uint32_t hi = (wi + 1) < 16 ? select16(a, wi + 1) : select16(b, (wi + 1 - 16) & 15u);
-    const uint32_t v = bo ? ((lo >> bo) | (hi << (32 - bo))) : lo;
-    tab[(phase - 1) * n_words + w] = v & valid_mask(w, n_words, n_slots);
+    for (int k = 0; k < 16; k++) s_blk[t][k] = b[k];
+  }
+  __syncthreads();
+  const uint64_t wbase = g0 * 16, row = (phase - 1) * n_words;
+  const uint64_t ng = n_groups - g0 < kCoinGroupsPerWg ? n_groups - g0 : kCoinGroupsPerWg;
+  const uint32_t nw = (uint32_t)(wbase + ng * 16 <= n_words ? ng * 16 : n_words - wbase);
+  for (uint32_t w = t; w < nw; w += kCoinBlock) {
+    // bits [sh + 32k, sh + 32k + 32) of the group's two blocks
+    const uint32_t gl = w >> 4, i = ws + (w & 15u);  // i + 1 <= 31
+    const uint32_t lo = i < 16 ? s_blk[gl][i] : s_blk[gl + 1][i - 16];
+    const uint32_t hi = i + 1 < 16 ? s_blk[gl][i + 1] : s_blk[gl + 1][i - 15];
+    tab[row + wbase + w] = __builtin_amdgcn_alignbit(hi, lo, bo) & valid_mask(wbase + w, n_words, n_slots);
   }
 }
 

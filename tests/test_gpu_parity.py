@@ -410,3 +410,24 @@ def test_wmvc_cluster_fused_bitmaps(S):
         np.testing.assert_array_equal(bits[0, :S], dec <= 1)
         np.testing.assert_array_equal(bits[1, :S], dec == 1)
         assert not bits[:, S:].any()
+
+
+@pytest.mark.parametrize("slot_base", [512, 1 + 32 * 7, 1000, (1 << 40) + 300, 479])
+def test_wmvc_cluster_slot_base_offsets(oracle, slot_base):
+    """The coin table's word shift (slot_base mod 512: whole words and a bit offset,
+    both, or none) against the CPU restatement, n = 5, and past the 8 tabled phases
+    (inline coins) for a few slots."""
+    torch = torch_cuda()
+    n, S = 5, 300_001
+    q, fp1 = n // 2 + 1, (n - 1) // 2 + 1
+    stride = ((S + 127) // 128) * 4
+    states = torch.zeros(n * stride, dtype=torch.int32, device="cuda")
+    info = torch.zeros(S, dtype=torch.int32, device="cuda")
+    with PhaseEvaluator(n, mode="wmvc", coin_seed=7, epoch=3) as ev:
+        ev.cluster_trace_async(42, slot_base, S, stride, states.data_ptr())
+        ev.wmvc_cluster_async(states.data_ptr(), stride, S, slot_base, 99, 32, info.data_ptr())
+        ev.sync()
+    exp = oracle.wmvc_cluster(n, q, fp1, 7, 3, 99, 32, slot_base, oracle.cluster_trace(n, 42, slot_base, S))
+    got = info.cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(got, exp)
+    assert ((exp >> 8) & 255).max() > 8  # some slots ran past the coin table
