@@ -679,7 +679,9 @@ def run_c3(a, world, rank, dist, comm):
         step(t)
     torch.cuda.synchronize()
     barrier()
-    evs = launch_events(a, every=2)  # the cluster call (coin table, cluster kernel with the bitmaps, statistics fold), sampled
+    # the cluster call (coin table, cluster kernel with the bitmaps, statistics fold): at world 1
+    # it is the whole step (span / K); with the all-gathers in the step, every 2nd call bracketed
+    evs = launch_events(a, every=2 if world > 1 else 0)
     t_begin, t_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t_begin.record(stream)
     for k in range(a.steps):
