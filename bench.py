@@ -106,6 +106,10 @@ def parse():
     ap.add_argument("--c5-batch", type=int, default=32,
                     help="C5: consecutive C5 windows per step: one shard-step launch of K windows per rank (the "
                          "multi-window lag kernel from 2^28 slots per launch at n = 9), one K-window launch at N = 1")
+    ap.add_argument("--c5-payload", choices=["lists", "lists-nov1", "bitmaps"], default="lists",
+                    help="C5 decided-slot payload per step: every rank's undecided-slot lists + V1 bitmaps (default), "
+                         "the lists alone (callers that apply only their own shard), or the round-5 committed + V1 "
+                         "bitmaps")
     ap.add_argument("--sharded", "--c5-sharded", dest="sharded", action="store_true",
                     help="N = 1: run the multi-GPU pipeline (shard step + fix-up + commit, exchanges with one "
                          "rank) instead of the single evaluator: the per-GPU cost of the N > 1 path")
@@ -473,9 +477,19 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, comm, bitmaps):
     g_fixed = torch.zeros((n_total, world, K, 10), **i64)
     result = torch.zeros((n_total, K, 10), **i64)
     nw = (S + 31) // 32
-    if bitmaps:
+    # C5 payload: undecided lists (cap per window; count > cap flags the window, 32) + V1 bitmaps
+    lists = bitmaps and a.c5_payload != "bitmaps"
+    und_cap = max(S // 512, 1024)  # agree90: ~0.04 % of a shard's slots are undecided
+    P = K * (1 + und_cap) + (K * nw if a.c5_payload == "lists" else 0)
+    if comm is not None:  # the exchange scratch (rows; C5: the decided-slot payload) sized before the pipeline
+        comm.reserve(ev, K, S if bitmaps else 1, und_cap)
+    if bitmaps and not lists:
         bm = torch.zeros((n_total, K, 2, nw), dtype=torch.int32, device="cuda")
         bm_all = torch.zeros((n_total, world, K, 2, nw), dtype=torch.int32, device="cuda")
+    elif lists:
+        if comm is None:
+            raise SystemExit("bench.py: --c5-payload lists runs through the C ABI's communicator (--backend nccl)")
+        dec_all = torch.zeros((n_total, world, P), dtype=torch.int32, device="cuda")
     torch.cuda.synchronize()
     e_main = [torch.cuda.Event() for _ in range(n_total)]
     e_rows = [torch.cuda.Event() for _ in range(n_total)]
@@ -548,9 +562,16 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, comm, bitmaps):
         base = 1 + t * K * window_slots
         if comm is not None:  # stages 2-4 + bitmaps: one C-ABI call, RCCL on the device stream
             fs_stream.wait_event(e_main[t])
-            ev.shard_exchange_windows_async(K, out.data_ptr(), out_words, S, stride, base + start, base, window_slots,
-                                            rec.data_ptr(), cap, rows[t].data_ptr(), result[t].data_ptr(),
-                                            bm_all[t].data_ptr() if bitmaps else 0, stream=fs_stream.cuda_stream)
+            if lists:
+                ev.shard_exchange_decisions_async(K, out.data_ptr(), out_words, S, stride, base + start, base,
+                                                  window_slots, rec.data_ptr(), cap, rows[t].data_ptr(),
+                                                  result[t].data_ptr(), und_cap, dec_all[t].data_ptr(),
+                                                  with_v1=a.c5_payload == "lists", stream=fs_stream.cuda_stream)
+            else:
+                ev.shard_exchange_windows_async(K, out.data_ptr(), out_words, S, stride, base + start, base,
+                                                window_slots, rec.data_ptr(), cap, rows[t].data_ptr(),
+                                                result[t].data_ptr(), bm_all[t].data_ptr() if bitmaps else 0,
+                                                stream=fs_stream.cuda_stream)
             e_done[t].record(fs_stream)
             return
         fs_stream.wait_event(e_rows[t])
@@ -607,18 +628,27 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, comm, bitmaps):
     timed = res[a.warmup * K:]
     assert (timed[:, 0] == window_slots).all(), "a timed window did not complete"
     decided = int(timed[:, 1].sum())  # global (every shard), identical on every rank
-    if bitmaps:  # the gathered committed bitmaps carry exactly the folded decided count
+    if bitmaps and not lists:  # the gathered committed bitmaps carry exactly the folded decided count
         b_all = bm_all[a.warmup:].cpu().numpy().view(np.uint32)
         pop = int(np.unpackbits(b_all[:, :, :, 0].view(np.uint8)).sum())
         assert pop == decided, (pop, decided)
+    elif lists:  # the gathered undecided lists count exactly the slots the folded rows left undecided
+        heads = dec_all[a.warmup:, :, :K * (1 + und_cap)].reshape(a.steps, world, K, 1 + und_cap)[..., 0]
+        und = int(heads.cpu().numpy().view(np.uint32).astype(np.int64).sum())
+        assert und == a.steps * K * window_slots - decided, (und, decided)
     if comm is not None and world > 1:
         total_ms, kern_ms = ev.comm_max([total_ms, kern_ms])
     elif dist is not None:
         tm = torch.tensor([total_ms, kern_ms], dtype=torch.float64, device="cuda" if a.backend == "nccl" else "cpu")
         dist.all_reduce(tm, op=dist.ReduceOp.MAX)
         total_ms, kern_ms = float(tm[0]), float(tm[1])
+    payload = None
+    if bitmaps:  # decided-slot payload bytes all-gathered per step (every rank's share)
+        payload = {"kind": a.c5_payload, "bytes_per_step": world * (P if lists else K * 2 * nw) * 4,
+                   "undecided_cap": und_cap if lists else None}
     return {"total_ms": total_ms, "kern_ms": kern_ms, "decided": decided, "sweep_us": None, "ev": ev,
-            "stream": comp, "windows_per_launch": K, "launch": ev.last_launch(), "sharded": True}
+            "stream": comp, "windows_per_launch": K, "launch": ev.last_launch(), "sharded": True,
+            "payload": payload}
 
 
 # ---------------------------------------------------------------------------
@@ -868,6 +898,8 @@ def main():
             "cpu_baseline": cpu,
             "sweep_1m_us": r["sweep_us"],
         }
+        if r.get("payload"):
+            line["config"]["payload"] = r["payload"]
         print(json.dumps(line), file=out, flush=True)
     r["ev"].close()
     if dist is not None:

@@ -54,9 +54,13 @@
 extern "C" {
 #endif
 
-#define RG_ABI_VERSION 4
+#define RG_ABI_VERSION 5
 #define RG_MAX_REPLICAS 16
 #define RG_OUT_PLANES 8
+/* rg_create's scratch reservation (rg_reserve): launches of up to 2^32 slots over up to
+ * 128 windows per call. */
+#define RG_RESERVE_DEFAULT_SLOTS (1ull << 32)
+#define RG_RESERVE_DEFAULT_WINDOWS 128u
 
 typedef struct rg_ctx rg_ctx;
 
@@ -96,7 +100,14 @@ typedef struct rg_config {
   uint32_t reserved;
 } rg_config;
 
-/* Per-step result (host or device memory). */
+/* Per-step result (host or device memory). flags (nonzero = RG_ESTATE; values OR'ed):
+ *   1  look-back wait timed out (a predecessor tile never published)
+ *   2  statistics fold timed out (a workgroup's granules never arrived)
+ *   4  stale launch-record ring (a step ran while the previous launch's record was live)
+ *   8  draw-record overflow (shard step: n_draws > records_cap; set by the fix-up)
+ *   16 the shard rows do not tile the window (commit: their n_slots sum != window_slots)
+ *   32 undecided-list overflow (exchange: some shard has more undecided slots than the
+ *      list capacity; its list is truncated, the rows and state are still exact) */
 typedef struct rg_step_result {
   uint64_t n_slots;
   uint64_t n_decided;          /* PhaseData.is_committed slots                      */
@@ -129,6 +140,18 @@ int rg_create(rg_ctx** out, const rg_config* cfg);
 int rg_destroy(rg_ctx* ctx);
 const char* rg_last_error(const rg_ctx* ctx);
 int rg_get_config(const rg_ctx* ctx, rg_config* out);
+
+/* Scratch reservation. The phase-step, sharded-pipeline and decision-list entry points
+ * (rg_phase_step*_async, rg_shard_fixup*_async, rg_shard_commit*_async,
+ * rg_decision_lists_windows_async, and the exchange calls below with rg_comm_reserve)
+ * NEVER allocate or synchronise the device: their scratch is sized here, and a call past
+ * the reservation returns RG_EINVAL (nothing enqueued). rg_reserve sizes it for calls of
+ * up to max_slots slots (over all windows of one call) and max_windows windows; it only
+ * grows, and it synchronises the device (it frees buffers launches in flight may use),
+ * so call it before a pipeline starts. rg_create reserves RG_RESERVE_DEFAULT_SLOTS /
+ * RG_RESERVE_DEFAULT_WINDOWS. (The round-1 vote, cluster, kv and ingest entry points
+ * still grow their scratch on first use of a larger size, synchronising the device.) */
+int rg_reserve(rg_ctx* ctx, uint64_t max_slots, uint32_t max_windows);
 
 /* Engine state (synchronous w.r.t. the context's stream). */
 int rg_set_state(rg_ctx* ctx, const rg_engine_state* st);
@@ -171,7 +194,7 @@ int rg_last_stage_result(rg_ctx* ctx, int stage, rg_step_result* out_host);
  *     row (rg_step_result): counts, extremes and n_draws of its NON-VQ slots.
  *     Draw-record overflow (n_draws > records_cap: the records past the cap are not
  *     written) is NOT flagged in this row: the step cannot know it before its
- *     statistics fold. The fix-up flags it (flags bit 8) in its final row, and the
+ *     statistics fold. The fix-up flags it (flags value 8) in its final row, and the
  *     commit carries the bit into the window's result, so a caller checks the
  *     fix-up's or the commit's row, not the step's;
  *  2. exchange the rows (all-gather, rank order) -> rows_dev[n_shards];
@@ -253,12 +276,19 @@ int rg_shard_commit_async(rg_ctx* ctx, const rg_step_result* rows_dev, uint32_t 
  * is loaded at run time ($RG_RCCL_LIB, else the ROCm install's librccl.so.1); the
  * library itself needs no RCCL until rg_comm_unique_id / rg_comm_create.
  * Exchange calls of one context must be stream-ordered among themselves (they share the
- * communicator's scratch) and follow the stage rules above. */
+ * communicator's scratch) and follow the stage rules above. Their scratch is sized by
+ * rg_comm_reserve (synchronous; rg_comm_create reserves rows for 128 windows and no
+ * decision payload); an exchange past the reservation returns RG_EINVAL. */
 #define RG_COMM_ID_BYTES 128
 int rg_comm_unique_id(uint8_t* id_out /* RG_COMM_ID_BYTES */);
 int rg_comm_create(rg_ctx* ctx, const uint8_t* id /* RG_COMM_ID_BYTES */, int rank, int world);
 int rg_comm_destroy(rg_ctx* ctx); /* also done by rg_destroy */
 int rg_comm_rank(const rg_ctx* ctx, int* rank, int* world);
+/* Size the exchange scratch for up to max_windows windows per call, shards of up to
+ * max_slots slots per window, and undecided lists of up to undecided_cap entries (also
+ * covers the committed + V1 bitmap payload of rg_shard_exchange_windows_async). Grows
+ * only; synchronises the device. Also reserves the context (rg_reserve) for the calls. */
+int rg_comm_reserve(rg_ctx* ctx, uint32_t max_windows, uint64_t max_slots, uint32_t undecided_cap);
 /* Rank-ordered all-gather: recv_dev = world x `bytes` (send_dev of rank r at r x bytes). */
 int rg_comm_allgather_async(rg_ctx* ctx, const void* send_dev, void* recv_dev, uint64_t bytes, void* stream);
 /* Stages (2)-(4) of the sharded pipeline for n_windows windows of this rank's shard
@@ -276,8 +306,28 @@ int rg_shard_exchange_windows_async(rg_ctx* ctx, uint32_t n_windows, uint32_t* o
                                     uint64_t window_slots, uint64_t max_phase, const uint64_t* records_dev,
                                     uint64_t records_cap, const rg_step_result* rows_dev, rg_step_result* results_dev,
                                     uint32_t* bitmaps_all_dev, void* stream);
+/* The same stages (2)-(4), with the decided-slot payload as undecided lists instead of
+ * committed bitmaps (rg_decision_lists_windows_async per rank, one all-gather): every
+ * rank receives decisions_all_dev = [world][P] u32 words, P = n_windows * (1 +
+ * undecided_cap) + (with_v1 ? n_windows * ceil(n_slots/32) : 0): rank r's undecided list
+ * of window w at r * P + w * (1 + undecided_cap) (count, then up to undecided_cap slot
+ * offsets from rank r's shard start, ascending), then, with_v1, its V1 bitmap of window w
+ * at r * P + n_windows * (1 + undecided_cap) + w * ceil(n_slots/32). A slot of rank r's
+ * shard is committed iff it is not listed; the lists are complete iff no result has flags
+ * value 32 (then fetch the bitmaps: rg_decision_bitmap_windows_async + an all-gather).
+ * with_v1 = 0 for callers that apply only their own shard's batches (the lists and rows
+ * still give every rank the global commit order and watermark). */
+int rg_shard_exchange_decisions_async(rg_ctx* ctx, uint32_t n_windows, uint32_t* out_dev, uint64_t out_pitch_words,
+                                      uint64_t n_slots, uint64_t stride_words, uint64_t slot_base,
+                                      uint64_t window_base, uint64_t window_slots, uint64_t max_phase,
+                                      const uint64_t* records_dev, uint64_t records_cap,
+                                      const rg_step_result* rows_dev, rg_step_result* results_dev,
+                                      uint32_t undecided_cap, uint32_t with_v1, uint32_t* decisions_all_dev,
+                                      void* stream);
 /* Host-synchronous helpers for the caller's control loop (bench timing, shutdown):
- * a barrier over all ranks, and the element-wise max over ranks of 1..64 host doubles. */
+ * a barrier over all ranks, and the element-wise max over ranks of 1..64 host doubles.
+ * Both synchronise the device first (so no exchange of the communicator is still running
+ * on another stream when their collective starts), then run on the context's stream. */
 int rg_comm_barrier(rg_ctx* ctx);
 int rg_comm_max_f64(rg_ctx* ctx, double* values, uint32_t count);
 
@@ -338,6 +388,14 @@ int rg_decision_bitmap_windows_async(rg_ctx* ctx, uint32_t n_windows, const uint
                                      uint64_t out_pitch_words, uint64_t n_slots, uint64_t stride_words,
                                      uint32_t* committed_dev, uint32_t* v1_dev, uint64_t bitmap_pitch_words,
                                      void* stream);
+/* The compact exchange payload of n_windows windows of a shard: lists_dev[w * (1 + cap)]
+ * = the window's count of UNDECIDED slots (output plane 6 clear), followed by the first
+ * min(count, cap) of their offsets in the window (slot id - the window's first slot id),
+ * ascending; v1_dev (optional) = the V1 bitmap (plane 7, bits past n_slots cleared) of
+ * window w at v1_dev + w * v1_pitch_words. */
+int rg_decision_lists_windows_async(rg_ctx* ctx, uint32_t n_windows, const uint32_t* out_dev, uint64_t out_pitch_words,
+                                    uint64_t n_slots, uint64_t stride_words, uint32_t* lists_dev, uint32_t cap,
+                                    uint32_t* v1_dev, uint64_t v1_pitch_words, void* stream);
 
 /* StdRng::seed_from_u64(seed).next_u64() draws first..first+count-1 (random access;
  * the stream the REF mode consumes, engine.rs:461-604). */

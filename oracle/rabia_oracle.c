@@ -206,6 +206,124 @@ int or_ref_step(int n, int q, int self_lane, uint64_t seed, uint64_t rng_base,
 }
 
 /* ------------------------------------------------------------------------- */
+/* Sharded REF, stage 1 (the SHARD step; rabia_amd/csrc/rg_kernels.h           */
+/* ref_lag_kernel<..., SHARD>): or_ref_step over one shard of a window, except  */
+/* that a VQ slot takes no draw (its global stream position, engine.rs:567-611, */
+/* depends on the VQ slots of the lower shards, which this shard does not see): */
+/* its provisional own vote is the likelier outcome of the draw (c1 > c0: V1,   */
+/* c1 < c0: V0, tie: V1, the branches of engine.rs:583-607), and it leaves a    */
+/* draw record with the decision under either own vote (engine.rs:540-542,      */
+/* 624-628). The row counts the NON-VQ slots only; n_draws = the VQ slots;     */
+/* rng_next = n_draws (the provisional position from 0); watermark 0.           */
+/* ------------------------------------------------------------------------- */
+int or_shard_step(int n, int q, int self_lane, uint64_t slot_base, uint64_t max_phase,
+                  const uint8_t* r1, const uint8_t* r2, uint64_t S, uint8_t* o_r1, uint8_t* o_r2own,
+                  uint8_t* o_dec, uint8_t* o_committed, uint8_t* o_value, uint64_t* records,
+                  uint64_t records_cap, or_result* row) {
+  if (n < 1 || n > 16 || q < 1) return -1;
+  memset(row, 0, sizeof *row);
+  uint64_t k = 0, max_v1p1 = 0, first_und = slot_base + S;
+  uint8_t votes2[16];
+  const int lane_ok = self_lane >= 0 && self_lane < n;
+  for (uint64_t s = 0; s < S; s++) {
+    const uint8_t* x1 = r1 + s * n;
+    int c0, c1, cq, present;
+    count3(x1, n, &c0, &c1, &cq, &present);
+    const int res1 = or_ref_round1(x1, n, q);
+    const uint64_t id = slot_base + s;
+    memcpy(votes2, r2 + s * n, (size_t)n);
+    o_r1[s] = (uint8_t)res1;
+    if (res1 == OR_VQ) {
+      const uint32_t cls = c1 > c0 ? 1u : (c1 < c0 ? 2u : 0u);
+      const int prov = cls == 2u ? OR_V0 : OR_V1;
+      if (lane_ok) votes2[self_lane] = OR_V0;
+      const uint32_t d0 = (uint32_t)or_count_votes(votes2, n, q);
+      if (lane_ok) votes2[self_lane] = OR_V1;
+      const uint32_t d1 = (uint32_t)or_count_votes(votes2, n, q);
+      const uint32_t d = prov == OR_V1 ? d1 : d0;
+      o_r2own[s] = (uint8_t)prov;
+      o_dec[s] = (uint8_t)d;
+      o_committed[s] = (uint8_t)(d <= OR_V1);
+      o_value[s] = (uint8_t)(d == OR_V1);
+      const uint32_t info = cls | (d0 << 2) | (d1 << 4) | ((uint32_t)(prov == OR_V1) << 6);
+      if (k < records_cap) records[k] = ((uint64_t)info << 32) | (uint32_t)s;
+      k++;
+      continue;  /* counted by the fix-up */
+    }
+    int own = OR_NONE;
+    if (res1 == OR_V0 || res1 == OR_V1) own = res1;
+    else row->n_pending_r1++;
+    if (own != OR_NONE && lane_ok) votes2[self_lane] = (uint8_t)own;
+    const int d = or_count_votes(votes2, n, q);
+    const int committed = (d == OR_V0 || d == OR_V1);
+    o_r2own[s] = (uint8_t)own;
+    o_dec[s] = (uint8_t)d;
+    o_committed[s] = (uint8_t)committed;
+    o_value[s] = (uint8_t)(d == OR_V1);
+    row->n_decided += (uint64_t)committed;
+    if (d == OR_V1) {
+      row->n_v1++;
+      if (max_phase == 0 || id <= max_phase) max_v1p1 = id + 1;
+    }
+    if (!committed && id < first_und) first_und = id;
+  }
+  row->n_slots = S;
+  row->n_draws = k;
+  row->rng_next = k;
+  row->last_committed_max = max_v1p1 ? max_v1p1 - 1 : 0;
+  row->first_undecided = first_und;
+  row->commit_watermark = 0;
+  return 0;
+}
+
+/* Sharded REF, stage 3 (the fix-up; rg_kernels.h shard_fixup_kernel and
+ * shard_fixup_finish_kernel): record k of the shard is the engine's draw g0 + k, where
+ * g0 = the engine position at the step's first window + every shard's draws of the
+ * earlier windows + the lower shards' draws of this window (ascending slot order over
+ * the whole window, engine.rs:567-611). The draw picks the own vote
+ * (or_ref_round2_vote_for_question) and with it the recorded decision; the outputs of
+ * the VQ slots are rewritten and the VQ slots counted into the row (n_decided, n_v1,
+ * last_committed_max within max_phase, first_undecided). out_row.rng_next = rng_after
+ * (the engine position after this window, every shard's draws); *flags |= 8 when the
+ * records did not fit (n_draws > records_cap: the outputs past the cap stay provisional). */
+int or_shard_fixup(uint64_t seed, uint64_t g0, uint64_t slot_base, uint64_t max_phase,
+                   const uint64_t* records, uint64_t records_cap, uint8_t* o_r2own, uint8_t* o_dec,
+                   uint8_t* o_committed, uint8_t* o_value, const or_result* row, uint64_t rng_after,
+                   or_result* out_row, uint64_t* flags) {
+  uint32_t key[8];
+  or_seed_from_u64(seed, key);
+  *out_row = *row;
+  const uint64_t nn = row->n_draws < records_cap ? row->n_draws : records_cap;
+  uint64_t max_v1p1 = row->last_committed_max ? row->last_committed_max + 1 : 0;
+  for (uint64_t k = 0; k < nn; k++) {
+    const uint32_t off = (uint32_t)records[k], info = (uint32_t)(records[k] >> 32);
+    const uint32_t cls = info & 3u;
+    const int c1 = cls == 1u, c0 = cls == 2u;  /* only the comparison matters */
+    const int own = or_ref_round2_vote_for_question(c0, c1, or_ref_draw(key, g0 + k));
+    const uint32_t d = own == OR_V1 ? (info >> 4) & 3u : (info >> 2) & 3u;
+    const uint64_t id = slot_base + off;
+    o_r2own[off] = (uint8_t)own;
+    o_dec[off] = (uint8_t)d;
+    o_committed[off] = (uint8_t)(d <= OR_V1);
+    o_value[off] = (uint8_t)(d == OR_V1);
+    if (d <= OR_V1) {
+      out_row->n_decided++;
+      if (d == OR_V1) {
+        out_row->n_v1++;
+        if ((max_phase == 0 || id <= max_phase) && id + 1 > max_v1p1) max_v1p1 = id + 1;
+      }
+    } else if (id < out_row->first_undecided) {
+      out_row->first_undecided = id;
+    }
+  }
+  out_row->last_committed_max = max_v1p1 ? max_v1p1 - 1 : 0;
+  out_row->rng_next = rng_after;
+  out_row->commit_watermark = 0;
+  if (row->n_draws > records_cap) *flags |= 8u;
+  return 0;
+}
+
+/* ------------------------------------------------------------------------- */
 /* WMVC phase step, one replica's view (docs/weak_mvc.ivy:129-191; paper     */
 /* Alg. 2). q = majority (n/2+1), fp1 = f+1.                                  */
 /*   round 1 (phase_rnd1, ivy:129-143): needs >= q round-1 messages; vote2 = */

@@ -81,6 +81,7 @@ _SIGS = {
     "rg_destroy": (ctypes.c_int, [vp]),
     "rg_last_error": (ctypes.c_char_p, [vp]),
     "rg_get_config": (ctypes.c_int, [vp, ctypes.POINTER(RgConfig)]),
+    "rg_reserve": (ctypes.c_int, [vp, u64, u32]),
     "rg_set_state": (ctypes.c_int, [vp, ctypes.POINTER(RgEngineState)]),
     "rg_get_state": (ctypes.c_int, [vp, ctypes.POINTER(RgEngineState)]),
     "rg_phase_step_async": (ctypes.c_int, [vp, vp, vp, u64, u64, u64, u64, u64, vp, vp]),
@@ -93,6 +94,7 @@ _SIGS = {
                                                     vp, vp]),
     "rg_shard_commit_windows_async": (ctypes.c_int, [vp, u32, vp, u32, u64, u64, vp, vp]),
     "rg_decision_bitmap_windows_async": (ctypes.c_int, [vp, u32, vp, u64, u64, u64, vp, vp, u64, vp]),
+    "rg_decision_lists_windows_async": (ctypes.c_int, [vp, u32, vp, u64, u64, u64, vp, u32, vp, u64, vp]),
     "rg_shard_commit_async": (ctypes.c_int, [vp, vp, u32, u64, u64, vp, vp]),
     "rg_last_result": (ctypes.c_int, [vp, ctypes.POINTER(RgStepResult)]),
     "rg_last_stage_result": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(RgStepResult)]),
@@ -117,9 +119,12 @@ _SIGS = {
     "rg_comm_create": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int]),
     "rg_comm_destroy": (ctypes.c_int, [vp]),
     "rg_comm_rank": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    "rg_comm_reserve": (ctypes.c_int, [vp, u32, u64, u32]),
     "rg_comm_allgather_async": (ctypes.c_int, [vp, vp, vp, u64, vp]),
     "rg_shard_exchange_windows_async": (ctypes.c_int, [vp, u32, vp, u64, u64, u64, u64, u64, u64, u64, vp, u64, vp,
                                                        vp, vp, vp]),
+    "rg_shard_exchange_decisions_async": (ctypes.c_int, [vp, u32, vp, u64, u64, u64, u64, u64, u64, u64, vp, u64,
+                                                         vp, vp, u32, u32, vp, vp]),
     "rg_comm_barrier": (ctypes.c_int, [vp]),
     "rg_comm_max_f64": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), u32]),
     # kvstore apply (include/rabia_kv.h)

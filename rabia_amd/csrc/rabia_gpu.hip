@@ -165,27 +165,77 @@ Record fresh_record() {
   return r;
 }
 
-// (Re)allocate the per-tile look-back and statistics granules, zeroed so no
-// stale tag can match a live launch sequence number.
-int ensure_tiles(rg_ctx* ctx, uint64_t n_tiles, bool force_zero) {
-  if (n_tiles <= ctx->tile_cap && !force_zero) return RG_OK;
+// Scratch a launch of `slots` slots over `windows` windows may need (rg_reserve):
+// look-back / statistics granules (the smallest tile is 128 words = 4,096 slots, every
+// window a ragged tail; the lag kernel keeps >= 3 x its grid of <= 2 workgroups per CU),
+// fix-up partials (<= kFixGrid per window), decision-list chunk counts.
+uint64_t tiles_for(const rg_ctx* ctx, uint64_t slots, uint32_t windows) {
+  return slots / 4096 + 1 + windows + 6ull * ctx->n_cu;
+}
+uint64_t list_chunks_for(uint64_t slots, uint32_t windows) { return slots / (32ull * kListChunkWords) + 1 + windows; }
+
+// Size the context's scratch for launches of up to max_slots slots over up to max_windows
+// windows (grow only). Synchronous: it frees buffers launches in flight may use, so it
+// is the one place that synchronises the device; the _async entry points never grow
+// scratch and return RG_EINVAL past the reservation instead (include/rabia_gpu.h).
+int reserve_impl(rg_ctx* ctx, uint64_t max_slots, uint32_t max_windows) {
+  if (max_windows < 1) max_windows = 1;
+  if (max_slots < ctx->res_slots) max_slots = ctx->res_slots;
+  if (max_windows < ctx->res_windows) max_windows = ctx->res_windows;
+  const uint64_t tiles = tiles_for(ctx, max_slots, max_windows);
+  const uint64_t acc = 4ull * kFixGrid * max_windows;
+  const uint64_t chunks = list_chunks_for(max_slots, max_windows);
+  if (tiles <= ctx->tile_cap && acc <= ctx->fix_acc_cap && chunks <= ctx->list_counts_cap) {
+    ctx->res_slots = max_slots;
+    ctx->res_windows = max_windows;
+    return RG_OK;
+  }
+  RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
   RG_HIP(ctx, hipDeviceSynchronize());
-  if (n_tiles > ctx->tile_cap) {
-    uint64_t cap = ctx->tile_cap ? ctx->tile_cap : 4096;
-    while (cap < n_tiles) cap *= 2;
+  ctx->res_slots = 0;  // until every array below is in place
+  ctx->res_windows = 0;
+  if (tiles > ctx->tile_cap) {
     (void)hipFree(ctx->lookback);
     (void)hipFree(ctx->stats);
     ctx->lookback = nullptr;
     ctx->stats = nullptr;
     ctx->tile_cap = 0;
-    RG_HIP(ctx, hipMalloc(&ctx->lookback, cap * 8));
-    RG_HIP(ctx, hipMalloc(&ctx->stats, cap * kStatGranules * 8));
-    ctx->tile_cap = cap;
+    RG_HIP(ctx, hipMalloc(&ctx->lookback, tiles * 8));
+    RG_HIP(ctx, hipMalloc(&ctx->stats, tiles * kStatGranules * 8));
+    // zeroed, so no stale tag can match a live launch sequence number
+    RG_HIP(ctx, hipMemset(ctx->lookback, 0, tiles * 8));
+    RG_HIP(ctx, hipMemset(ctx->stats, 0, tiles * kStatGranules * 8));
+    ctx->tile_cap = tiles;
   }
-  RG_HIP(ctx, hipMemset(ctx->lookback, 0, ctx->tile_cap * 8));
-  RG_HIP(ctx, hipMemset(ctx->stats, 0, ctx->tile_cap * kStatGranules * 8));
+  if (acc > ctx->fix_acc_cap) {
+    (void)hipFree(ctx->fix_acc);
+    ctx->fix_acc = nullptr;
+    ctx->fix_acc_cap = 0;
+    RG_HIP(ctx, hipMalloc(&ctx->fix_acc, acc * sizeof(unsigned long long)));
+    ctx->fix_acc_cap = acc;
+  }
+  if (chunks > ctx->list_counts_cap) {
+    (void)hipFree(ctx->list_counts);
+    (void)hipFree(ctx->list_nz);
+    (void)hipFree(ctx->list_pairs);
+    ctx->list_counts = ctx->list_nz = nullptr;
+    ctx->list_pairs = nullptr;
+    ctx->list_counts_cap = 0;
+    RG_HIP(ctx, hipMalloc(&ctx->list_counts, chunks * 4));
+    RG_HIP(ctx, hipMalloc(&ctx->list_nz, chunks * 4));
+    RG_HIP(ctx, hipMalloc(&ctx->list_pairs, chunks * kListPairs * sizeof(uint2)));
+    ctx->list_counts_cap = chunks;
+  }
   RG_HIP(ctx, hipDeviceSynchronize());
+  ctx->res_slots = max_slots;
+  ctx->res_windows = max_windows;
   return RG_OK;
+}
+
+int beyond_reservation(rg_ctx* ctx, const char* who) {
+  return fail(ctx, RG_EINVAL, std::string(who) + ": the launch exceeds the context's reservation (" +
+                                  std::to_string(ctx->res_slots) + " slots, " + std::to_string(ctx->res_windows) +
+                                  " windows per call): call rg_reserve first (an _async call never allocates)");
 }
 
 // Plane addressing for a buffer of `planes` planes in the context's layout and
@@ -308,7 +358,8 @@ int rg_create(rg_ctx** out, const rg_config* cfg) {
   if ((e = hipMalloc(&ctx->state, sizeof(DevState))) != hipSuccess) return bail(e, "hipMalloc(state)");
   if ((e = hipMalloc(&ctx->result, sizeof(DevResult))) != hipSuccess) return bail(e, "hipMalloc(result)");
   if ((e = hipMalloc(&ctx->stage_result, 3 * sizeof(DevResult))) != hipSuccess) return bail(e, "hipMalloc(stage_result)");
-  if ((e = hipMalloc(&ctx->fix_acc, 4 * sizeof(unsigned long long))) != hipSuccess) return bail(e, "hipMalloc(fix_acc)");
+  if ((e = hipMalloc(&ctx->fix_arrivals, sizeof(unsigned int))) != hipSuccess) return bail(e, "hipMalloc(fix_arrivals)");
+  if ((e = hipMemset(ctx->fix_arrivals, 0, sizeof(unsigned int))) != hipSuccess) return bail(e, "init fix_arrivals");
   if ((e = hipMalloc(&ctx->follow_acc, 4ull * kFollowGrid * sizeof(unsigned long long))) != hipSuccess)
     return bail(e, "hipMalloc(follow_acc)");
   Record recs[2] = {fresh_record(), fresh_record()};
@@ -320,7 +371,7 @@ int rg_create(rg_ctx** out, const rg_config* cfg) {
   if ((e = hipMemcpy(ctx->result, &res, sizeof res, hipMemcpyHostToDevice)) != hipSuccess) return bail(e, "init result");
   if ((e = hipMemset(ctx->stage_result, 0, 3 * sizeof(DevResult))) != hipSuccess) return bail(e, "init stage results");
   if ((e = hipDeviceSynchronize()) != hipSuccess) return bail(e, "init sync");
-  if (ensure_tiles(ctx, 4096, true) != RG_OK) {
+  if (reserve_impl(ctx, RG_RESERVE_DEFAULT_SLOTS, RG_RESERVE_DEFAULT_WINDOWS) != RG_OK) {
     g_err = ctx->err;
     rg_destroy(ctx);
     return RG_EHIP;
@@ -353,6 +404,10 @@ int rg_destroy(rg_ctx* ctx) {
   (void)hipFree(ctx->cluster_part);
   (void)hipFree(ctx->cluster_stats);
   (void)hipFree(ctx->fix_acc);
+  (void)hipFree(ctx->fix_arrivals);
+  (void)hipFree(ctx->list_counts);
+  (void)hipFree(ctx->list_nz);
+  (void)hipFree(ctx->list_pairs);
   (void)hipFree(ctx->follow_acc);
   (void)hipFree(ctx->stage_result);
   (void)hipFree(ctx->d_votes);
@@ -470,11 +525,15 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
   const uint32_t lag_grid = (uint32_t)(launch_tiles < lag_grid_max ? launch_tiles : lag_grid_max);
   const uint64_t gran_tiles = lag ? (launch_tiles > 3ull * lag_grid ? launch_tiles : 3ull * lag_grid)
                                   : n_tiles * win.n;
-  if (int rc = ensure_tiles(ctx, gran_tiles, false)) return rc;
+  if (gran_tiles > ctx->tile_cap || n_slots * win.n > ctx->res_slots || win.n > ctx->res_windows)
+    return beyond_reservation(ctx, "rg_phase_step");
+  hipStream_t s = pick_stream(ctx, stream);
   // Statistics granules carry 12 bits of seq and look-back granules 31: start a
-  // fresh epoch on zeroed granules whenever either wraps.
+  // fresh epoch on zeroed granules whenever either wraps (zeroed on the launch's
+  // stream: the context's phase steps are stream-ordered, and nothing else reads them).
   if (++ctx->seq >= (1u << 31) || (ctx->seq & 0xFFFu) == 0) {
-    if (int rc = ensure_tiles(ctx, gran_tiles, true)) return rc;
+    RG_HIP(ctx, hipMemsetAsync(ctx->lookback, 0, ctx->tile_cap * 8, s));
+    RG_HIP(ctx, hipMemsetAsync(ctx->stats, 0, ctx->tile_cap * kStatGranules * 8, s));
     ctx->seq = 2 - (ctx->seq & 1u);  // keep the record-ring parity
   }
   StepParams p;
@@ -522,7 +581,6 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
     RG_HIP(ctx, hipMemsetAsync(ctx->dbg, 0, words * 8, pick_stream(ctx, stream)));
     p.dbg = ctx->dbg;
   }
-  hipStream_t s = pick_stream(ctx, stream);
   ctx->last_launch[0] = lag ? 1u : (wmvc ? 2u : 0u);
   ctx->last_launch[1] = shard ? 1u : 0u;
   ctx->last_launch[2] = lag ? (uint32_t)(lag1024 ? lag_one_block(n) : kLagBlockSmall) : (uint32_t)cfg_block(cfg);
@@ -612,14 +670,8 @@ static int fixup_impl(rg_ctx* ctx, uint32_t n_win, uint32_t* out_dev, uint64_t o
   const uint64_t rec_most = records_cap < n_slots ? records_cap : n_slots;
   const uint64_t blk_most = rec_most / 8 + 2;
   const uint32_t n_part = (uint32_t)std::min<uint64_t>((blk_most + 255) / 256, kFixGrid);
-  if (4ull * n_part * n_win > ctx->fix_acc_cap) {
-    RG_HIP(ctx, hipDeviceSynchronize());
-    (void)hipFree(ctx->fix_acc);
-    ctx->fix_acc = nullptr;
-    ctx->fix_acc_cap = 0;
-    RG_HIP(ctx, hipMalloc(&ctx->fix_acc, 4ull * n_part * n_win * sizeof(unsigned long long)));
-    ctx->fix_acc_cap = 4ull * n_part * n_win;
-  }
+  if (4ull * n_part * n_win > ctx->fix_acc_cap || n_win > ctx->res_windows)
+    return beyond_reservation(ctx, "rg_shard_fixup");
   hipStream_t s = pick_stream(ctx, stream);
   FixParams f;
   f.rec = reinterpret_cast<const unsigned long long*>(records_dev);
@@ -639,8 +691,8 @@ static int fixup_impl(rg_ctx* ctx, uint32_t n_win, uint32_t* out_dev, uint64_t o
   f.out_pitch = out_pitch;
   f.id_stride = id_stride;
   hipLaunchKernelGGL(shard_fixup_kernel, dim3(n_part, n_win), dim3(256), 0, s, f);
-  hipLaunchKernelGGL(shard_fixup_finish_kernel, dim3(1), dim3(256), 0, s, f, ctx->stage_result + 0,
-                     reinterpret_cast<DevResult*>(rows_out_dev));
+  hipLaunchKernelGGL(shard_fixup_finish_kernel, dim3(n_win), dim3(256), 0, s, f, ctx->stage_result + 0,
+                     reinterpret_cast<DevResult*>(rows_out_dev), ctx->fix_arrivals);
   RG_HIP(ctx, hipGetLastError());
   return RG_OK;
 }
@@ -694,28 +746,72 @@ int rg_follower_commit_async(rg_ctx* ctx, const uint32_t* out_dev, uint64_t n_sl
   return RG_OK;
 }
 
-int rg_shard_commit_async(rg_ctx* ctx, const rg_step_result* rows_dev, uint32_t n_shards, uint64_t window_base,
-                          uint64_t window_slots, rg_step_result* result_dev, void* stream) {
+int rg_shard_commit_impl(rg_ctx* ctx, uint32_t n_windows, const rg_step_result* rows_dev, uint32_t n_shards,
+                         uint64_t window_base, uint64_t window_slots, rg_step_result* results_dev, uint64_t und_chk,
+                         void* stream) {
   if (!ctx) return fail(nullptr, RG_EINVAL, "rg_shard_commit: null context");
-  if (!rows_dev || n_shards == 0 || window_slots == 0) return fail(ctx, RG_EINVAL, "rg_shard_commit: bad argument");
+  if (!rows_dev || n_shards == 0 || window_slots == 0 || n_windows == 0)
+    return fail(ctx, RG_EINVAL, "rg_shard_commit: bad argument");
   RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
-  hipLaunchKernelGGL(shard_commit_kernel, dim3(1), dim3(64), 0, pick_stream(ctx, stream),
-                     reinterpret_cast<const DevResult*>(rows_dev), n_shards, 1u, window_base, window_slots, ctx->state,
-                     ctx->stage_result + 1, reinterpret_cast<DevResult*>(result_dev));
+  hipLaunchKernelGGL(shard_commit_kernel, dim3(1), dim3(kCommitBlock), 0, pick_stream(ctx, stream),
+                     reinterpret_cast<const DevResult*>(rows_dev), n_shards, n_windows, window_base, window_slots,
+                     ctx->state, ctx->stage_result + 1, reinterpret_cast<DevResult*>(results_dev), und_chk);
   RG_HIP(ctx, hipGetLastError());
   return RG_OK;
+}
+
+int rg_shard_commit_async(rg_ctx* ctx, const rg_step_result* rows_dev, uint32_t n_shards, uint64_t window_base,
+                          uint64_t window_slots, rg_step_result* result_dev, void* stream) {
+  return rg_shard_commit_impl(ctx, 1, rows_dev, n_shards, window_base, window_slots, result_dev, 0, stream);
 }
 
 int rg_shard_commit_windows_async(rg_ctx* ctx, uint32_t n_windows, const rg_step_result* rows_dev, uint32_t n_shards,
                                   uint64_t window_base, uint64_t window_slots, rg_step_result* results_dev,
                                   void* stream) {
-  if (!ctx) return fail(nullptr, RG_EINVAL, "rg_shard_commit_windows: null context");
-  if (!rows_dev || n_shards == 0 || window_slots == 0 || n_windows == 0)
-    return fail(ctx, RG_EINVAL, "rg_shard_commit_windows: bad argument");
+  return rg_shard_commit_impl(ctx, n_windows, rows_dev, n_shards, window_base, window_slots, results_dev, 0, stream);
+}
+
+int rg_reserve(rg_ctx* ctx, uint64_t max_slots, uint32_t max_windows) {
+  if (!ctx) return fail(nullptr, RG_EINVAL, "rg_reserve: null context");
+  if (max_slots == 0 || max_slots > (1ull << 40) || max_windows == 0 || max_windows > 65535)
+    return fail(ctx, RG_EINVAL, "rg_reserve: 1..2^40 slots, 1..65535 windows");
+  return reserve_impl(ctx, max_slots, max_windows);
+}
+
+int rg_decision_lists_windows_async(rg_ctx* ctx, uint32_t n_windows, const uint32_t* out_dev, uint64_t out_pitch_words,
+                                    uint64_t n_slots, uint64_t stride_words, uint32_t* lists_dev, uint32_t cap,
+                                    uint32_t* v1_dev, uint64_t v1_pitch_words, void* stream) {
+  if (!ctx) return fail(nullptr, RG_EINVAL, "rg_decision_lists_windows: null context");
+  if (!out_dev || !lists_dev || n_slots == 0 || n_slots >= (1ull << 32) || n_windows == 0 || n_windows > 65535)
+    return fail(ctx, RG_EINVAL, "rg_decision_lists_windows: bad argument");
+  const uint64_t n_words = (n_slots + 31) / 32;
+  if (v1_dev && n_windows > 1 && v1_pitch_words < n_words)
+    return fail(ctx, RG_EINVAL, "rg_decision_lists_windows: V1 bitmap pitch < ceil(n_slots/32)");
+  Layout lout;
+  uint64_t need;
+  if (int rc = make_layout(ctx, kOutPlanes, n_words, stride_words, &lout, &need, "rg_decision_lists_windows"))
+    return rc;
+  const uint64_t n_chunks = (n_words + kListChunkWords - 1) / kListChunkWords;
+  if (n_chunks * n_windows > ctx->list_counts_cap || n_windows > ctx->res_windows)
+    return beyond_reservation(ctx, "rg_decision_lists_windows");
   RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
-  hipLaunchKernelGGL(shard_commit_kernel, dim3(1), dim3(64), 0, pick_stream(ctx, stream),
-                     reinterpret_cast<const DevResult*>(rows_dev), n_shards, n_windows, window_base, window_slots,
-                     ctx->state, ctx->stage_result + 1, reinterpret_cast<DevResult*>(results_dev));
+  ListParams L;
+  L.out = out_dev;
+  L.lout = lout;
+  L.n_words = n_words;
+  L.n_slots = n_slots;
+  L.out_pitch = out_pitch_words;
+  L.v1 = v1_dev;
+  L.v1_pitch = v1_pitch_words;
+  L.lists = lists_dev;
+  L.cap = cap;
+  L.counts = ctx->list_counts;
+  L.nz = ctx->list_nz;
+  L.pairs = ctx->list_pairs;
+  L.n_chunks = (uint32_t)n_chunks;
+  hipStream_t s = pick_stream(ctx, stream);
+  hipLaunchKernelGGL(list_scan_kernel, dim3((uint32_t)n_chunks, n_windows), dim3(256), 0, s, L);
+  hipLaunchKernelGGL(list_emit_kernel, dim3((uint32_t)n_chunks, n_windows), dim3(256), 0, s, L);
   RG_HIP(ctx, hipGetLastError());
   return RG_OK;
 }

@@ -85,13 +85,14 @@ struct RgComm {
   DevResult* rows_all = nullptr;   // [world][windows] shard rows (stage 2)
   DevResult* fixed = nullptr;      // [windows] this rank's final rows (stage 3)
   DevResult* fixed_all = nullptr;  // [world][windows] final rows (stage 4)
-  uint64_t rows_cap = 0;           // windows
-  uint32_t* bitmaps = nullptr;     // [windows][2][words] this rank's committed / V1 bitmaps
-  uint64_t bitmaps_cap = 0;        // words
+  uint32_t res_windows = 0;        // rg_comm_reserve: windows per call the rows are sized for
+  uint32_t* payload = nullptr;     // this rank's decision payload (bitmaps, or lists + V1 bitmaps)
+  uint64_t payload_cap = 0;        // words
   double* scalars = nullptr;       // rg_comm_barrier / rg_comm_max_f64 (device, 64 doubles)
 };
 
 constexpr uint32_t kCommScalars = 64;
+constexpr uint32_t kCommDefaultWindows = 128;
 
 void rg_comm_release(rg_ctx* ctx) {
   if (!ctx || !ctx->comm) return;
@@ -101,7 +102,7 @@ void rg_comm_release(rg_ctx* ctx) {
   (void)hipFree(c->rows_all);
   (void)hipFree(c->fixed);
   (void)hipFree(c->fixed_all);
-  (void)hipFree(c->bitmaps);
+  (void)hipFree(c->payload);
   (void)hipFree(c->scalars);
   delete c;
   ctx->comm = nullptr;
@@ -119,19 +120,40 @@ int hip_err(rg_ctx* ctx, hipError_t e, const char* what) {
   return rg_set_error(ctx, RG_EHIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
-// Grow a device scratch array to at least `count` elements (the previous contents are
-// not kept; callers run stream-ordered, so the device is synchronised first).
-template <class T>
-int grow(rg_ctx* ctx, T** p, uint64_t* cap, uint64_t count, const char* what) {
-  if (count <= *cap) return RG_OK;
-  hipError_t e = hipDeviceSynchronize();
-  if (e != hipSuccess) return hip_err(ctx, e, what);
-  (void)hipFree(*p);
-  *p = nullptr;
-  *cap = 0;
-  if ((e = hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T))) != hipSuccess) return hip_err(ctx, e, what);
-  *cap = count;
+// Reserve the rows for max_windows windows and a payload of payload_words words (grow
+// only; the caller synchronised the device). The capacities are published only once every
+// array is in place, so a failed allocation leaves no array the capacity claims.
+int comm_reserve_impl(rg_ctx* ctx, uint32_t max_windows, uint64_t payload_words) {
+  RgComm* c = ctx->comm;
+  hipError_t e;
+  if (max_windows > c->res_windows) {
+    const uint64_t n = (uint64_t)max_windows * (uint64_t)c->world;
+    c->res_windows = 0;
+    DevResult** arrs[3] = {&c->rows_all, &c->fixed, &c->fixed_all};
+    for (DevResult** a : arrs) {
+      (void)hipFree(*a);
+      *a = nullptr;
+    }
+    for (DevResult** a : arrs)
+      if ((e = hipMalloc(reinterpret_cast<void**>(a), n * sizeof(DevResult))) != hipSuccess)
+        return hip_err(ctx, e, "hipMalloc(exchange rows)");
+    c->res_windows = max_windows;
+  }
+  if (payload_words > c->payload_cap) {
+    (void)hipFree(c->payload);
+    c->payload = nullptr;
+    c->payload_cap = 0;
+    if ((e = hipMalloc(&c->payload, payload_words * 4)) != hipSuccess) return hip_err(ctx, e, "hipMalloc(exchange payload)");
+    c->payload_cap = payload_words;
+  }
   return RG_OK;
+}
+
+int comm_beyond(rg_ctx* ctx, const char* who) {
+  return rg_set_error(ctx, RG_EINVAL, std::string(who) + ": the exchange exceeds the communicator's reservation (" +
+                                          std::to_string(ctx->comm->res_windows) + " windows, " +
+                                          std::to_string(ctx->comm->payload_cap) +
+                                          " payload words): call rg_comm_reserve first (an _async call never allocates)");
 }
 
 int gather(rg_ctx* ctx, const void* send, void* recv, uint64_t bytes, hipStream_t s, const char* what) {
@@ -143,6 +165,27 @@ int gather(rg_ctx* ctx, const void* send, void* recv, uint64_t bytes, hipStream_
                                        ctx->comm->comm, s);
   if (e != ncclSuccess) return rg_set_error(ctx, RG_EHIP, rccl_msg(r, e, what));
   return RG_OK;
+}
+
+// Stages 2-4 of a K-window step: the rows all-gathered (rank-major [world][K]), this
+// shard's VQ slots re-drawn at their global positions, the final rows all-gathered and
+// folded window by window into the engine state and results_dev[K].
+int exchange_rows(rg_ctx* ctx, uint32_t n_windows, uint32_t* out_dev, uint64_t out_pitch_words, uint64_t n_slots,
+                  uint64_t stride_words, uint64_t slot_base, uint64_t window_base, uint64_t window_slots,
+                  uint64_t max_phase, const uint64_t* records_dev, uint64_t records_cap, const rg_step_result* rows_dev,
+                  rg_step_result* results_dev, uint64_t und_chk, hipStream_t s) {
+  RgComm* c = ctx->comm;
+  const uint64_t row_bytes = (uint64_t)n_windows * sizeof(DevResult);
+  if (int rc = gather(ctx, rows_dev, c->rows_all, row_bytes, s, "ncclAllGather(rows)")) return rc;
+  if (int rc = rg_shard_fixup_windows_async(ctx, n_windows, out_dev, out_pitch_words, n_slots, stride_words, slot_base,
+                                            window_slots, max_phase, records_dev, records_cap,
+                                            reinterpret_cast<const rg_step_result*>(c->rows_all),
+                                            (uint32_t)c->rank, (uint32_t)c->world,
+                                            reinterpret_cast<rg_step_result*>(c->fixed), s))
+    return rc;
+  if (int rc = gather(ctx, c->fixed, c->fixed_all, row_bytes, s, "ncclAllGather(final rows)")) return rc;
+  return rg_shard_commit_impl(ctx, n_windows, reinterpret_cast<const rg_step_result*>(c->fixed_all),
+                              (uint32_t)c->world, window_base, window_slots, results_dev, und_chk, s);
 }
 
 }  // namespace
@@ -186,7 +229,25 @@ int rg_comm_create(rg_ctx* ctx, const uint8_t* id, int rank, int world) {
     return hip_err(ctx, he, "hipMalloc(comm scalars)");
   }
   ctx->comm = c;
+  if (int rc = comm_reserve_impl(ctx, kCommDefaultWindows, 0)) {
+    rg_comm_release(ctx);
+    return rc;
+  }
   return RG_OK;
+}
+
+int rg_comm_reserve(rg_ctx* ctx, uint32_t max_windows, uint64_t max_slots, uint32_t undecided_cap) {
+  if (int rc = need_comm(ctx, "rg_comm_reserve")) return rc;
+  if (max_windows == 0 || max_windows > 65535 || max_slots == 0 || max_slots >= (1ull << 32))
+    return rg_set_error(ctx, RG_EINVAL, "rg_comm_reserve: 1..65535 windows, 1..2^32-1 slots per window");
+  hipError_t he = hipSetDevice(ctx->cfg.device);
+  if (he != hipSuccess) return hip_err(ctx, he, "hipSetDevice");
+  if ((he = hipDeviceSynchronize()) != hipSuccess) return hip_err(ctx, he, "hipDeviceSynchronize");
+  const uint64_t nw = (max_slots + 31) / 32, K = max_windows;
+  const uint64_t bitmaps = K * 2 * nw, lists = K * (1 + (uint64_t)undecided_cap) + K * nw;
+  if (int rc = comm_reserve_impl(ctx, max_windows, bitmaps > lists ? bitmaps : lists)) return rc;
+  // the calls the exchange makes on the context (fix-up partials, decision lists)
+  return rg_reserve(ctx, max_slots * K, max_windows);
 }
 
 int rg_comm_destroy(rg_ctx* ctx) {
@@ -226,38 +287,51 @@ int rg_shard_exchange_windows_async(rg_ctx* ctx, uint32_t n_windows, uint32_t* o
   if (he != hipSuccess) return hip_err(ctx, he, "hipSetDevice");
   RgComm* c = ctx->comm;
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
-  const uint64_t K = n_windows, W = (uint64_t)c->world;
-  if (K * W > c->rows_cap) {  // the three row arrays grow together
-    uint64_t a = c->rows_cap, b = c->rows_cap, d = c->rows_cap;
-    if (int rc = grow(ctx, &c->rows_all, &a, K * W, "hipMalloc(exchange rows)")) return rc;
-    if (int rc = grow(ctx, &c->fixed, &b, K * W, "hipMalloc(exchange rows)")) return rc;
-    if (int rc = grow(ctx, &c->fixed_all, &d, K * W, "hipMalloc(exchange rows)")) return rc;
-    c->rows_cap = K * W;
-  }
-  const uint64_t row_bytes = K * sizeof(DevResult);
-  // (2) every shard's rows, rank-major [world][K]
-  if (int rc = gather(ctx, rows_dev, c->rows_all, row_bytes, s, "ncclAllGather(rows)")) return rc;
-  // (3) this shard's VQ slots re-drawn at their global positions
-  if (int rc = rg_shard_fixup_windows_async(ctx, n_windows, out_dev, out_pitch_words, n_slots, stride_words, slot_base,
-                                            window_slots, max_phase, records_dev, records_cap,
-                                            reinterpret_cast<const rg_step_result*>(c->rows_all),
-                                            (uint32_t)c->rank, (uint32_t)c->world,
-                                            reinterpret_cast<rg_step_result*>(c->fixed), s))
-    return rc;
-  // (4) every shard's final rows, folded into the engine state window by window
-  if (int rc = gather(ctx, c->fixed, c->fixed_all, row_bytes, s, "ncclAllGather(final rows)")) return rc;
-  if (int rc = rg_shard_commit_windows_async(ctx, n_windows, reinterpret_cast<const rg_step_result*>(c->fixed_all),
-                                             (uint32_t)c->world, window_base, window_slots, results_dev, s))
+  const uint64_t K = n_windows, nw = (n_slots + 31) / 32;
+  if (n_windows > c->res_windows || (bitmaps_all_dev && K * 2 * nw > c->payload_cap))
+    return comm_beyond(ctx, "rg_shard_exchange_windows");
+  if (int rc = exchange_rows(ctx, n_windows, out_dev, out_pitch_words, n_slots, stride_words, slot_base, window_base,
+                             window_slots, max_phase, records_dev, records_cap, rows_dev, results_dev, 0, s))
     return rc;
   if (bitmaps_all_dev) {  // committed / V1 bitmaps of every shard, [world][K][2][words]
-    const uint64_t nw = (n_slots + 31) / 32;
-    if (int rc = grow(ctx, &c->bitmaps, &c->bitmaps_cap, K * 2 * nw, "hipMalloc(exchange bitmaps)")) return rc;
     if (int rc = rg_decision_bitmap_windows_async(ctx, n_windows, out_dev, out_pitch_words, n_slots, stride_words,
-                                                  c->bitmaps, c->bitmaps + nw, 2 * nw, s))
+                                                  c->payload, c->payload + nw, 2 * nw, s))
       return rc;
-    if (int rc = gather(ctx, c->bitmaps, bitmaps_all_dev, K * 2 * nw * 4, s, "ncclAllGather(bitmaps)")) return rc;
+    if (int rc = gather(ctx, c->payload, bitmaps_all_dev, K * 2 * nw * 4, s, "ncclAllGather(bitmaps)")) return rc;
   }
   return RG_OK;
+}
+
+int rg_shard_exchange_decisions_async(rg_ctx* ctx, uint32_t n_windows, uint32_t* out_dev, uint64_t out_pitch_words,
+                                      uint64_t n_slots, uint64_t stride_words, uint64_t slot_base,
+                                      uint64_t window_base, uint64_t window_slots, uint64_t max_phase,
+                                      const uint64_t* records_dev, uint64_t records_cap,
+                                      const rg_step_result* rows_dev, rg_step_result* results_dev,
+                                      uint32_t undecided_cap, uint32_t with_v1, uint32_t* decisions_all_dev,
+                                      void* stream) {
+  if (int rc = need_comm(ctx, "rg_shard_exchange_decisions")) return rc;
+  if (!rows_dev || !results_dev || !decisions_all_dev || n_windows == 0 || n_windows > 65535 || n_slots == 0 ||
+      n_slots >= (1ull << 32) || window_slots < n_slots)
+    return rg_set_error(ctx, RG_EINVAL, "rg_shard_exchange_decisions: bad argument");
+  hipError_t he = hipSetDevice(ctx->cfg.device);
+  if (he != hipSuccess) return hip_err(ctx, he, "hipSetDevice");
+  RgComm* c = ctx->comm;
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
+  const uint64_t K = n_windows, nw = (n_slots + 31) / 32, lw = 1 + (uint64_t)undecided_cap;
+  const uint64_t P = K * lw + (with_v1 ? K * nw : 0);  // payload words per rank
+  if (n_windows > c->res_windows) return comm_beyond(ctx, "rg_shard_exchange_decisions");
+  // stages 2-4; the commit flags (32) a window where a shard has more undecided slots than a list holds
+  if (int rc = exchange_rows(ctx, n_windows, out_dev, out_pitch_words, n_slots, stride_words, slot_base, window_base,
+                             window_slots, max_phase, records_dev, records_cap, rows_dev, results_dev,
+                             (uint64_t)undecided_cap + 1, s))
+    return rc;
+  // this rank's payload (K lists, then with_v1 K V1 bitmaps) built in place at its own slot of
+  // the receive buffer, and one in-place all-gather: no scratch, no local copy of it
+  uint32_t* mine = decisions_all_dev + (uint64_t)c->rank * P;
+  if (int rc = rg_decision_lists_windows_async(ctx, n_windows, out_dev, out_pitch_words, n_slots, stride_words, mine,
+                                               undecided_cap, with_v1 ? mine + K * lw : nullptr, nw, s))
+    return rc;
+  return gather(ctx, mine, decisions_all_dev, P * 4, s, "ncclAllGather(decisions)");
 }
 
 int rg_comm_barrier(rg_ctx* ctx) {
@@ -265,6 +339,8 @@ int rg_comm_barrier(rg_ctx* ctx) {
   const Rccl* r = rccl();
   hipError_t he = hipSetDevice(ctx->cfg.device);
   if (he != hipSuccess) return hip_err(ctx, he, "hipSetDevice");
+  // no exchange of this communicator may still run on another stream (include/rabia_gpu.h)
+  if ((he = hipDeviceSynchronize()) != hipSuccess) return hip_err(ctx, he, "hipDeviceSynchronize");
   const ncclResult_t e = r->all_reduce(ctx->comm->scalars, ctx->comm->scalars, 1, ncclFloat64, ncclMax,
                                        ctx->comm->comm, ctx->stream);
   if (e != ncclSuccess) return rg_set_error(ctx, RG_EHIP, rccl_msg(r, e, "ncclAllReduce(barrier)"));
@@ -279,6 +355,7 @@ int rg_comm_max_f64(rg_ctx* ctx, double* values, uint32_t count) {
   const Rccl* r = rccl();
   hipError_t he = hipSetDevice(ctx->cfg.device);
   if (he != hipSuccess) return hip_err(ctx, he, "hipSetDevice");
+  if ((he = hipDeviceSynchronize()) != hipSuccess) return hip_err(ctx, he, "hipDeviceSynchronize");
   double* d = ctx->comm->scalars;
   if ((he = hipMemcpyAsync(d, values, count * sizeof(double), hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
     return hip_err(ctx, he, "hipMemcpyAsync");

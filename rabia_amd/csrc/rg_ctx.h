@@ -41,8 +41,17 @@ struct rg_ctx {
   unsigned long long* cluster_part = nullptr;  // [blocks][kClusterStats]
   uint64_t cluster_part_cap = 0;                // blocks
   unsigned long long* cluster_stats = nullptr;  // [kClusterStats]
-  unsigned long long* fix_acc = nullptr;        // sharded REF fix-up accumulators [4][windows]
-  uint64_t fix_acc_cap = 4;
+  unsigned long long* fix_acc = nullptr;        // sharded REF fix-up partials [windows][kFixGrid][4]
+  uint64_t fix_acc_cap = 0;                     // u64 elements
+  unsigned int* fix_arrivals = nullptr;         // fix-up finish: workgroups arrived (reset by the last)
+  uint32_t* list_counts = nullptr;              // decision lists: per-chunk undecided counts,
+  uint32_t* list_nz = nullptr;                  //   words holding one, and their (word, mask)
+  uint2* list_pairs = nullptr;                  //   pairs [chunks][kListPairs]
+  uint64_t list_counts_cap = 0;                 // chunks
+  // rg_reserve: the largest launch the context's scratch is sized for (slots over all
+  // windows of one call, windows of one call); *_async calls past it return RG_EINVAL
+  uint64_t res_slots = 0;
+  uint32_t res_windows = 0;
   unsigned long long* follow_acc = nullptr;     // follower commit partials [kFollowGrid][4]
   // results of the shard fix-up / shard commit / follower commit: each stage writes
   // its own (a fix-up may run on another stream than the next window's step, whose
@@ -59,3 +68,9 @@ struct rg_ctx {
 void rg_comm_release(rg_ctx* ctx);
 // rabia_gpu.hip: records msg as the context's (or the thread's) last error, returns code
 int rg_set_error(rg_ctx* ctx, int code, const std::string& msg);
+// rabia_gpu.hip: rg_shard_commit_windows_async with the undecided-list check: und_chk =
+// list capacity + 1 flags (32) a window where some shard has more undecided slots than
+// the capacity; 0 = no check
+extern "C" int rg_shard_commit_impl(rg_ctx* ctx, uint32_t n_windows, const rg_step_result* rows_dev,
+                                    uint32_t n_shards, uint64_t window_base, uint64_t window_slots,
+                                    rg_step_result* results_dev, uint64_t und_chk, void* stream);

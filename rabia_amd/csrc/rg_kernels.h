@@ -1021,6 +1021,15 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p_arg) {
 // workgroup publishes one record and the last to arrive (Record.done) folds them.
 // ============================================================================
 constexpr int kLagPoll = 4;
+// The 512-thread lag kernel (2 waves per SIMD) keeps <= 224 VGPRs, so one 64-VGPR wave of
+// the exchange kernels (the fix-up, finish, commit and decision lists of the previous step,
+// on a second stream) fits beside the sharded step on every SIMD (2 x 224 + 64 = 512); at
+// n = 9 it would take 232 (n <= 8: <= 216 anyway), and the exchange chain then waits for
+// the whole step kernel at each launch. (The request is in units gfx950 doubles, unified
+// VGPR/AGPR file; it cannot depend on the template arguments, so the single evaluator's
+// instantiations carry it too; ignored where the shape's own budget is lower: the
+// 1024-thread forms get 128.)
+#define RG_LAG_REGS __attribute__((amdgpu_num_vgpr(112)))
 constexpr int kLagStatGranules = 6;  // dec v1 pend draws max_off1 min_off, {tag:13 | value:51}
 
 // Poll granules at distances d = 64k + lane below `pos` (index pos - d); indices at
@@ -1325,7 +1334,7 @@ __device__ __forceinline__ void lag_fold_windows(const StepParams& p, Record* re
 // tile's stores by wave 0, and the last workgroup to arrive folds them window by window
 // (one wave per window).
 template <int N, int W, int BLOCK, bool SHARD, int OCC = 4, bool MW = false>
-__global__ __launch_bounds__(BLOCK, OCC) void ref_lag_kernel(StepParams p) {  // OCC waves/SIMD: 2 x 512 or 1 x 1024 per CU
+__global__ __launch_bounds__(BLOCK, OCC) RG_LAG_REGS void ref_lag_kernel(StepParams p) {  // OCC waves/SIMD: 2 x 512 or 1 x 1024 per CU
   static_assert(!MW || SHARD, "multi-window lag launches are sharded launches");
   constexpr int B = ctr_bits(N);
   constexpr int WAVES = BLOCK / 64;
@@ -1994,20 +2003,21 @@ __device__ __forceinline__ unsigned long long fold4(const unsigned long long (&r
   }
   return x;
 }
+template <int U = 8>  // U quadruples per thread in flight at once
 __device__ __forceinline__ void fold_partials(const unsigned long long* acc, uint32_t n, unsigned long long (&red)[4][4],
                                               unsigned long long (&a)[4]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   a[0] = 0; a[1] = 0; a[2] = 0; a[3] = ~0ull;
-  for (uint32_t b0 = threadIdx.x; b0 < n; b0 += 256 * 8) {  // 8 quadruples per thread in flight at once
-    unsigned long long x[8][4];
+  for (uint32_t b0 = threadIdx.x; b0 < n; b0 += 256 * U) {
+    unsigned long long x[U][4];
 #pragma unroll
-    for (int u = 0; u < 8; u++) {
+    for (int u = 0; u < U; u++) {
       const uint32_t b = b0 + 256u * u;
 #pragma unroll
       for (int j = 0; j < 4; j++) x[u][j] = b < n ? acc[(uint64_t)b * 4 + j] : (j == 3 ? ~0ull : 0ull);
     }
 #pragma unroll
-    for (int u = 0; u < 8; u++) {
+    for (int u = 0; u < U; u++) {
       a[0] += x[u][0];
       a[1] += x[u][1];
       a[2] = x[u][2] > a[2] ? x[u][2] : a[2];
@@ -2045,17 +2055,31 @@ struct FixParams {
   uint64_t out_pitch, id_stride;
 };
 
+// Sum of one 64-bit value per thread over a 256-thread workgroup, returned to every
+// thread (red: 4 LDS words; the trailing barrier lets the caller reuse them).
+__device__ __forceinline__ unsigned long long block_sum256(unsigned long long v, unsigned long long* red) {
+  v = wave_sum64(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  v = red[0] + red[1] + red[2] + red[3];
+  __syncthreads();
+  return v;
+}
+
 // Global stream position of local draw 0 of window w of shard f.shard: the engine
 // position at the first window + every shard's draws of the earlier windows + the
-// lower shards' draws of window w (ascending slot order, engine.rs:567-611).
-__device__ __forceinline__ unsigned long long fix_first_draw(const FixParams& f, uint32_t w) {
-  unsigned long long pre = f.state->rng_next;
-  for (uint32_t r = 0; r < f.n_shards; r++) {
-    const DevResult* rr = f.rows + (uint64_t)r * f.n_win;
-    for (uint32_t v = 0; v < w; v++) pre += rr[v].n_draws;
-    if (r < f.shard) pre += rr[w].n_draws;
+// lower shards' draws of window w (ascending slot order, engine.rs:567-611). Summed by
+// the whole workgroup, one row per thread: round 5 ran it as a chain of n_shards x w
+// dependent scalar loads in every thread (256 at the 8-GPU C5 shape, 32 windows), which
+// was most of the fix-up's time there.
+__device__ __forceinline__ unsigned long long fix_first_draw(const FixParams& f, uint32_t w, unsigned long long* red) {
+  unsigned long long pre = 0;
+  const uint64_t n_rows = (uint64_t)f.n_shards * f.n_win;
+  for (uint64_t i = threadIdx.x; i < n_rows; i += 256) {
+    const uint32_t r = (uint32_t)(i / f.n_win), v = (uint32_t)(i % f.n_win);
+    if (v < w || (v == w && r < f.shard)) pre += f.rows[i].n_draws;
   }
-  return pre;
+  return f.state->rng_next + block_sum256(pre, red);
 }
 
 // The fix-up, one thread per ChaCha12 block of the window's global draw positions
@@ -2068,67 +2092,86 @@ __device__ __forceinline__ unsigned long long fix_first_draw(const FixParams& f,
 // on a block of its own, so no lane idles on a partial pass and no LDS is needed; the
 // statistics are one partial per workgroup.
 constexpr uint32_t kFixGrid = 2048;  // fix-up workgroups at most (grid-stride beyond)
-static __global__ __launch_bounds__(256) void shard_fixup_kernel(FixParams f) {
+// The exchange-stage kernels (fix-up, finish, commit, decision lists) run on a second
+// stream while the NEXT step's persistent lag kernel holds every CU: one 512-thread
+// workgroup per CU at 2 waves per SIMD, 232 VGPRs each at n = 9 (168 at n = 5) and 129 KB
+// of LDS. A wave of these kernels fits beside it only within the 48 VGPRs per SIMD that
+// leaves; above that it cannot be placed before the lag kernel ends, so every kernel of
+// the exchange chain waited a whole step kernel (round 5: the finish kernel's 266 us).
+// So: the exchange kernels at <= 64 VGPRs (8 waves per SIMD, the hardware's maximum, is
+// the lowest budget the compiler takes), and the lag kernel at <= 224 (RG_LAG_REGS).
+static __global__ __launch_bounds__(256, 8) void shard_fixup_kernel(FixParams f) {
+  __shared__ unsigned long long sred[4];
   const uint32_t win = blockIdx.y;
   const unsigned long long n = f.rows[(uint64_t)f.shard * f.n_win + win].n_draws;
-  const unsigned long long g0 = fix_first_draw(f, win);  // global position of local draw 0
+  const unsigned long long g0 = fix_first_draw(f, win, sred);  // global position of local draw 0
   if (win) {  // this window's outputs, slot ids, records
     f.out += win * f.out_pitch;
     f.slot_base += win * f.id_stride;
     f.rec += win * f.vq_cap;
   }
   const unsigned long long nn = n < f.vq_cap ? n : f.vq_cap;
-  unsigned long long dec = 0, v1 = 0, mx = 0, mn = ~0ull;
+  // per-thread statistics in 32 bits (window-relative offsets: max V1 offset + 1, min
+  // undecided offset), widened for the workgroup fold
+  uint32_t dec = 0, v1 = 0, mx = 0, mn = ~0u;
+  const uint64_t lim = f.max_phase == 0 ? ~0ull : (f.max_phase >= f.slot_base ? f.max_phase - f.slot_base : 0);
+  const bool any_in = f.max_phase == 0 || f.max_phase >= f.slot_base;  // some slot id <= max_phase
   uint32_t* p2 = f.out + 2 * f.lout.pstride;
   const unsigned long long b_end = (g0 + nn + 7) >> 3;
   for (unsigned long long b = (g0 >> 3) + (unsigned long long)blockIdx.x * 256 + threadIdx.x; nn && b < b_end;
        b += (unsigned long long)gridDim.x * 256) {
     const long long k0 = (long long)(b << 3) - (long long)g0;  // local index of the block's first draw
-    unsigned long long rr[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      const long long k = k0 + j;
-      rr[j] = (k >= 0 && (unsigned long long)k < nn) ? f.rec[k] : ~0ull;
-    }
+    // the block first, then the records: the ChaCha state and the 8 records are never live
+    // together, so the kernel fits the 64 VGPRs it may take beside the next step's lag kernel
     uint32_t x[16];
     chacha_block<12>(f.key, b, 0, x);
     uint32_t cur_w = ~0u, cur_m = 0;  // the run's word being patched and its XOR mask
+    const bool whole = k0 >= 0 && (unsigned long long)k0 + 8 <= nn;  // all but the ends
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
-      const unsigned long long r = rr[j];
-      if (r == ~0ull) continue;
-      const uint32_t off = (uint32_t)r, info = (uint32_t)(r >> 32);
-      const unsigned long long u = (unsigned long long)x[2 * j] | ((unsigned long long)x[2 * j + 1] << 32);
-      const uint32_t cls = info & 3u;
-      const uint32_t own = cls == kRecGt ? (u < kP90) : (cls == kRecLt ? (u >= kP90) : (u < kP80));
-      const uint32_t prov = (info >> 6) & 1u;
-      const uint32_t d = own ? (info >> 4) & 3u : (info >> 2) & 3u;
-      const unsigned long long id = f.slot_base + off;
-      if (d <= kCodeV1) {
-        dec++;
-        if (d == kCodeV1) {
-          v1++;
-          if ((f.max_phase == 0 || id <= f.max_phase) && id + 1 > mx) mx = id + 1;
-        }
-      } else if (id < mn) {
-        mn = id;
+    for (int h = 0; h < 2; h++) {  // the 8 records in two halves (register budget)
+      unsigned long long rr[4];
+#pragma unroll
+      for (int jj = 0; jj < 4; jj++) {
+        const long long k = k0 + 4 * h + jj;
+        rr[jj] = (whole || (k >= 0 && (unsigned long long)k < nn)) ? f.rec[k] : ~0ull;
       }
-      if (own != prov) {
-        const uint32_t w = off >> 5, bit = 1u << (off & 31u);
-        if (w != cur_w) {
-          if (cur_m) atomicXor(p2 + f.lout.base(cur_w), cur_m);
-          cur_w = w;
-          cur_m = 0;
+#pragma unroll
+      for (int jj = 0; jj < 4; jj++) {
+        const int j = 4 * h + jj;
+        const unsigned long long r = rr[jj];
+        if (r == ~0ull) continue;
+        const uint32_t off = (uint32_t)r, info = (uint32_t)(r >> 32);
+        const unsigned long long u = (unsigned long long)x[2 * j] | ((unsigned long long)x[2 * j + 1] << 32);
+        const uint32_t cls = info & 3u;
+        const uint32_t own = cls == kRecGt ? (u < kP90) : (cls == kRecLt ? (u >= kP90) : (u < kP80));
+        const uint32_t prov = (info >> 6) & 1u;
+        const uint32_t d = own ? (info >> 4) & 3u : (info >> 2) & 3u;
+        if (d <= kCodeV1) {
+          dec++;
+          if (d == kCodeV1) {
+            v1++;
+            if (any_in && off <= lim && off + 1 > mx) mx = off + 1;
+          }
+        } else if (off < mn) {
+          mn = off;
         }
-        cur_m ^= bit;
-        const uint32_t dp = prov ? (info >> 4) & 3u : (info >> 2) & 3u;
-        const uint32_t dd = d ^ dp;
-        if (dd || (d <= kCodeV1) != (dp <= kCodeV1)) {  // the decision changed: rare
-          const uint64_t base = f.lout.base(w);
-          if (dd & 1u) atomicXor(f.out + base + 4 * f.lout.pstride, bit);
-          if (dd & 2u) atomicXor(f.out + base + 5 * f.lout.pstride, bit);
-          if ((d <= kCodeV1) != (dp <= kCodeV1)) atomicXor(f.out + base + 6 * f.lout.pstride, bit);
-          if ((d == kCodeV1) != (dp == kCodeV1)) atomicXor(f.out + base + 7 * f.lout.pstride, bit);
+        if (own != prov) {
+          const uint32_t w = off >> 5, bit = 1u << (off & 31u);
+          if (w != cur_w) {
+            if (cur_m) atomicXor(p2 + f.lout.base(cur_w), cur_m);
+            cur_w = w;
+            cur_m = 0;
+          }
+          cur_m ^= bit;
+          const uint32_t dp = prov ? (info >> 4) & 3u : (info >> 2) & 3u;
+          const uint32_t dd = d ^ dp;
+          if (dd || (d <= kCodeV1) != (dp <= kCodeV1)) {  // the decision changed: rare
+            const uint64_t base = f.lout.base(w);
+            if (dd & 1u) atomicXor(f.out + base + 4 * f.lout.pstride, bit);
+            if (dd & 2u) atomicXor(f.out + base + 5 * f.lout.pstride, bit);
+            if ((d <= kCodeV1) != (dp <= kCodeV1)) atomicXor(f.out + base + 6 * f.lout.pstride, bit);
+            if ((d == kCodeV1) != (dp == kCodeV1)) atomicXor(f.out + base + 7 * f.lout.pstride, bit);
+          }
         }
       }
     }
@@ -2136,84 +2179,127 @@ static __global__ __launch_bounds__(256) void shard_fixup_kernel(FixParams f) {
   }
   __shared__ unsigned long long red[4][4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  dec = wave_sum64(dec);
-  v1 = wave_sum64(v1);
-  mx = wave_max64(mx);
-  mn = wave_min64(mn);
-  if (lane == 0) { red[wave][0] = dec; red[wave][1] = v1; red[wave][2] = mx; red[wave][3] = mn; }
+  const unsigned long long dsum = wave_sum64(dec), vsum = wave_sum64(v1);
+  const unsigned long long mxx = wave_max64(mx ? f.slot_base + mx : 0ull);  // max V1 id + 1
+  const unsigned long long mnn = wave_min64(mn != ~0u ? f.slot_base + mn : ~0ull);
+  if (lane == 0) { red[wave][0] = dsum; red[wave][1] = vsum; red[wave][2] = mxx; red[wave][3] = mnn; }
   __syncthreads();
   // every workgroup writes its partial (zeros / all ones when it had no records)
   if (threadIdx.x < 4) f.acc[((uint64_t)win * f.n_part + blockIdx.x) * 4 + threadIdx.x] = fold4(red, threadIdx.x);
 }
 
 
-// The shard's final row: VQ-slot counts and extremes folded in, the engine's
-// stream position advanced past the whole window's draws (every shard's).
-static __global__ __launch_bounds__(256) void shard_fixup_finish_kernel(FixParams f, DevResult* row_ctx,
-                                                                        DevResult* row_user) {
+// The shard's final rows: VQ-slot counts and extremes folded in, the engine's stream
+// position advanced past the whole window's draws (every shard's). One workgroup per
+// window (round 5 folded the windows one after another in one workgroup: 266 us at the
+// 8-GPU C5 shape, 32 windows, longer than the step kernel): window w's partials, and
+// its position = the engine position + every shard's draws of windows 0..w. The
+// context's rng_next is read by every workgroup and written by the last to arrive.
+static __global__ __launch_bounds__(256, 8) void shard_fixup_finish_kernel(FixParams f, DevResult* row_ctx,
+                                                                        DevResult* row_user, unsigned int* arrivals) {
   __shared__ unsigned long long red[4][4];
-  unsigned long long pos = f.state->rng_next;
-  for (uint32_t w = 0; w < f.n_win; w++) {
-    unsigned long long a[4];  // the window's workgroup partials (shard_fixup_kernel)
-    fold_partials(f.acc + (uint64_t)w * f.n_part * 4, f.n_part, red, a);
-    if (threadIdx.x != 0) continue;
-    const unsigned long long a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3];
-    DevResult r = f.rows[(uint64_t)f.shard * f.n_win + w];
-    unsigned long long total = 0;
-    for (uint32_t s = 0; s < f.n_shards; s++) total += f.rows[(uint64_t)s * f.n_win + w].n_draws;
-    r.n_decided += a0;
-    r.n_v1 += a1;
-    if (a2 && a2 - 1 > r.last_committed_max) r.last_committed_max = a2 - 1;
-    if (a3 < r.first_undecided) r.first_undecided = a3;
-    if (r.n_draws > f.vq_cap) r.flags |= 8ull;  // records did not fit: the patch is incomplete
-    // only rng_next: a later window's shard step (shard_draws) may run on another stream
-    pos += total;
-    r.rng_next = pos;
-    r.commit_watermark = 0;
-    if (w + 1 == f.n_win) *row_ctx = r;
-    if (row_user) row_user[w] = r;
+  __shared__ unsigned long long sred[4];
+  const uint32_t w = blockIdx.x;
+  unsigned long long a[4];  // the window's workgroup partials (shard_fixup_kernel)
+  fold_partials<2>(f.acc + (uint64_t)w * f.n_part * 4, f.n_part, red, a);  // <= 2 x 256 partials per window
+  unsigned long long upto = 0, all = 0;  // draws of windows <= w, of every window (every shard)
+  const uint64_t n_rows = (uint64_t)f.n_shards * f.n_win;
+  for (uint64_t i = threadIdx.x; i < n_rows; i += 256) {
+    const unsigned long long d = f.rows[i].n_draws;
+    all += d;
+    if (i % f.n_win <= w) upto += d;
   }
-  if (threadIdx.x == 0) f.state->rng_next = pos;
+  upto = block_sum256(upto, sred);
+  all = block_sum256(all, sred);
+  if (threadIdx.x != 0) return;
+  const unsigned long long base = f.state->rng_next;  // before any workgroup's arrival (below)
+  DevResult r = f.rows[(uint64_t)f.shard * f.n_win + w];
+  r.n_decided += a[0];
+  r.n_v1 += a[1];
+  if (a[2] && a[2] - 1 > r.last_committed_max) r.last_committed_max = a[2] - 1;
+  if (a[3] < r.first_undecided) r.first_undecided = a[3];
+  if (r.n_draws > f.vq_cap) r.flags |= 8ull;  // records did not fit: the patch is incomplete
+  r.rng_next = base + upto;
+  r.commit_watermark = 0;
+  if (w + 1 == f.n_win) *row_ctx = r;
+  if (row_user) row_user[w] = r;
+  __threadfence();
+  // only rng_next: a later window's shard step (shard_draws) may run on another stream
+  if (atomicAdd(arrivals, 1u) + 1u == f.n_win) {
+    f.state->rng_next = base + all;
+    __hip_atomic_store(arrivals, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
-// Fold the shards' final rows of one window into the engine state exactly as one
-// evaluator over the whole window: commit_phase max (state.rs:77-99), first
-// undecided = min over shards, contiguous watermark advance.
-static __global__ void shard_commit_kernel(const DevResult* rows_all, uint32_t n_shards, uint32_t n_win,
-                                    uint64_t window_base0, uint64_t window_slots, DevState* state, DevResult* res_ctx,
-                                    DevResult* res_user) {
-  if (threadIdx.x != 0) return;
-  for (uint32_t w = 0; w < n_win; w++) {  // consecutive windows, in order (the watermark chains)
-    const uint64_t window_base = window_base0 + w * window_slots;
-    DevState s = *state;
+// Fold the shards' final rows of consecutive windows into the engine state exactly as
+// one evaluator over the windows in order: commit_phase max (state.rs:77-99), first
+// undecided = min over shards, contiguous watermark advance. One thread per window
+// loads and folds its window's rows (round 5: one thread for every window and shard,
+// 17 us at 32 windows x 8 shards); thread 0 then chains last_committed and the
+// watermark over the window values in LDS. und_chk = list capacity + 1 (0: no check): a
+// shard with more undecided slots than the capacity flags the window (32: its undecided
+// list is truncated).
+constexpr uint32_t kCommitBlock = 256;
+static __global__ __launch_bounds__(kCommitBlock, 8) void shard_commit_kernel(
+    const DevResult* rows_all, uint32_t n_shards, uint32_t n_win, uint64_t window_base0, uint64_t window_slots,
+    DevState* state, DevResult* res_ctx, DevResult* res_user, uint64_t und_chk) {
+  __shared__ unsigned long long s_fu[kCommitBlock], s_lc[kCommitBlock], s_wm[kCommitBlock];
+  const uint32_t tid = threadIdx.x;
+  unsigned long long lc = 0, wm = 0, steps = 0;  // thread 0: the chain
+  if (tid == 0) {
+    lc = state->last_committed;
+    wm = state->commit_watermark;
+    steps = state->steps;
+  }
+  for (uint32_t c0 = 0; c0 < n_win; c0 += kCommitBlock) {
+    const uint32_t w = c0 + tid;
     DevResult g;
     g.n_slots = g.n_decided = g.n_v1 = g.n_pending_r1 = g.n_draws = g.flags = 0;
-    unsigned long long lc = s.last_committed;
-    const unsigned long long end = window_base + window_slots;
-    unsigned long long fu = end;
-    for (uint32_t r = 0; r < n_shards; r++) {
-      const DevResult& x = rows_all[(uint64_t)r * n_win + w];
-      g.n_slots += x.n_slots;
-      g.n_decided += x.n_decided;
-      g.n_v1 += x.n_v1;
-      g.n_pending_r1 += x.n_pending_r1;
-      g.n_draws += x.n_draws;
-      g.flags |= x.flags;
-      if (x.last_committed_max > lc) lc = x.last_committed_max;
-      if (x.n_slots && x.first_undecided < fu) fu = x.first_undecided;
+    const uint64_t window_base = window_base0 + (uint64_t)w * window_slots;
+    unsigned long long lcx = 0, fu = window_base + window_slots;
+    if (w < n_win) {
+      for (uint32_t r = 0; r < n_shards; r++) {
+        const DevResult& x = rows_all[(uint64_t)r * n_win + w];
+        g.n_slots += x.n_slots;
+        g.n_decided += x.n_decided;
+        g.n_v1 += x.n_v1;
+        g.n_pending_r1 += x.n_pending_r1;
+        g.n_draws += x.n_draws;
+        g.flags |= x.flags;
+        if (und_chk && x.n_slots - x.n_decided >= und_chk) g.flags |= 32ull;
+        if (x.last_committed_max > lcx) lcx = x.last_committed_max;
+        if (x.n_slots && x.first_undecided < fu) fu = x.first_undecided;
+      }
+      if (g.n_slots != window_slots) g.flags |= 16ull;  // the rows do not tile the window
+      s_fu[tid] = fu;
+      s_lc[tid] = lcx;
     }
-    if (g.n_slots != window_slots) g.flags |= 16ull;  // the rows do not tile the window
-    unsigned long long wm = s.commit_watermark;
-    if (window_base <= wm && wm < fu) wm = fu;
-    g.last_committed_max = lc;
-    g.first_undecided = fu;
-    g.rng_next = rows_all[w].rng_next;  // the fixed rows carry the position after window w
-    g.commit_watermark = wm;
-    state->last_committed = lc;  // the fields it owns (the shard step and fix-up own the others)
+    __syncthreads();
+    if (tid == 0) {  // the chain: in window order
+      const uint32_t m = n_win - c0 < kCommitBlock ? n_win - c0 : kCommitBlock;
+      for (uint32_t i = 0; i < m; i++) {
+        const uint64_t b = window_base0 + (uint64_t)(c0 + i) * window_slots;
+        if (s_lc[i] > lc) lc = s_lc[i];
+        if (b <= wm && wm < s_fu[i]) wm = s_fu[i];
+        s_lc[i] = lc;
+        s_wm[i] = wm;
+      }
+    }
+    __syncthreads();
+    if (w < n_win) {
+      g.last_committed_max = s_lc[tid];
+      g.first_undecided = fu;
+      g.rng_next = rows_all[w].rng_next;  // the fixed rows carry the position after window w
+      g.commit_watermark = s_wm[tid];
+      if (w + 1 == n_win) *res_ctx = g;
+      if (res_user) res_user[w] = g;
+    }
+    __syncthreads();  // s_* are rewritten by the next chunk
+  }
+  if (tid == 0) {  // the fields it owns (the shard step and fix-up own the others)
+    state->last_committed = lc;
     state->commit_watermark = wm;
-    state->steps = s.steps + 1;
-    if (w + 1 == n_win) *res_ctx = g;
-    if (res_user) res_user[w] = g;
+    state->steps = steps + n_win;
   }
 }
 
@@ -2568,6 +2654,172 @@ static __global__ void bitmap_kernel(const uint32_t* out, Layout lout, uint64_t 
   const uint64_t b = lout.base(w);
   committed[w] = out[b + 6 * lout.pstride];
   v1[w] = out[b + 7 * lout.pstride];
+}
+
+// ---- the decided-slot exchange payload (rg_decision_lists_windows_async) ------------
+// Per window of a shard: the list of its UNDECIDED slots (committed bit 0), ascending,
+// as slot offsets from the shard's first slot, and optionally the V1 bitmap (plane 7 as
+// one contiguous bit array, bits past n_slots cleared). At agree90 ~0.04 % of the slots
+// are undecided, so the list replaces a committed bitmap that is ~99.96 % ones (1 bit
+// per slot) with ~0.013 bits per slot. Two passes over 4096-word chunks (131,072 slots,
+// one 256-thread workgroup each; a thread reads 16-B groups, so a wave keeps 8 KiB in
+// flight: these kernels run beside the next step's lag kernel, one wave per SIMD, and
+// must pull their bytes with few waves):
+//  (1) list_scan: the chunk's V1 words, its undecided count, and its words holding an
+//      undecided slot as (word, mask) pairs in word order (at most kListPairs; more: the
+//      second pass re-reads the chunk's committed plane);
+//  (2) list_emit: the chunk's offset in the list = the counts of the chunks before it;
+//      every pair expands into slot offsets.
+// The list holds at most `cap` entries; its first word is the true count (count > cap:
+// truncated).
+constexpr uint32_t kListChunkWords = 4096, kListPairs = 128;
+struct ListParams {
+  const uint32_t* out;  // window w at out + w * out_pitch
+  Layout lout;
+  uint64_t n_words, n_slots, out_pitch;
+  uint32_t* v1;         // optional: window w at v1 + w * v1_pitch
+  uint64_t v1_pitch;
+  uint32_t* lists;      // [n_win][1 + cap]
+  uint32_t cap;
+  uint32_t* counts;     // [n_win][n_chunks] undecided slots of the chunk
+  uint32_t* nz;         // [n_win][n_chunks] words of the chunk holding one
+  uint2* pairs;         // [n_win][n_chunks][kListPairs] (word, undecided mask)
+  uint32_t n_chunks;
+};
+
+// Exclusive prefix over a 256-thread workgroup of one u32 per thread (returned) and the
+// total (tot); buf: two parity halves of 4 words, par alternating between calls.
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t c, uint32_t (&buf)[2][4], int par, uint32_t& tot) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t incl = wave_incl_scan32(c, (int)lane);
+  if (lane == 63) buf[par][wave] = incl;
+  __syncthreads();  // (a half is rewritten two calls later, after every thread read it)
+  uint32_t pre = 0;
+  tot = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; k++) {
+    const uint32_t t = buf[par][k];
+    pre += k < wave ? t : 0u;
+    tot += t;
+  }
+  return pre + incl - c;
+}
+
+// The 4 words [w, w + 4) of a plane, w a multiple of 4 (one 16-B load: a group never
+// crosses a slot tile, T >= 64, or a 4-word-multiple planar stride).
+__device__ __forceinline__ u32x4 load_group(const uint32_t* out, const Layout& lo, uint64_t w, int plane) {
+  return *reinterpret_cast<const u32x4*>(out + lo.base(w) + plane * lo.pstride);
+}
+
+static __global__ __launch_bounds__(256, 8) void list_scan_kernel(ListParams L) {
+  __shared__ uint32_t sbuf[2][4];
+  __shared__ unsigned long long sred[4];
+  const uint32_t win = blockIdx.y, chunk = blockIdx.x, tid = threadIdx.x;
+  const uint32_t* out = L.out + win * L.out_pitch;
+  const uint64_t cidx = (uint64_t)win * L.n_chunks + chunk;
+  uint2* pairs = L.pairs + cidx * kListPairs;
+  uint32_t run = 0, pop = 0;
+#pragma unroll 1
+  for (int j = 0; j < 4; j++) {
+    const uint64_t w = (uint64_t)chunk * kListChunkWords + j * 1024 + 4 * tid;
+    uint32_t und[4] = {0, 0, 0, 0};
+    if (w < L.n_words) {
+      const u32x4 c = load_group(out, L.lout, w, 6);
+      u32x4 v = c;
+      if (L.v1) v = load_group(out, L.lout, w, 7);
+      const uint32_t cw[4] = {c.x, c.y, c.z, c.w};
+      const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint32_t vm = valid_mask(w + q, L.n_words, L.n_slots);
+        und[q] = ~cw[q] & vm;
+        if (L.v1 && w + q < L.n_words) L.v1[win * L.v1_pitch + w + q] = vw[q] & vm;
+      }
+    }
+    uint32_t nzc = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      nzc += und[q] ? 1u : 0u;
+      pop += (uint32_t)__builtin_popcount(und[q]);
+    }
+    uint32_t tot;
+    uint32_t pos = run + block_excl_scan256(nzc, sbuf, j & 1, tot);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      if (und[q]) {
+        if (pos < kListPairs) pairs[pos] = make_uint2((uint32_t)(w + q), und[q]);
+        pos++;
+      }
+    }
+    run += tot;
+  }
+  const unsigned long long c = block_sum256(pop, sred);
+  if (tid == 0) {
+    L.counts[cidx] = (uint32_t)c;
+    L.nz[cidx] = run;
+  }
+}
+
+static __global__ __launch_bounds__(256, 8) void list_emit_kernel(ListParams L) {
+  __shared__ unsigned long long sred[4];
+  __shared__ uint32_t sbuf[2][4];
+  const uint32_t win = blockIdx.y, chunk = blockIdx.x, tid = threadIdx.x;
+  const uint32_t* cnts = L.counts + (uint64_t)win * L.n_chunks;
+  unsigned long long before = 0, total = 0;
+  for (uint32_t c = tid; c < L.n_chunks; c += 256) {
+    const uint32_t x = cnts[c];
+    total += x;
+    if (c < chunk) before += x;
+  }
+  before = block_sum256(before, sred);
+  total = block_sum256(total, sred);
+  uint32_t* lst = L.lists + (uint64_t)win * (1ull + L.cap);
+  if (chunk == 0 && tid == 0) lst[0] = (uint32_t)total;
+  if (cnts[chunk] == 0 || before >= L.cap) return;  // uniform: nothing of this chunk is listed
+  const uint64_t cidx = (uint64_t)win * L.n_chunks + chunk;
+  const uint32_t nz = L.nz[cidx];
+  if (nz <= kListPairs) {  // the pairs, one per thread (kListPairs <= the workgroup size)
+    uint2 pr = make_uint2(0u, 0u);
+    if (tid < nz) pr = L.pairs[cidx * kListPairs + tid];
+    uint32_t tot;
+    unsigned long long pos = before + block_excl_scan256((uint32_t)__builtin_popcount(pr.y), sbuf, 0, tot);
+    uint32_t m = pr.y;
+    while (m) {
+      if (pos < L.cap) lst[1 + pos] = 32u * pr.x + (uint32_t)__builtin_ctz(m);
+      pos++;
+      m &= m - 1u;
+    }
+    return;
+  }
+  // more words with undecided slots than pairs: re-read the chunk's committed plane
+  const uint32_t* out = L.out + win * L.out_pitch;
+  unsigned long long run = before;
+#pragma unroll 1
+  for (int j = 0; j < 4; j++) {
+    const uint64_t w = (uint64_t)chunk * kListChunkWords + j * 1024 + 4 * tid;
+    uint32_t und[4] = {0, 0, 0, 0};
+    if (w < L.n_words) {
+      const u32x4 c = load_group(out, L.lout, w, 6);
+      const uint32_t cw[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+      for (int q = 0; q < 4; q++) und[q] = ~cw[q] & valid_mask(w + q, L.n_words, L.n_slots);
+    }
+    uint32_t c = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) c += (uint32_t)__builtin_popcount(und[q]);
+    uint32_t tot;
+    unsigned long long pos = run + block_excl_scan256(c, sbuf, j & 1, tot);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      uint32_t m = und[q];
+      while (m) {
+        if (pos < L.cap) lst[1 + pos] = (uint32_t)(32 * (w + q) + (uint32_t)__builtin_ctz(m));
+        pos++;
+        m &= m - 1u;
+      }
+    }
+    run += tot;
+  }
 }
 
 // ---- own round-1 votes for received proposals (engine.rs:380-481) -------------

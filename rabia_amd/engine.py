@@ -222,6 +222,12 @@ class PhaseEvaluator:
     def __exit__(self, *a):
         self.close()
 
+    def reserve(self, max_slots: int, max_windows: int = 1):
+        """rg_reserve: size the context's scratch for calls of up to max_slots slots (all
+        windows of one call) and max_windows windows. Synchronous; the _async calls never
+        allocate and raise RG_EINVAL past the reservation (rg_create reserves 2^32 / 128)."""
+        N.check(self.lib.rg_reserve(self.ctx, int(max_slots), int(max_windows)), self.ctx)
+
     # -- engine state -----------------------------------------------------
     def get_state(self) -> dict:
         st = N.RgEngineState()
@@ -344,6 +350,11 @@ class PhaseEvaluator:
         N.check(self.lib.rg_comm_rank(self.ctx, ctypes.byref(r), ctypes.byref(w)), self.ctx)
         return r.value, w.value
 
+    def comm_reserve(self, max_windows: int, max_slots: int, undecided_cap: int = 0):
+        """rg_comm_reserve: the exchange scratch for up to max_windows windows of up to
+        max_slots-slot shards (and undecided lists of up to undecided_cap entries)."""
+        N.check(self.lib.rg_comm_reserve(self.ctx, int(max_windows), int(max_slots), int(undecided_cap)), self.ctx)
+
     def comm_allgather_async(self, send_ptr, recv_ptr, nbytes, stream=0):
         N.check(self.lib.rg_comm_allgather_async(self.ctx, send_ptr, recv_ptr, nbytes, stream or None), self.ctx)
 
@@ -356,6 +367,17 @@ class PhaseEvaluator:
                                                          slot_base, window_base, window_slots, max_phase, records_ptr,
                                                          records_cap, rows_ptr, results_ptr, bitmaps_all_ptr or None,
                                                          stream or None), self.ctx)
+
+    def shard_exchange_decisions_async(self, n_windows, out_ptr, out_pitch, n_slots, stride, slot_base, window_base,
+                                       window_slots, records_ptr, records_cap, rows_ptr, results_ptr, undecided_cap,
+                                       decisions_all_ptr, with_v1=True, max_phase=0, stream=0):
+        """Stages 2-4 with the compact decided-slot payload: every rank's undecided lists
+        (+ V1 bitmaps) all-gathered into decisions_all_ptr ([world][P] u32, include/rabia_gpu.h)."""
+        N.check(self.lib.rg_shard_exchange_decisions_async(self.ctx, n_windows, out_ptr, out_pitch, n_slots, stride,
+                                                           slot_base, window_base, window_slots, max_phase,
+                                                           records_ptr, records_cap, rows_ptr, results_ptr,
+                                                           undecided_cap, 1 if with_v1 else 0, decisions_all_ptr,
+                                                           stream or None), self.ctx)
 
     def comm_barrier(self):
         N.check(self.lib.rg_comm_barrier(self.ctx), self.ctx)
@@ -397,6 +419,14 @@ class PhaseEvaluator:
                                       bitmap_pitch, stream=0):
         N.check(self.lib.rg_decision_bitmap_windows_async(self.ctx, n_windows, out_ptr, out_pitch, n_slots, stride,
                                                           committed_ptr, v1_ptr, bitmap_pitch, stream or None),
+                self.ctx)
+
+    def decision_lists_windows_async(self, n_windows, out_ptr, out_pitch, n_slots, stride, lists_ptr, cap, v1_ptr=0,
+                                     v1_pitch=0, stream=0):
+        """Undecided-slot lists ([n_windows][1 + cap] u32: count, then ascending offsets)
+        and optional V1 bitmaps of n_windows windows (rg_decision_lists_windows_async)."""
+        N.check(self.lib.rg_decision_lists_windows_async(self.ctx, n_windows, out_ptr, out_pitch, n_slots, stride,
+                                                         lists_ptr, cap, v1_ptr or None, v1_pitch, stream or None),
                 self.ctx)
 
     def ref_draws_async(self, first, count, out_ptr, stream=0):

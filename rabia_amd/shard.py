@@ -83,6 +83,49 @@ def draw_bases(n_draws, rng_base: int):
     return out, acc
 
 
+def window_draw_bases(n_draws, rank: int, rng_base: int):
+    """The fix-up's stream positions for K consecutive windows of one step (the device's
+    fix_first_draw / finish algebra, rg_kernels.h): n_draws[r][w] = shard r's VQ slots in
+    window w (the step rows, rank-major as the all-gather lays them out). Window w of
+    shard `rank` draws from g0[w] = rng_base + every shard's draws of windows < w + the
+    lower shards' draws of window w (ascending slot order over the windows,
+    engine.rs:567-611); after[w] = the engine position after window w."""
+    world, K = len(n_draws), len(n_draws[0]) if n_draws else 0
+    g0, after, pos = [], [], int(rng_base)
+    for w in range(K):
+        col = [int(n_draws[r][w]) for r in range(world)]
+        g0.append(pos + sum(col[:rank]))
+        pos += sum(col)
+        after.append(pos)
+    return g0, after
+
+
+def commit_windows(rows_all, window_base: int, window_slots: int, watermark_in: int, last_committed_in: int):
+    """The commit fold of K consecutive windows (rg_shard_commit_windows_async): rows_all
+    [world][K] final rows (dicts); each window folds like `combine`, the watermark and
+    last_committed chaining from window to window. Returns the K GlobalCommits."""
+    world, K = len(rows_all), len(rows_all[0]) if rows_all else 0
+    out, wm, lc = [], int(watermark_in), int(last_committed_in)
+    for w in range(K):
+        base = window_base + w * window_slots
+        fu = base + window_slots
+        tot = {k: 0 for k in ("n_slots", "n_decided", "n_v1", "n_pending_r1", "n_draws", "flags")}
+        for r in range(world):
+            x = rows_all[r][w]
+            for k in tot:
+                tot[k] = tot[k] | int(x.get(k, 0)) if k == "flags" else tot[k] + int(x[k])
+            lc = max(lc, int(x["last_committed_max"]))
+            if int(x["n_slots"]):
+                fu = min(fu, int(x["first_undecided"]))
+        if tot["n_slots"] != window_slots:
+            tot["flags"] |= 16
+        if base <= wm < fu:
+            wm = fu
+        out.append(GlobalCommit(tot["n_slots"], tot["n_decided"], tot["n_v1"], tot["n_pending_r1"], tot["n_draws"],
+                                lc, fu, wm, tot["flags"]))
+    return out
+
+
 CLUSTER_FIELDS = ["all_decided", "decided_v1", "sum_phases", "max_phases", "sum_coin_phases",
                   "sum_first_decision_phase", "slots", "reserved"]
 
@@ -152,22 +195,44 @@ class RcclComm:
     it) to attach to this rank's evaluator contexts (rg_comm_create, a collective). World
     1 needs no store."""
 
-    def __init__(self, rank: int, world: int, store=None, key: str = "uid"):
-        from .engine import PhaseEvaluator
+    _made = 0  # communicators made by this process (every rank makes them in the same order)
+
+    def __init__(self, rank: int, world: int, store=None, key: str = None, make_uid=None):
+        if make_uid is None:  # rank 0's id maker (rg_comm_unique_id); tests pass their own
+            from .engine import PhaseEvaluator
+            make_uid = PhaseEvaluator.comm_unique_id
         self.rank, self.world = rank, world
         if world == 1:
-            self.uid = PhaseEvaluator.comm_unique_id()
+            self.uid = make_uid()
             return
         store = store if store is not None else rendezvous_store(rank, world)
+        self.key = key if key is not None else self.default_key()
         if rank == 0:
-            self.uid = PhaseEvaluator.comm_unique_id()
-            store.set(key, self.uid)
+            self.uid = bytes(make_uid())
+            store.set(self.key, self.uid)
         else:
-            self.uid = bytes(store.get(key))
+            self.uid = bytes(store.get(self.key))
+            if len(self.uid) != 128:
+                raise RuntimeError(f"rendezvous key {self.key}: {len(self.uid)}-byte value, not a 128-byte RCCL id")
+
+    @classmethod
+    def default_key(cls) -> str:
+        """A key no earlier communicator of the job used: the launcher's agent store outlives
+        worker restarts (TORCHELASTIC_RESTART_COUNT changes on each) and one process may make
+        several communicators (a per-process counter, advanced alike on every rank)."""
+        import os
+        RcclComm._made += 1
+        return f"uid/{os.environ.get('TORCHELASTIC_RESTART_COUNT', '0')}/{RcclComm._made}"
 
     def attach(self, ev):
         ev.comm_create(self.uid, self.rank, self.world)
         return ev
+
+    @staticmethod
+    def reserve(ev, max_windows: int, max_slots: int, undecided_cap: int = 0):
+        """Size the attached context's exchange scratch (rg_comm_reserve, synchronous): the
+        exchange calls themselves never allocate."""
+        ev.comm_reserve(max_windows, max_slots, undecided_cap)
 
 
 class ShardedRefStep:

@@ -16,7 +16,20 @@ def test_header_symbols_exported():
     for s in syms:
         assert hasattr(lib, s), f"librabia_gpu.so does not export {s}"
         assert s in N._SIGS, f"binding lacks a signature for {s}"
-    assert lib.rg_abi_version() == 4
+    assert lib.rg_abi_version() == 5
+
+
+def test_reservation_entry_points_error_path():
+    """The reservation calls (rg_reserve, rg_comm_reserve) and the compact-payload entry
+    points validate their arguments on the host before any device work: a null context is
+    RG_EINVAL with a message, no device touched (no GPU needed)."""
+    lib = N.load()
+    assert lib.rg_reserve(None, 1 << 20, 4) == N.RG_EINVAL
+    assert b"null context" in lib.rg_last_error(None)
+    assert lib.rg_comm_reserve(None, 4, 1 << 20, 16) == N.RG_EINVAL
+    assert lib.rg_decision_lists_windows_async(None, 1, None, 0, 1024, 0, None, 16, None, 0, None) == N.RG_EINVAL
+    assert lib.rg_shard_exchange_decisions_async(None, 1, None, 0, 1024, 0, 1, 1, 1024, 0, None, 0, None, None, 16, 1,
+                                                 None, None) == N.RG_EINVAL
 
 
 def test_plane_stride():

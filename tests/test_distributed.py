@@ -101,9 +101,14 @@ def test_two_rank_gloo_global_commit(oracle):
 
 
 def _ref_worker(rank, world, port, q):
-    """REF mode: every rank holds the SAME engine seed; the shard's draws start at
-    the global exclusive prefix of the shards' VQ counts (shard.draw_bases over an
-    all_gather), so the window consumes ONE StdRng stream in ascending slot order."""
+    """REF mode through the product's sharded protocol (include/rabia_gpu.h "Sharded
+    REF"), the oracle's restatement of each device stage standing in for the GPU: every
+    rank holds the SAME engine seed; per step of K windows each rank evaluates its shard
+    of every window at provisional draws and leaves draw records (or_shard_step), the K
+    rows are all-gathered (rank-major [world][K]), each VQ slot is re-drawn at its global
+    stream position (window_draw_bases: the fix-up's algebra; or_shard_fixup), the final
+    rows are all-gathered and folded window by window (commit_windows). Two steps, so the
+    second starts from the first one's engine position."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
     import sys
@@ -112,35 +117,58 @@ def _ref_worker(rank, world, port, q):
     import oracle_lib as O
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        n, S, base, rng0, seed = 5, 20_000, 1, 777, 42
-        r1, r2, _ = O.trace(0, n, 5, base, S)
-        start, count = shard.shard_range(S, world, rank)
-        sl = slice(start, start + count)
-        # the shard's VQ count does not depend on where its draws start
-        _, probe = O.ref_step(n, 3, 2, seed, 0, base + start, r1[sl], r2[sl], max_phase=S // 2, lc_in=5, wm_in=1)
-        counts = shard.exchange_results(torch.tensor([probe["n_draws"]], dtype=torch.int64)).view(-1).tolist()
-        bases, total = shard.draw_bases(counts, rng0)
-        out, res = O.ref_step(n, 3, 2, seed, bases[rank], base + start, r1[sl], r2[sl], max_phase=S // 2,
-                              lc_in=5, wm_in=1)
-        assert res["rng_next"] == bases[rank] + counts[rank]
-        rows = shard.exchange_results(torch.tensor(shard.result_row(res), dtype=torch.int64))
-        starts = [shard.shard_range(S, world, r)[0] for r in range(world)]
-        cnts = [shard.shard_range(S, world, r)[1] for r in range(world)]
-        g = shard.combine([shard.row_result(rw.tolist()) for rw in rows], starts, cnts, base, 1, 5)
-        width = max(cnts)
-        packed = np.zeros((5, width), np.uint8)
-        for i, k in enumerate(("r1", "r2own", "dec", "committed", "value")):
-            packed[i, :count] = out[k]
-        allp = shard.exchange_bitmap(torch.from_numpy(packed)).numpy()
-        full = {k: np.concatenate([allp[r][i][:cnts[r]] for r in range(world)])
-                for i, k in enumerate(("r1", "r2own", "dec", "committed", "value"))}
-        q.put((rank, g, total, {k: v.tolist() for k, v in full.items()}))
+        n, quorum, lane, seed, K, steps, W = 5, 3, 2, 42, 3, 2, 20_000
+        kinds = (0, 1, 2)
+        rng, wm, lc = 777, 1, 5
+        max_phase = K * steps * W // 2
+        start, count = shard.shard_range(W, world, rank)
+        results, outs_all = [], []
+        for t in range(steps):
+            outs, recs, rows = [], [], []
+            for w in range(K):
+                base = 1 + (t * K + w) * W
+                r1, r2, _ = O.trace(kinds[w % 3], n, 5 + w, base, W)
+                sl = slice(start, start + count)
+                out, rec, row = O.shard_step(n, quorum, lane, base + start, r1[sl], r2[sl], max_phase=max_phase)
+                outs.append(out)
+                recs.append(rec)
+                rows.append(row)
+            g = shard.exchange_results(torch.tensor([shard.result_row(r) for r in rows], dtype=torch.int64))
+            n_draws = [[int(g[r, w, 4]) for w in range(K)] for r in range(world)]
+            g0, after = shard.window_draw_bases(n_draws, rank, rng)
+            fixed = []
+            for w in range(K):
+                base = 1 + (t * K + w) * W
+                row, flags = O.shard_fixup(seed, g0[w], base + start, outs[w], recs[w], rows[w], after[w],
+                                           max_phase=max_phase)
+                assert flags == 0
+                fixed.append(row)
+            gf = shard.exchange_results(torch.tensor([shard.result_row(r) for r in fixed], dtype=torch.int64))
+            rows_all = [[shard.row_result(gf[r, w].tolist()) for w in range(K)] for r in range(world)]
+            res = shard.commit_windows(rows_all, 1 + t * K * W, W, wm, lc)
+            wm, lc, rng = res[-1].commit_watermark, res[-1].last_committed, after[-1]
+            results.extend(res)
+            outs_all.extend(outs)
+        width = max(shard.shard_range(W, world, r)[1] for r in range(world))
+        keys = ("r1", "r2own", "dec", "committed", "value")
+        full = []
+        for out in outs_all:  # every window's fixed outputs, gathered
+            packed = np.zeros((5, width), np.uint8)
+            for i, k in enumerate(keys):
+                packed[i, :count] = out[k]
+            allp = shard.exchange_bitmap(torch.from_numpy(packed)).numpy()
+            full.append({k: np.concatenate([allp[r][i][:shard.shard_range(W, world, r)[1]] for r in range(world)])
+                         .tolist() for i, k in enumerate(keys)})
+        q.put((rank, results, rng, full))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_ref_shards_one_stream_gloo(oracle, world):
+    """gloo world 2 and 3, the product's shard protocol (provisional likely-outcome votes,
+    8-B draw records, re-draw at global positions, K-window commit) == one engine
+    (oracle.ref_step) over every window of both steps: outputs, results, engine position."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -157,18 +185,70 @@ def test_ref_shards_one_stream_gloo(oracle, world):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    n, S = 5, 20_000
-    r1, r2, _ = oracle.trace(0, n, 5, 1, S)
-    exp, eres = oracle.ref_step(n, 3, 2, 42, 777, 1, r1, r2, max_phase=S // 2, lc_in=5, wm_in=1)
-    assert eres["n_draws"] > 0
-    for rank, g, total, full in got:
-        assert total == eres["rng_next"]
-        assert g.n_draws == eres["n_draws"] and g.n_decided == eres["n_decided"] and g.n_v1 == eres["n_v1"]
-        assert g.last_committed == eres["last_committed_max"]
-        assert g.first_undecided == eres["first_undecided"]
-        assert g.commit_watermark == eres["commit_watermark"]
-        for k in exp:
-            np.testing.assert_array_equal(np.array(full[k], np.uint8), exp[k], err_msg=k)
+    n, K, steps, W = 5, 3, 2, 20_000
+    kinds = (0, 1, 2)
+    rng, wm, lc = 777, 1, 5
+    max_phase = K * steps * W // 2
+    exp_res, exp_out = [], []
+    for t in range(steps):
+        for w in range(K):
+            base = 1 + (t * K + w) * W
+            r1, r2, _ = oracle.trace(kinds[w % 3], n, 5 + w, base, W)
+            out, res = oracle.ref_step(n, 3, 2, 42, rng, base, r1, r2, max_phase=max_phase, lc_in=lc, wm_in=wm)
+            rng, wm, lc = res["rng_next"], res["commit_watermark"], res["last_committed_max"]
+            exp_res.append(res)
+            exp_out.append(out)
+    assert sum(r["n_draws"] for r in exp_res) > 0
+    for rank, results, rng_end, full in got:
+        assert rng_end == rng
+        for w, (g, e) in enumerate(zip(results, exp_res)):
+            assert g.n_draws == e["n_draws"] and g.n_decided == e["n_decided"] and g.n_v1 == e["n_v1"], w
+            assert g.n_pending_r1 == e["n_pending_r1"] and g.flags == 0
+            assert g.last_committed == e["last_committed_max"], w
+            assert g.first_undecided == e["first_undecided"], w
+            assert g.commit_watermark == e["commit_watermark"], w
+        for w, (f, e) in enumerate(zip(full, exp_out)):
+            for k in e:
+                np.testing.assert_array_equal(np.array(f[k], np.uint8), e[k], err_msg=f"rank {rank} window {w} {k}")
+
+
+def _rendezvous_worker(rank, world, port, q):
+    """Two RcclComm rendezvous through shard.rendezvous_store (the TCP store rank 0 serves
+    at MASTER_ADDR:MASTER_PORT): rank 0 makes the 128-byte ids, every rank reads them."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TORCHELASTIC_RESTART_COUNT="3")
+    import hashlib
+    store = shard.rendezvous_store(rank, world, timeout_s=60)
+    ids = []
+    for i in range(2):  # two communicators of one job: distinct keys, distinct ids
+        uid = lambda i=i: hashlib.sha512(b"rg-%d" % i).digest() * 2  # noqa: E731  (128 bytes)
+        c = shard.RcclComm(rank, world, store=store, make_uid=uid)
+        ids.append((c.key, c.uid))
+    store.add("read", 1)  # rank 0 serves the store: it stays until every rank has read
+    while int(store.add("read", 0)) < world:
+        import time
+        time.sleep(0.05)
+    q.put((rank, ids))
+
+
+def test_rendezvous_store_carries_128_byte_id():
+    """The RCCL id's host channel on CPU: world 2, rank 0 serves the store and publishes
+    two 128-byte ids; both ranks end with the same ids under restart-scoped, per-communicator
+    keys (a restarted job or a second communicator never reads a stale id)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rendezvous_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[0] == got[1]
+    (k0, u0), (k1, u1) = got[0]
+    assert len(u0) == len(u1) == 128 and u0 != u1
+    assert k0 != k1 and k0.startswith("uid/3/") and k1.startswith("uid/3/")
 
 
 def _cluster_stats(info):

@@ -204,3 +204,63 @@ def test_soa_cpu_path_equals_oracle(oracle, n, S):
         for k in exp:
             np.testing.assert_array_equal(got[k], exp[k], err_msg=k)
         assert res == eres
+
+
+@pytest.mark.parametrize("n,world,K,W,kind", [(5, 1, 2, 3000, 1), (3, 4, 3, 1001, 0), (9, 3, 2, 2048, 2),
+                                              (7, 5, 1, 777, 0)])
+def test_shard_protocol_equals_one_engine(oracle, n, world, K, W, kind):
+    """The sharded pipeline's algebra on the oracle alone (or_shard_step -> rows ->
+    window_draw_bases -> or_shard_fixup -> commit_windows) over `world` shards of K
+    consecutive windows == or_ref_step over the windows in order: every output, every
+    window's result, the engine position. Shards are ragged (world does not divide W)."""
+    import sys, os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from rabia_amd import shard
+    q, lane, seed, rng0, wm0, lc0 = n // 2 + 1, n // 2, 42, 1000, 1, 3
+    max_phase = K * W * 2 // 3
+    traces = [oracle.trace(kind, n, 11 + w, 1 + w * W, W) for w in range(K)]
+    parts = [shard.shard_range(W, world, r, align=32) for r in range(world)]
+    outs = [[None] * K for _ in range(world)]
+    recs = [[None] * K for _ in range(world)]
+    rows = [[None] * K for _ in range(world)]
+    for r, (start, cnt) in enumerate(parts):
+        for w in range(K):
+            r1, r2, _ = traces[w]
+            sl = slice(start, start + cnt)
+            outs[r][w], recs[r][w], rows[r][w] = oracle.shard_step(n, q, lane, 1 + w * W + start, r1[sl], r2[sl],
+                                                                   max_phase=max_phase)
+            assert rows[r][w]["n_draws"] == len(recs[r][w])
+    n_draws = [[rows[r][w]["n_draws"] for w in range(K)] for r in range(world)]
+    fixed = [[None] * K for _ in range(world)]
+    for r, (start, cnt) in enumerate(parts):
+        g0, after = shard.window_draw_bases(n_draws, r, rng0)
+        for w in range(K):
+            fixed[r][w], flags = oracle.shard_fixup(seed, g0[w], 1 + w * W + start, outs[r][w], recs[r][w],
+                                                    rows[r][w], after[w], max_phase=max_phase)
+            assert flags == 0
+    res = shard.commit_windows(fixed, 1, W, wm0, lc0)
+    rng, wm, lc = rng0, wm0, lc0
+    for w in range(K):
+        r1, r2, _ = traces[w]
+        exp, e = oracle.ref_step(n, q, lane, seed, rng, 1 + w * W, r1, r2, max_phase=max_phase, lc_in=lc, wm_in=wm)
+        rng, wm, lc = e["rng_next"], e["commit_watermark"], e["last_committed_max"]
+        g = res[w]
+        assert (g.n_slots, g.n_decided, g.n_v1, g.n_pending_r1, g.n_draws) == \
+            (e["n_slots"], e["n_decided"], e["n_v1"], e["n_pending_r1"], e["n_draws"]), w
+        assert (g.last_committed, g.first_undecided, g.commit_watermark, g.flags) == \
+            (e["last_committed_max"], e["first_undecided"], e["commit_watermark"], 0), w
+        assert fixed[world - 1][w]["rng_next"] == e["rng_next"]
+        for k in exp:
+            got = np.concatenate([outs[r][w][k] for r in range(world)])
+            np.testing.assert_array_equal(got, exp[k], err_msg=f"window {w} {k}")
+
+
+def test_shard_fixup_flags_record_overflow(oracle):
+    """Records past the capacity are not written: the fix-up flags it (8) and leaves those
+    slots provisional, as the device does (include/rabia_gpu.h, flags value 8)."""
+    n, W = 5, 4000
+    r1, r2, _ = oracle.trace(0, n, 3, 1, W)
+    out, rec, row = oracle.shard_step(n, 3, 2, 1, r1, r2, records_cap=10)
+    assert row["n_draws"] > 10 and len(rec) == 10
+    fixed, flags = oracle.shard_fixup(42, 0, 1, out, rec, row, row["n_draws"], records_cap=10)
+    assert flags == 8

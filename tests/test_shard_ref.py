@@ -530,6 +530,10 @@ def test_rccl_exchange_world1_equals_one_evaluator(n, K, S, kind):
         ev.set_state(**state)
         ev.phase_step_shard_windows_async(K, votes.data_ptr(), Sp // 32, out.data_ptr(), Sp // 32, S, stride, 1, S,
                                           rec.data_ptr(), S, rows.data_ptr(), max_phase=mp)
+        with pytest.raises(N.RabiaGpuError, match="rg_comm_reserve"):  # no payload reserved: nothing enqueued
+            ev.shard_exchange_windows_async(K, out.data_ptr(), Sp // 32, S, stride, 1, 1, S, rec.data_ptr(), S,
+                                            rows.data_ptr(), res.data_ptr(), bm_all.data_ptr(), max_phase=mp)
+        ev.comm_reserve(K, S)
         ev.shard_exchange_windows_async(K, out.data_ptr(), Sp // 32, S, stride, 1, 1, S, rec.data_ptr(), S,
                                         rows.data_ptr(), res.data_ptr(), bm_all.data_ptr(), max_phase=mp)
         ev.sync()
@@ -570,3 +574,176 @@ def test_rccl_exchange_world1_equals_one_evaluator(n, K, S, kind):
     assert {k: g[k] for k in RES_CMP} == {k: res_1[0][k] for k in RES_CMP}
     assert torch.equal(out_d[: Sp // 32], out_1[: Sp // 32])
 
+
+
+def _committed_from_lists(lists, K, cap, nw, S):
+    """Committed bitmaps rebuilt from undecided lists: every valid slot set, listed slots
+    cleared (the consumer side of rg_shard_exchange_decisions_async)."""
+    bits = np.ones((K, nw * 32), np.uint8)
+    bits[:, S:] = 0
+    for w in range(K):
+        cnt = int(lists[w, 0])
+        assert cnt <= cap
+        offs = lists[w, 1:1 + cnt].astype(np.int64)
+        assert np.all(np.diff(offs) > 0) and (cnt == 0 or offs[-1] < S)  # ascending, inside the shard
+        bits[w, offs] = 0
+    return np.packbits(bits, axis=1, bitorder="little").view(np.uint32)
+
+
+@pytest.mark.parametrize("n,K,S,kind", [(5, 3, 300_032, 1), (9, 4, 1 << 20, 2), (7, 2, 65_601, 0)])
+def test_rccl_exchange_decisions_world1(n, K, S, kind):
+    """rg_shard_exchange_decisions_async at world 1: the rows, results and engine state
+    equal one evaluator's; the gathered undecided lists hold exactly the slots whose
+    committed bit is clear (ascending, count = n_slots - n_decided of the final row), so
+    the committed bitmap rebuilt from them equals rg_decision_bitmap_windows_async's; the
+    V1 bitmaps equal its V1 bitmaps (bits past n_slots cleared). A list capacity below a
+    window's undecided count flags the window (32) and keeps the first `cap` offsets."""
+    torch = torch_cuda()
+    votes, stride, total = make_votes(n, [S] * K, kind, seed=43)
+    Sp = ((S + 127) // 128) * 128
+    nw = (S + 31) // 32
+    i64 = dict(dtype=torch.int64, device="cuda")
+    state = {"rng_next": 7, "last_committed": 0, "commit_watermark": 1, "steps": 0}
+    bm = torch.zeros((K, 2, nw), dtype=torch.int32, device="cuda")
+    runs = {}
+    for cap, with_v1 in ((S, True), (S // 3, False), (3, True)):
+        out = torch.zeros(8 * stride, dtype=torch.int32, device="cuda")
+        rows = torch.zeros((K, 10), **i64)
+        res = torch.zeros((K, 10), **i64)
+        rec = torch.zeros(K * S, **i64)
+        P = K * (1 + cap) + (K * nw if with_v1 else 0)
+        dec = torch.full((P,), -1, dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        with PhaseEvaluator(n, self_lane=n // 2, seed=42) as ev:
+            shard.RcclComm(0, 1).attach(ev)
+            ev.comm_reserve(K, S, cap)
+            ev.set_state(**state)
+            ev.phase_step_shard_windows_async(K, votes.data_ptr(), Sp // 32, out.data_ptr(), Sp // 32, S, stride, 1,
+                                              S, rec.data_ptr(), S, rows.data_ptr())
+            ev.shard_exchange_decisions_async(K, out.data_ptr(), Sp // 32, S, stride, 1, 1, S, rec.data_ptr(), S,
+                                              rows.data_ptr(), res.data_ptr(), cap, dec.data_ptr(), with_v1=with_v1)
+            ev.sync()
+            st = ev.get_state()
+            if not runs:
+                ev.decision_bitmap_windows_async(K, out.data_ptr(), Sp // 32, S, stride, bm[0, 0].data_ptr(),
+                                                 bm[0, 1].data_ptr(), 2 * nw)
+                ev.sync()
+        runs[(cap, with_v1)] = (out, rows_of(res), st, dec.cpu().numpy().view(np.uint32))
+    out_1 = torch.zeros(8 * stride, dtype=torch.int32, device="cuda")
+    res_1, st_1 = run_single(n, [S] * K, votes, out_1, stride, self_lane=n // 2, state=state)
+    b = bm.cpu().numpy().view(np.uint32)
+    tail = np.uint32((1 << (S % 32)) - 1) if S % 32 else np.uint32(0xFFFFFFFF)
+    full = None
+    for (cap, with_v1), (out, got, st, dec) in runs.items():
+        assert torch.equal(out, out_1) and st == st_1
+        lists = dec[:K * (1 + cap)].reshape(K, 1 + cap)
+        for w in range(K):
+            und = res_1[w]["n_slots"] - res_1[w]["n_decided"]
+            assert int(lists[w, 0]) == und, (cap, w)
+            exp_flags = 32 if und > cap else 0
+            assert got[w]["flags"] == exp_flags, (cap, w)
+            assert {k: got[w][k] for k in RES_CMP if k != "flags"} == {k: res_1[w][k] for k in RES_CMP if k != "flags"}
+        if cap == S:  # complete lists: the committed bitmap rebuilt equals the step's
+            committed = _committed_from_lists(lists, K, cap, nw, S)
+            exp = b[:, 0].copy()
+            exp[:, -1] &= tail
+            np.testing.assert_array_equal(committed, exp)
+            full = lists
+        else:  # truncated: the first min(count, cap) offsets of the complete list
+            for w in range(K):
+                m = min(int(lists[w, 0]), cap)
+                np.testing.assert_array_equal(lists[w, 1:1 + m], full[w, 1:1 + m])
+        if with_v1:
+            v1 = dec[K * (1 + cap):].reshape(K, nw)
+            exp = b[:, 1].copy()
+            exp[:, -1] &= tail
+            np.testing.assert_array_equal(v1, exp)
+        else:
+            assert dec.size == K * (1 + cap)
+
+
+def test_async_calls_refuse_past_reservation():
+    """The _async entry points never allocate or synchronise: past the context's
+    reservation (rg_reserve; rg_create's default is 128 windows per call) they return
+    RG_EINVAL and enqueue nothing; after rg_reserve the same calls run and equal one
+    evaluator."""
+    torch = torch_cuda()
+    n, K, S = 5, 130, 1024
+    votes, stride, total = make_votes(n, [S] * K, 1, seed=5)
+    i64 = dict(dtype=torch.int64, device="cuda")
+    out = torch.zeros(8 * stride, dtype=torch.int32, device="cuda")
+    rows = torch.zeros((K, 10), **i64)
+    fixed = torch.zeros((K, 10), **i64)
+    res = torch.zeros((K, 10), **i64)
+    rec = torch.zeros(K * S, **i64)
+    lists = torch.zeros(K * (1 + S), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    with PhaseEvaluator(n, self_lane=2, seed=42) as ev:
+        step = lambda: ev.phase_step_shard_windows_async(K, votes.data_ptr(), S // 32, out.data_ptr(), S // 32, S,  # noqa
+                                                         stride, 1, S, rec.data_ptr(), S, rows.data_ptr())
+        fix = lambda: ev.shard_fixup_windows_async(K, out.data_ptr(), S // 32, S, stride, 1, S, rec.data_ptr(), S,  # noqa
+                                                   rows.data_ptr(), 0, 1, fixed.data_ptr())
+        lst = lambda: ev.decision_lists_windows_async(K, out.data_ptr(), S // 32, S, stride, lists.data_ptr(), S)  # noqa
+        for call in (step, fix, lst):
+            with pytest.raises(N.RabiaGpuError, match="rg_reserve") as e:
+                call()
+            assert e.value.code == N.RG_EINVAL
+        ev.reserve(K * S, K)
+        step()
+        fix()
+        ev.shard_commit_windows_async(K, fixed.data_ptr(), 1, 1, S, res.data_ptr())
+        lst()
+        ev.sync()
+        st = ev.get_state()
+    out_1 = torch.zeros(8 * stride, dtype=torch.int32, device="cuda")
+    res_1, st_1 = run_single(n, [S] * K, votes, out_1, stride, self_lane=2)
+    assert torch.equal(out, out_1) and st == st_1
+    got = rows_of(res)
+    for w in range(K):
+        assert {k: got[w][k] for k in RES_CMP} == {k: res_1[w][k] for k in RES_CMP}, w
+    ls = lists.cpu().numpy().view(np.uint32).reshape(K, 1 + S)
+    assert [int(x) for x in ls[:, 0]] == [r["n_slots"] - r["n_decided"] for r in res_1]
+
+
+@pytest.mark.parametrize("n,K,S,kind,force_lag", [(5, 3, 300_032, 1, True), (9, 2, 262_144, 0, True),
+                                                   (7, 1, 100_000, 2, False), (3, 2, 65_536, 1, False)])
+def test_shard_step_records_equal_oracle(oracle, n, K, S, kind, force_lag):
+    """Stage 1 itself against the oracle's restatement (or_shard_step): the device's draw
+    records (slot offset, c1-vs-c0 class, the decision under each own vote, the
+    provisional vote) and its row of the non-VQ slots, bit for bit. The lag kernel's
+    provisional vote is the likelier outcome, as the oracle's; the tiled kernel draws at
+    the provisional position instead (bit 6 then differs: the fix-up re-draws either)."""
+    torch = torch_cuda()
+    votes, stride, total = make_votes(n, [S] * K, kind, seed=61)
+    Sp = ((S + 127) // 128) * 128
+    i64 = dict(dtype=torch.int64, device="cuda")
+    out = torch.zeros(8 * stride, dtype=torch.int32, device="cuda")
+    rows = torch.zeros((K, 10), **i64)
+    rec = torch.zeros(K * S, **i64)
+    mp = K * S // 2
+    torch.cuda.synchronize()
+    with PhaseEvaluator(n, self_lane=n // 2, seed=42) as ev:
+        if force_lag:
+            ev.debug_set(0x200000)
+        ev.phase_step_shard_windows_async(K, votes.data_ptr(), Sp // 32, out.data_ptr(), Sp // 32, S, stride, 1, S,
+                                          rec.data_ptr(), S, rows.data_ptr(), max_phase=mp)
+        ev.sync()
+        la = ev.last_launch()
+    assert la["kernel"] == ("lag" if force_lag else "tiled"), la
+    got_rows = rows_of(rows)
+    recs = rec.cpu().numpy().view(np.uint64).reshape(K, S)
+    planes = out.view(8, stride).cpu().numpy().view(np.uint32)
+    for w in range(K):
+        base = 1 + w * S
+        r1, r2, _ = oracle.trace(kind, n, 61, base, S)
+        exp, erec, erow = oracle.shard_step(n, n // 2 + 1, n // 2, base, r1, r2, max_phase=mp)
+        for k in ("n_slots", "n_decided", "n_v1", "n_pending_r1", "n_draws", "last_committed_max", "first_undecided"):
+            assert got_rows[w][k] == erow[k], (w, k)
+        g = recs[w, :erow["n_draws"]]
+        mask = np.uint64(0xFFFFFFFFFFFFFFFF if force_lag else ~(1 << 38) & 0xFFFFFFFFFFFFFFFF)
+        np.testing.assert_array_equal(g & mask, erec.astype(np.uint64) & mask, err_msg=f"window {w} records")
+        if force_lag:  # the provisional outputs too
+            w0 = (w * Sp) // 32
+            dec = decode_outputs(planes[:, w0:w0 + (S + 31) // 32], S)
+            for k in exp:
+                np.testing.assert_array_equal(dec[k], exp[k], err_msg=f"window {w} {k}")
