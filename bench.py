@@ -53,6 +53,18 @@ def bytes_per_slot_ref(n: int) -> float:
     return (4 * n + 8) / 8.0
 
 
+C3_COIN_TABLE_PHASES = 8  # rabia_gpu.hip cluster_run: kCoinTablePhases (RG_COIN_TABLE_PHASES)
+
+
+def c3_bytes_per_slot(n: int, mean_phases: float) -> float:
+    """Bytes per slot of the call the C3 step makes, rg_wmvc_cluster_bitmaps_async (the
+    decided / V1 bitmaps built inside the cluster kernel, no second pass over the info
+    words): n initial-state bits read, the u32 info word written, 2 bitmap bits written,
+    the coin table's bits written (one per slot per table phase) and read (about one per
+    phase the slot runs)."""
+    return n / 8 + 4 + 2 / 8 + C3_COIN_TABLE_PHASES / 8 + mean_phases / 8
+
+
 def c3_roofline(r, bytes_slot):
     """C3 is VALU-issue bound (per phase 2n keyed scheduler picks per slot + the coin),
     not HBM bound. achieved = VALU wave-instructions per launch (per-slot count from the
@@ -106,10 +118,12 @@ def parse():
     ap.add_argument("--c5-batch", type=int, default=32,
                     help="C5: consecutive C5 windows per step: one shard-step launch of K windows per rank (the "
                          "multi-window lag kernel from 2^28 slots per launch at n = 9), one K-window launch at N = 1")
-    ap.add_argument("--c5-payload", choices=["lists", "lists-nov1", "bitmaps"], default="lists",
-                    help="C5 decided-slot payload per step: every rank's undecided-slot lists + V1 bitmaps (default), "
-                         "the lists alone (callers that apply only their own shard), or the round-5 committed + V1 "
-                         "bitmaps")
+    ap.add_argument("--c5-payload", choices=["lists", "lists-v1", "bitmaps"], default="lists",
+                    help="C5 decided-slot payload per step: every rank's undecided-slot lists (the decided-slot "
+                         "bitmaps' complement, ~0.04 %% of the slots at agree90; default: the state machine is sharded "
+                         "with the slots, so a rank applies its own shard's V1 batches and needs only the global "
+                         "decided set and watermark), the lists + every rank's V1 bitmap (every rank applies every "
+                         "batch), or the round-5 committed + V1 bitmaps")
     ap.add_argument("--sharded", "--c5-sharded", dest="sharded", action="store_true",
                     help="N = 1: run the multi-GPU pipeline (shard step + fix-up + commit, exchanges with one "
                          "rank) instead of the single evaluator: the per-GPU cost of the N > 1 path")
@@ -118,6 +132,8 @@ def parse():
                          "0.80 vs 0.81, 0.84 vs 0.86, 0.86 vs 0.88 ms per one-shard step in three round-4 "
                          "runs, profiles/r04_c2_sharded_n1*.json) or on the compute stream right behind step "
                          "t + 1's launch")
+    ap.add_argument("--comp-priority", type=int, default=0, choices=[0, 1],
+                    help="N > 1 / --sharded: the step kernels' stream at high priority (1) or default (0)")
     ap.add_argument("--fixup-eager", action="store_true",
                     help="N > 1 / --sharded: enqueue step t's exchange right after step t's launch (default: after "
                          "step t + 1's launch)")
@@ -449,7 +465,9 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, comm, bitmaps):
     gather = (None if comm is not None else
               make_gather(dist, a.backend) if world > 1 else (lambda out, inp: out.copy_(inp.unsqueeze(0))))
     stride, in_words, out_words = layout(n, S, T)
-    comp = torch.cuda.Stream()
+    # the step kernels' stream at high priority: when a step kernel ends, the exchange
+    # kernels it releases and the next step kernel race for the freed CUs
+    comp = torch.cuda.Stream(priority=-1) if a.comp_priority else torch.cuda.Stream()
     fix = torch.cuda.Stream()
     torch.cuda.set_stream(comp)
     # one seed on every rank; the context on this rank's GPU (main: torch.cuda.set_device(LOCAL_RANK))
@@ -480,7 +498,7 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, comm, bitmaps):
     # C5 payload: undecided lists (cap per window; count > cap flags the window, 32) + V1 bitmaps
     lists = bitmaps and a.c5_payload != "bitmaps"
     und_cap = max(S // 512, 1024)  # agree90: ~0.04 % of a shard's slots are undecided
-    P = K * (1 + und_cap) + (K * nw if a.c5_payload == "lists" else 0)
+    P = K * (1 + und_cap) + (K * nw if a.c5_payload == "lists-v1" else 0)
     if comm is not None:  # the exchange scratch (rows; C5: the decided-slot payload) sized before the pipeline
         comm.reserve(ev, K, S if bitmaps else 1, und_cap)
     if bitmaps and not lists:
@@ -520,12 +538,16 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, comm, bitmaps):
     # costs the stream 6-10 us (an event record 7, a one-thread kernel 6, a wait 5-6:
     # tools/gap_probe.py, profiles/r05/gap_probe.json); back-to-back step kernels cost 0.
 
+    host_wait = [0.0]  # host time blocked on e_done (the rest of the loop is enqueue work)
+
     def step(t, evs=None, chain=True):
         votes, out, rec = sets[t % a.sets]
         base = 1 + t * K * window_slots
         if t >= a.sets:  # the output buffers and records of step t - sets must be fixed up first
             if comm is not None:
+                w0 = time.perf_counter()
                 e_done[t - a.sets].synchronize()
+                host_wait[0] += time.perf_counter() - w0
             else:
                 comp.wait_event(e_done[t - a.sets])
         if evs is not None:
@@ -566,7 +588,7 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, comm, bitmaps):
                 ev.shard_exchange_decisions_async(K, out.data_ptr(), out_words, S, stride, base + start, base,
                                                   window_slots, rec.data_ptr(), cap, rows[t].data_ptr(),
                                                   result[t].data_ptr(), und_cap, dec_all[t].data_ptr(),
-                                                  with_v1=a.c5_payload == "lists", stream=fs_stream.cuda_stream)
+                                                  with_v1=a.c5_payload == "lists-v1", stream=fs_stream.cuda_stream)
             else:
                 ev.shard_exchange_windows_async(K, out.data_ptr(), out_words, S, stride, base + start, base,
                                                 window_slots, rec.data_ptr(), cap, rows[t].data_ptr(),
@@ -607,12 +629,15 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, comm, bitmaps):
     evs = launch_events(a, every=4)  # the step kernel alone, sampled: the step time holds the exchange too
     t_begin, t_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t_begin.record(comp)
+    host_wait[0] = 0.0
+    h0 = time.perf_counter()
     for k in range(a.steps):  # (the warm-up's last fix-up is done: the timed chain starts afresh)
         step(a.warmup + k, evs[k] if evs else None, chain=k > 0)
     if defer:
         later(n_total - 1, fs_main)
     comp.wait_event(e_done[n_total - 1])
     t_end.record(comp)
+    host_ms = (time.perf_counter() - h0) * 1000.0  # the host's enqueue time (it may block on e_done waits)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -648,7 +673,8 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, comm, bitmaps):
                    "undecided_cap": und_cap if lists else None}
     return {"total_ms": total_ms, "kern_ms": kern_ms, "decided": decided, "sweep_us": None, "ev": ev,
             "stream": comp, "windows_per_launch": K, "launch": ev.last_launch(), "sharded": True,
-            "payload": payload}
+            "payload": payload, "host_ms_per_step": host_ms / a.steps,
+            "host_enqueue_ms_per_step": (host_ms - host_wait[0] * 1000.0) / a.steps}
 
 
 # ---------------------------------------------------------------------------
@@ -806,11 +832,9 @@ def main():
     if a.config == "c3":
         r = run_c3(a, world, rank, dist, comm)
         if rank == 0:
-            # bytes the cluster kernels move per slot: 5 initial-state bits read, the u32 info word
-            # written, the u32 read + 2 bitmap bits written by the bitmap kernel, the coin table
-            # (16 phases x 1 bit written, ~mean phases bits read); the kernel is VALU-bound
+            # bytes the cluster call moves per slot (c3_bytes_per_slot); the kernel is VALU-bound
             # (per phase: 2n keyed scheduler hashes per slot), so this is not a roofline claim
-            bytes_slot = 5 / 8 + 4 + 4 + 2 / 8 + 16 / 8 + r["mean_phases"] / 8
+            bytes_slot = c3_bytes_per_slot(5, r["mean_phases"])
             line = {
                 "metric": "consensus slots decided/sec (5 replicas, 2^24 slots, adversarial split, "
                           "Weak-MVC to termination)",
@@ -863,10 +887,12 @@ def main():
              ", one engine: each rank's 2^30-slot shard at provisional draws, shard rows all-gathered, VQ slots "
              "re-drawn at their global positions, final rows all-gathered and folded") if sharded else "")
         if a.config == "c5":
-            metric = "consensus slots decided/sec (9 replicas, 2^26 slots per step, bitmap all-gather)"
+            metric = "consensus slots decided/sec (9 replicas, 2^26 slots per step, decided-slot all-gather)"
+            carried = {"lists": "undecided-slot lists", "lists-v1": "undecided-slot lists + V1 bitmaps",
+                       "bitmaps": "committed + V1 bitmaps"}[a.c5_payload]
             workload = (f"C5: {n} replicas x {window_slots}-slot windows, {K} per step (one engine), REF sweep "
-                        f"split over {world} GPU(s)" + (", committed + V1 bitmaps and shard rows all-gathered per "
-                                                        "window" if sharded else ""))
+                        f"split over {world} GPU(s)" + (f", shard rows and {carried} all-gathered every step"
+                                                        if sharded else ""))
             scaling = "strong"
         else:
             metric = "consensus slots decided/sec (5 replicas, 1M slots) + HBM GB/s as % of peak"
@@ -900,6 +926,9 @@ def main():
         }
         if r.get("payload"):
             line["config"]["payload"] = r["payload"]
+        if r.get("host_ms_per_step") is not None:  # the pipeline's host time per step (rank 0): all,
+            line["host_ms_per_step"] = r["host_ms_per_step"]  # and without the waits for buffer reuse
+            line["host_enqueue_ms_per_step"] = r["host_enqueue_ms_per_step"]
         print(json.dumps(line), file=out, flush=True)
     r["ev"].close()
     if dist is not None:

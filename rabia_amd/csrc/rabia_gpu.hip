@@ -650,7 +650,8 @@ int rg_phase_step_shard_windows_async(rg_ctx* ctx, uint32_t n_windows, const uin
 static int fixup_impl(rg_ctx* ctx, uint32_t n_win, uint32_t* out_dev, uint64_t out_pitch, uint64_t n_slots,
                       uint64_t stride_words, uint64_t slot_base, uint64_t id_stride, uint64_t max_phase,
                       const uint64_t* records_dev, uint64_t records_cap, const rg_step_result* rows_dev,
-                      uint32_t shard, uint32_t n_shards, rg_step_result* rows_out_dev, void* stream) {
+                      uint32_t shard, uint32_t n_shards, rg_step_result* rows_out_dev, void* stream,
+                      hipEvent_t patched = nullptr) {
   if (!ctx) return fail(nullptr, RG_EINVAL, "rg_shard_fixup: null context");
   if (ctx->cfg.mode != RG_MODE_REF) return fail(ctx, RG_EINVAL, "rg_shard_fixup: REF mode only");
   if (!out_dev || !records_dev || !rows_dev || n_shards == 0 || shard >= n_shards || n_slots == 0 || n_win == 0 ||
@@ -669,7 +670,12 @@ static int fixup_impl(rg_ctx* ctx, uint32_t n_win, uint32_t* out_dev, uint64_t o
   // at most kFixGrid workgroups (the record count lives on the device)
   const uint64_t rec_most = records_cap < n_slots ? records_cap : n_slots;
   const uint64_t blk_most = rec_most / 8 + 2;
-  const uint32_t n_part = (uint32_t)std::min<uint64_t>((blk_most + 255) / 256, kFixGrid);
+  // at most kFixGrid workgroups over ALL windows (>= 16 per window): the fix-up is launched
+  // the moment a step kernel ends, and a grid of n_win x 513 mostly empty workgroups (the
+  // record capacity, not the record count, sized it) took the CUs the next step kernel's
+  // workgroups were waiting for (20-30 us between step kernels at 32 windows)
+  const uint64_t per_win = std::max<uint64_t>(kFixGrid / n_win, 16);
+  const uint32_t n_part = (uint32_t)std::min<uint64_t>((blk_most + 255) / 256, per_win);
   if (4ull * n_part * n_win > ctx->fix_acc_cap || n_win > ctx->res_windows)
     return beyond_reservation(ctx, "rg_shard_fixup");
   hipStream_t s = pick_stream(ctx, stream);
@@ -691,6 +697,8 @@ static int fixup_impl(rg_ctx* ctx, uint32_t n_win, uint32_t* out_dev, uint64_t o
   f.out_pitch = out_pitch;
   f.id_stride = id_stride;
   hipLaunchKernelGGL(shard_fixup_kernel, dim3(n_part, n_win), dim3(256), 0, s, f);
+  // (the exchange forks the decision lists off here: the outputs are final, the rows not yet)
+  if (patched) RG_HIP(ctx, hipEventRecord(patched, s));
   hipLaunchKernelGGL(shard_fixup_finish_kernel, dim3(n_win), dim3(256), 0, s, f, ctx->stage_result + 0,
                      reinterpret_cast<DevResult*>(rows_out_dev), ctx->fix_arrivals);
   RG_HIP(ctx, hipGetLastError());
@@ -703,6 +711,15 @@ int rg_shard_fixup_async(rg_ctx* ctx, uint32_t* out_dev, uint64_t n_slots, uint6
                          uint32_t n_shards, rg_step_result* row_dev, void* stream) {
   return fixup_impl(ctx, 1, out_dev, 0, n_slots, stride_words, slot_base, n_slots, max_phase, records_dev, records_cap,
                     rows_dev, shard, n_shards, row_dev, stream);
+}
+
+int rg_shard_fixup_fork(rg_ctx* ctx, uint32_t n_windows, uint32_t* out_dev, uint64_t out_pitch_words, uint64_t n_slots,
+                        uint64_t stride_words, uint64_t slot_base, uint64_t window_stride, uint64_t max_phase,
+                        const uint64_t* records_dev, uint64_t records_cap, const rg_step_result* rows_dev,
+                        uint32_t shard, uint32_t n_shards, rg_step_result* rows_out_dev, void* stream,
+                        hipEvent_t patched) {
+  return fixup_impl(ctx, n_windows, out_dev, out_pitch_words, n_slots, stride_words, slot_base, window_stride,
+                    max_phase, records_dev, records_cap, rows_dev, shard, n_shards, rows_out_dev, stream, patched);
 }
 
 int rg_shard_fixup_windows_async(rg_ctx* ctx, uint32_t n_windows, uint32_t* out_dev, uint64_t out_pitch_words,

@@ -89,6 +89,12 @@ struct RgComm {
   uint32_t* payload = nullptr;     // this rank's decision payload (bitmaps, or lists + V1 bitmaps)
   uint64_t payload_cap = 0;        // words
   double* scalars = nullptr;       // rg_comm_barrier / rg_comm_max_f64 (device, 64 doubles)
+  // rg_shard_exchange_decisions_async forks the decision lists onto `aux` once the fix-up's
+  // re-draw has patched the outputs, so they run beside the finish, the final-row gather and
+  // the commit (each of those a short latency-bound kernel or collective), and joins them
+  // before the payload gather
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_patched = nullptr, ev_lists = nullptr;
 };
 
 constexpr uint32_t kCommScalars = 64;
@@ -104,6 +110,9 @@ void rg_comm_release(rg_ctx* ctx) {
   (void)hipFree(c->fixed_all);
   (void)hipFree(c->payload);
   (void)hipFree(c->scalars);
+  if (c->ev_patched) (void)hipEventDestroy(c->ev_patched);
+  if (c->ev_lists) (void)hipEventDestroy(c->ev_lists);
+  if (c->aux) (void)hipStreamDestroy(c->aux);
   delete c;
   ctx->comm = nullptr;
 }
@@ -173,15 +182,14 @@ int gather(rg_ctx* ctx, const void* send, void* recv, uint64_t bytes, hipStream_
 int exchange_rows(rg_ctx* ctx, uint32_t n_windows, uint32_t* out_dev, uint64_t out_pitch_words, uint64_t n_slots,
                   uint64_t stride_words, uint64_t slot_base, uint64_t window_base, uint64_t window_slots,
                   uint64_t max_phase, const uint64_t* records_dev, uint64_t records_cap, const rg_step_result* rows_dev,
-                  rg_step_result* results_dev, uint64_t und_chk, hipStream_t s) {
+                  rg_step_result* results_dev, uint64_t und_chk, hipStream_t s, hipEvent_t patched = nullptr) {
   RgComm* c = ctx->comm;
   const uint64_t row_bytes = (uint64_t)n_windows * sizeof(DevResult);
   if (int rc = gather(ctx, rows_dev, c->rows_all, row_bytes, s, "ncclAllGather(rows)")) return rc;
-  if (int rc = rg_shard_fixup_windows_async(ctx, n_windows, out_dev, out_pitch_words, n_slots, stride_words, slot_base,
-                                            window_slots, max_phase, records_dev, records_cap,
-                                            reinterpret_cast<const rg_step_result*>(c->rows_all),
-                                            (uint32_t)c->rank, (uint32_t)c->world,
-                                            reinterpret_cast<rg_step_result*>(c->fixed), s))
+  if (int rc = rg_shard_fixup_fork(ctx, n_windows, out_dev, out_pitch_words, n_slots, stride_words, slot_base,
+                                   window_slots, max_phase, records_dev, records_cap,
+                                   reinterpret_cast<const rg_step_result*>(c->rows_all), (uint32_t)c->rank,
+                                   (uint32_t)c->world, reinterpret_cast<rg_step_result*>(c->fixed), s, patched))
     return rc;
   if (int rc = gather(ctx, c->fixed, c->fixed_all, row_bytes, s, "ncclAllGather(final rows)")) return rc;
   return rg_shard_commit_impl(ctx, n_windows, reinterpret_cast<const rg_step_result*>(c->fixed_all),
@@ -229,6 +237,12 @@ int rg_comm_create(rg_ctx* ctx, const uint8_t* id, int rank, int world) {
     return hip_err(ctx, he, "hipMalloc(comm scalars)");
   }
   ctx->comm = c;
+  if ((he = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking)) != hipSuccess ||
+      (he = hipEventCreateWithFlags(&c->ev_patched, hipEventDisableTiming)) != hipSuccess ||
+      (he = hipEventCreateWithFlags(&c->ev_lists, hipEventDisableTiming)) != hipSuccess) {
+    rg_comm_release(ctx);
+    return hip_err(ctx, he, "rg_comm_create: aux stream / events");
+  }
   if (int rc = comm_reserve_impl(ctx, kCommDefaultWindows, 0)) {
     rg_comm_release(ctx);
     return rc;
@@ -323,14 +337,18 @@ int rg_shard_exchange_decisions_async(rg_ctx* ctx, uint32_t n_windows, uint32_t*
   // stages 2-4; the commit flags (32) a window where a shard has more undecided slots than a list holds
   if (int rc = exchange_rows(ctx, n_windows, out_dev, out_pitch_words, n_slots, stride_words, slot_base, window_base,
                              window_slots, max_phase, records_dev, records_cap, rows_dev, results_dev,
-                             (uint64_t)undecided_cap + 1, s))
+                             (uint64_t)undecided_cap + 1, s, c->ev_patched))
     return rc;
   // this rank's payload (K lists, then with_v1 K V1 bitmaps) built in place at its own slot of
-  // the receive buffer, and one in-place all-gather: no scratch, no local copy of it
+  // the receive buffer, on the aux stream from the moment the outputs are patched, and one
+  // in-place all-gather once both branches are done: no scratch, no local copy of it
   uint32_t* mine = decisions_all_dev + (uint64_t)c->rank * P;
+  if ((he = hipStreamWaitEvent(c->aux, c->ev_patched, 0)) != hipSuccess) return hip_err(ctx, he, "hipStreamWaitEvent");
   if (int rc = rg_decision_lists_windows_async(ctx, n_windows, out_dev, out_pitch_words, n_slots, stride_words, mine,
-                                               undecided_cap, with_v1 ? mine + K * lw : nullptr, nw, s))
+                                               undecided_cap, with_v1 ? mine + K * lw : nullptr, nw, c->aux))
     return rc;
+  if ((he = hipEventRecord(c->ev_lists, c->aux)) != hipSuccess) return hip_err(ctx, he, "hipEventRecord");
+  if ((he = hipStreamWaitEvent(s, c->ev_lists, 0)) != hipSuccess) return hip_err(ctx, he, "hipStreamWaitEvent");
   return gather(ctx, mine, decisions_all_dev, P * 4, s, "ncclAllGather(decisions)");
 }
 

@@ -2091,7 +2091,10 @@ __device__ __forceinline__ unsigned long long fix_first_draw(const FixParams& f,
 // the rare decision changes (the own vote decides the round-2 count). Every lane works
 // on a block of its own, so no lane idles on a partial pass and no LDS is needed; the
 // statistics are one partial per workgroup.
-constexpr uint32_t kFixGrid = 2048;  // fix-up workgroups at most (grid-stride beyond)
+#ifndef RG_FIX_GRID
+#define RG_FIX_GRID 2048
+#endif
+constexpr uint32_t kFixGrid = RG_FIX_GRID;  // fix-up workgroups at most, all windows (grid-stride beyond)
 // The exchange-stage kernels (fix-up, finish, commit, decision lists) run on a second
 // stream while the NEXT step's persistent lag kernel holds every CU: one 512-thread
 // workgroup per CU at 2 waves per SIMD, 232 VGPRs each at n = 9 (168 at n = 5) and 129 KB
@@ -2693,7 +2696,9 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t c, uint32_t (&bu
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint32_t incl = wave_incl_scan32(c, (int)lane);
   if (lane == 63) buf[par][wave] = incl;
-  __syncthreads();  // (a half is rewritten two calls later, after every thread read it)
+  // an LDS-only barrier: __syncthreads() would also drain the caller's outstanding stores
+  // (a half is rewritten two calls later, after every thread read it)
+  lds_barrier();
   uint32_t pre = 0;
   tot = 0;
 #pragma unroll
@@ -2718,17 +2723,23 @@ static __global__ __launch_bounds__(256, 8) void list_scan_kernel(ListParams L) 
   const uint32_t* out = L.out + win * L.out_pitch;
   const uint64_t cidx = (uint64_t)win * L.n_chunks + chunk;
   uint2* pairs = L.pairs + cidx * kListPairs;
+  // every 16-B group of the chunk in flight at once (8 loads per thread): these waves run
+  // one per SIMD beside the lag kernel, so a load round trip per slice would bound them
+  u32x4 cg[4], vg[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const uint64_t w = (uint64_t)chunk * kListChunkWords + j * 1024 + 4 * tid;
+    cg[j] = w < L.n_words ? load_group(out, L.lout, w, 6) : u32x4{~0u, ~0u, ~0u, ~0u};
+    vg[j] = (L.v1 && w < L.n_words) ? load_group(out, L.lout, w, 7) : u32x4{0u, 0u, 0u, 0u};
+  }
   uint32_t run = 0, pop = 0;
-#pragma unroll 1
+#pragma unroll
   for (int j = 0; j < 4; j++) {
     const uint64_t w = (uint64_t)chunk * kListChunkWords + j * 1024 + 4 * tid;
     uint32_t und[4] = {0, 0, 0, 0};
     if (w < L.n_words) {
-      const u32x4 c = load_group(out, L.lout, w, 6);
-      u32x4 v = c;
-      if (L.v1) v = load_group(out, L.lout, w, 7);
-      const uint32_t cw[4] = {c.x, c.y, c.z, c.w};
-      const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+      const uint32_t cw[4] = {cg[j].x, cg[j].y, cg[j].z, cg[j].w};
+      const uint32_t vw[4] = {vg[j].x, vg[j].y, vg[j].z, vg[j].w};
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         const uint32_t vm = valid_mask(w + q, L.n_words, L.n_slots);
