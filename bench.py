@@ -65,6 +65,12 @@ def c3_bytes_per_slot(n: int, mean_phases: float) -> float:
     return n / 8 + 4 + 2 / 8 + C3_COIN_TABLE_PHASES / 8 + mean_phases / 8
 
 
+# SQ_INSTS_VALU / (512 x GRBM_GUI_ACTIVE / 8) that independent v_xor_b32 / v_add_u32 chains reach
+# at 8 waves per SIMD (tools/valu_peak.hip under rocprofv3 --pmc, profiles/r06/valu_peak_counters.csv):
+# the issue ceiling of 32-bit integer VALU work, below the 512-per-cycle issue figure
+C3_INT_ISSUE_CEILING = 0.79
+
+
 def c3_roofline(r, bytes_slot):
     """C3 is VALU-issue bound (per phase 2n keyed scheduler picks per slot + the coin),
     not HBM bound. achieved = VALU wave-instructions per launch (per-slot count from the
@@ -82,11 +88,15 @@ def c3_roofline(r, bytes_slot):
         pmc = json.load(open(path))
         achieved = pmc["valu_wave_instr_per_slot"] * r["S"] / kern_s / 1e9
         out.update(achieved=achieved, frac=achieved / out["peak"], counter_issue_util=pmc["valu_issue_util"],
-                   counter_file="profiles/pmc_c3.json",
+                   counter_file="profiles/pmc_c3.json", measured_int_issue_ceiling=C3_INT_ISSUE_CEILING,
+                   frac_of_measured_ceiling=pmc["valu_issue_util"] / C3_INT_ISSUE_CEILING,
                    note="achieved = the cluster kernel's VALU wave-instructions over the rg_wmvc_cluster_bitmaps_async call's "
                         "time (coin table + cluster kernel with the bitmaps + statistics fold: a lower bound for the kernel); "
                         "counter_issue_util = SQ_INSTS_VALU / (512 x GRBM_GUI_ACTIVE/8 cycles) of the cluster kernel "
-                        "alone, at the clock the chip actually ran (DVFS); mix_per_slot in the counter file")
+                        "alone, at the clock the chip actually ran (DVFS); mix_per_slot in the counter file; "
+                        "measured_int_issue_ceiling = the same ratio for independent 32-bit integer ALU chains at 8 waves "
+                        "per SIMD (tools/valu_peak.hip, profiles/r06/valu_peak_counters.csv: v_xor / v_add 0.79, "
+                        "v_mul_lo_u32 / v_bcnt 0.48)")
     return out
 
 

@@ -127,7 +127,13 @@ struct Disp {
                          uint64_t base, uint32_t q, uint32_t fp1, Key key, uint64_t cs, uint64_t dseed,
                          uint32_t maxp, uint32_t* info, unsigned long long* part, const uint32_t* coins,
                          uint32_t coin_phases, uint64_t chunk, uint32_t* bm_dec, uint32_t* bm_v1) {
-    if (q == (uint32_t)(N / 2 + 1))  // the majority quorum: the straight-line instantiation
+    constexpr bool kPackable = N <= 5 && N % 2 == 1;  // N fields of N bits; q = fp1 = N / 2 + 1 by default
+    if (kPackable && q == (uint32_t)(N / 2 + 1) && fp1 == q) {  // subset tests instead of popcounts
+      if constexpr (kPackable)
+        hipLaunchKernelGGL((wmvc_cluster_lc_kernel<N, N / 2 + 1, true>), dim3(grid), dim3(256), 0, s, st, stride,
+                           n_slots, base, q, fp1, key, cs, dseed, maxp, info, part, coins, coin_phases, chunk, bm_dec,
+                           bm_v1);
+    } else if (q == (uint32_t)(N / 2 + 1))  // the majority quorum: the straight-line instantiation
       hipLaunchKernelGGL((wmvc_cluster_lc_kernel<N, N / 2 + 1>), dim3(grid), dim3(256), 0, s, st, stride, n_slots,
                          base, q, fp1, key, cs, dseed, maxp, info, part, coins, coin_phases, chunk, bm_dec, bm_v1);
     else

@@ -3233,8 +3233,66 @@ static __global__ __launch_bounds__(kCoinBlock) void coin_table_kernel(Key key, 
 // and of the votes, so the keys' LDS reads, the hashes and the table reads of both rounds
 // are all issued before the first popcount (round 4's body was one dependent LDS round
 // trip after another, per receiver, behind uniform branches on q).
-constexpr uint32_t kClusterChunk = 8192;
+// PK (packed tallies, n <= 5 with q = fp1 = n / 2 + 1, i.e. n = 1, 3, 5 at their
+// defaults): every count test of the phase is a subset test when the decide threshold
+// equals the quorum and every heard set has exactly q members (round 1: c1 >= q iff the
+// heard set lies inside the 1-voters, c0 < q iff it meets them; round 2 likewise over V1,
+// VQ and their union), so the N receivers' heard sets are packed into one word, N bits
+// per receiver, and all N tests of a kind are one AND plus a field-wise nonzero test
+// (packed_nz) instead of 2N popcounts (half-rate on gfx950, as v_mul_lo_u32 is:
+// tools/valu_peak.hip) and 2N compares. The heard sets come from a table indexed by the
+// raw hash bits the picks read (ClusterRaw), pre-shifted into the receiver's field: the
+// hash's bit extraction is one v_bfe instead of the picks' multiply-shift index arithmetic.
+// Bit-identical to the unpacked body (the same heard sets and rules).
 template <int N, int Q>
+struct ClusterRaw {  // raw-bits heard table of the packed body: bits [lo, lo + nb) of h
+  static constexpr int kPicks = Q - 1;
+  static constexpr int kSpan0 = N - 1;
+  static constexpr int kLog0 = kSpan0 == 4 ? 2 : kSpan0 == 2 ? 1 : kSpan0 == 1 ? 0 : -1;
+  static constexpr int lo = kPicks >= 1 && kLog0 >= 0 ? 6 - kLog0 : 0;
+  static constexpr int nb = kPicks >= 1 ? 6 * kPicks - lo : 0;
+  static constexpr uint32_t size = nb <= 12 ? (uint32_t)N << nb : 1u;  // (only n <= 5 instantiates the table)
+};
+template <int N>
+__host__ __device__ constexpr uint32_t packed_rep() {  // x * rep: the N-bit x in every receiver's field
+  uint32_t r = 0;
+  for (int i = 0; i < N; i++) r |= 1u << (N * i);
+  return r;
+}
+// flags at the top bit of each N-bit field: field != 0 (fields hold values < 2^N)
+template <int N>
+__device__ __forceinline__ uint32_t packed_nz(uint32_t x) {
+  constexpr uint32_t L = packed_rep<N>() * ((1u << (N - 1)) - 1u), H = packed_rep<N>() << (N - 1);
+  return (((x & L) + L) | x) & H;
+}
+// field flags (top bits) -> an N-bit mask, bit r = field r: one multiply gathers the
+// flags into bits [T, T + N) with T = (N - 1)^2 (no two partial products share a bit)
+template <int N>
+__host__ __device__ constexpr uint32_t packed_gather_mul() {
+  uint32_t m = 0;
+  for (int r = 0; r < N; r++) m |= 1u << ((N - 1) * (N - 1) - (N - 1) * r);
+  return m;
+}
+template <int N>
+__device__ __forceinline__ uint32_t packed_compress(uint32_t f) {
+  constexpr int T = (N - 1) * (N - 1);
+  return (__umul24(f >> (N - 1), packed_gather_mul<N>()) >> T) & ((1u << N) - 1u);
+}
+template <int N>
+__host__ __device__ constexpr bool packed_compress_exact() {  // every flag pattern gathers exactly
+  for (uint32_t m = 0; m < (1u << N); m++) {
+    uint64_t f = 0;
+    for (int r = 0; r < N; r++)
+      if (m >> r & 1u) f |= 1ull << (N * r);  // (already shifted down by N - 1)
+    if (((f * packed_gather_mul<N>()) >> ((N - 1) * (N - 1)) & ((1u << N) - 1u)) != m) return false;
+  }
+  return true;
+}
+static_assert(packed_compress_exact<1>() && packed_compress_exact<3>() && packed_compress_exact<5>(),
+              "packed_compress gathers every flag pattern");
+
+constexpr uint32_t kClusterChunk = 8192;
+template <int N, int Q, bool PK = false>
 __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* states, uint64_t stride,
                                                               uint64_t n_slots, uint64_t slot_base, uint32_t q_rt,
                                                               uint32_t fp1, Key ckey, uint64_t coin_stream,
@@ -3251,6 +3309,7 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
   __shared__ uint32_t s_bd[kStageWords], s_b1[kStageWords];  // the chunk's decided / V1 bitmap words
   constexpr uint32_t kTabCap = heard_tab_size<N>((uint32_t)N / 2 + 1) ? heard_tab_size<N>((uint32_t)N / 2 + 1) : 1;
   __shared__ uint16_t s_heard[kTabCap];     // heard sets at the majority quorum (heard_mask_tab)
+  __shared__ uint32_t s_raw[PK ? ClusterRaw<N, (Q ? Q : 1)>::size : 1];  // PK: raw-bits heard table, pre-shifted
   const uint32_t q = Q ? (uint32_t)Q : q_rt;
   const uint32_t tab_n = heard_tab_size<N>(q);
   const bool use_tab = tab_n != 0 && tab_n <= kTabCap;  // (uniform; a constant when Q is)
@@ -3263,8 +3322,27 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
     const uint32_t ph = e / (2 * N), rd = (e / N) % 2, rr = e % N;
     s_ck[ph][rd][rr] = (uint32_t)cluster_key(dseed, ph + 1, rd + 1, (int)rr);
   }
-  if (use_tab)
+  if constexpr (PK) {
+    static_assert(N <= 5 && Q == N / 2 + 1, "packed tallies: N fields of N bits, majority quorum");
+    using Raw = ClusterRaw<N, Q>;
+    for (uint32_t e = threadIdx.x; e < Raw::size; e += blockDim.x) {
+      const uint32_t r = e >> Raw::nb;
+      const uint32_t h = (e & ((1u << Raw::nb) - 1u)) << Raw::lo;  // the bits the picks read
+      uint32_t avail = kAll & ~(1u << r), mask = 1u << r;
+      for (int i = 0; i < Raw::kPicks; i++) {  // heard_mask_k's picks, from the raw bits
+        const uint32_t span = (uint32_t)N - 1 - (uint32_t)i;
+        const uint32_t k = (((h >> (6 * i)) & 63u) * span) >> 6;
+        uint32_t a = avail;
+        for (uint32_t t = 0; t < k; t++) a &= a - 1;
+        const uint32_t pick = a & (~a + 1u);
+        mask |= pick;
+        avail &= ~pick;
+      }
+      s_raw[e] = mask << (N * r);
+    }
+  } else if (use_tab) {
     for (uint32_t e = threadIdx.x; e < tab_n; e += blockDim.x) s_heard[e] = (uint16_t)heard_tab_entry<N>(e, q);
+  }
   const uint32_t nw = c1 > c0 ? (uint32_t)((c1 - 1) / 32 - w0 + 1) : 0u;  // <= kStageWords (chunk <= kClusterChunk)
   for (uint32_t e = threadIdx.x; e < N * nw; e += blockDim.x) {
     const uint32_t r = e / nw, w = e % nw;
@@ -3307,8 +3385,11 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
     if (!active) continue;
     // ---- one phase of every replica of slot s (same rules as wmvc_cluster_kernel)
     // the coin word of this phase, loaded ahead (its latency hides behind the heard sets)
+    // (unconditional: a conditional load meant a register zeroed with a load into it still
+    // in flight, so the compiler put a vmcnt(0) wait at the top of every phase, which also
+    // waited for the previous phase's info store; phase 1's row stands in for later phases)
     const bool coin_tabbed = p <= coin_phases;
-    const uint32_t coin_w = coin_tabbed ? coin_tab[(uint64_t)(p - 1) * n_words + s / 32] : 0u;
+    const uint32_t coin_w = coin_tab[(coin_tabbed ? (uint64_t)(p - 1) * n_words : 0ull) + s / 32];
     uint32_t ck[2][N];
     if (p <= kKeyPhases) {
 #pragma unroll
@@ -3321,30 +3402,68 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
 #pragma unroll
         for (int r = 0; r < N; r++) ck[rd][r] = (uint32_t)cluster_key(dseed, p, (uint32_t)rd + 1, r);
     }
-    uint32_t hm[2][N];  // heard sets of both rounds: independent of the votes
-#pragma unroll
-    for (int rd = 0; rd < 2; rd++)
-#pragma unroll
-      for (int r = 0; r < N; r++)
-        hm[rd][r] = use_tab ? heard_mask_tab<N>(s_heard, ck[rd][r], s32, r, q) : heard_mask_k<N>(ck[rd][r], s32, r, q);
-    uint32_t v1 = 0, vq = 0;
-#pragma unroll
-    for (int r = 0; r < N; r++) {
-      const uint32_t c1r = __builtin_popcount(hm[0][r] & st), c0r = __builtin_popcount(hm[0][r] & ~st);
-      v1 |= (uint32_t)(c1r >= q) << r;
-      vq |= (uint32_t)(c1r < q && c0r < q) << r;
-    }
     uint32_t nv1 = 0, need_coin = 0, newly = 0, newv = 0;  // per replica: round-2 vote 1, coin, decides now
+    uint32_t coin_tab_bit;
+    if constexpr (PK) {
+      using Raw = ClusterRaw<N, Q>;
+      constexpr uint32_t rep = packed_rep<N>(), H = rep << (N - 1);
+      uint32_t ph[2] = {0u, 0u};  // both rounds' heard sets, receiver r in bits [N r, N r + N)
 #pragma unroll
-    for (int r = 0; r < N; r++) {
-      const uint32_t c1r = __builtin_popcount(hm[1][r] & v1), cq = __builtin_popcount(hm[1][r] & vq);
-      const uint32_t c0r = q - c1r - cq;
-      const bool d0 = c0r >= fp1, d1 = !d0 && c1r >= fp1;
-      newly |= (uint32_t)(d0 || d1) << r;
-      newv |= (uint32_t)d1 << r;
-      // undecided this phase: 0 if any 0 was heard, else 1 if any 1, else the coin
-      nv1 |= (uint32_t)(d1 || (!d0 && c0r == 0 && c1r > 0)) << r;
-      need_coin |= (uint32_t)(!d0 && !d1 && c0r == 0 && c1r == 0) << r;
+      for (int rd = 0; rd < 2; rd++)
+#pragma unroll
+        for (int r = 0; r < N; r++) {
+          const uint32_t h = fmix32(ck[rd][r] ^ s32);
+          ph[rd] |= s_raw[((uint32_t)r << Raw::nb) + ((h >> Raw::lo) & ((1u << Raw::nb) - 1u))];
+        }
+      // round 1: v1 = all heard voted 1, vq = heard both values
+      const uint32_t rs = __umul24(st, rep);
+      const uint32_t some1 = packed_nz<N>(ph[0] & rs), some0 = packed_nz<N>(ph[0] & ~rs);
+      const uint32_t v1 = packed_compress<N>(H & ~some0), vq = packed_compress<N>(some1 & some0);
+      uint32_t coin_word = coin_w;  // consumed here, as in the unpacked body below
+      asm volatile("" : "+v"(coin_word));
+      coin_tab_bit = (coin_word >> (s & 31)) & 1u;
+      // round 2 (fp1 = q): d0 = none of V1 / VQ heard, d1 = only V1 heard; undecided:
+      // 1 if only V1 / VQ heard and some V1, the coin if only VQ heard
+      const uint32_t rv1 = __umul24(v1, rep), rvq = __umul24(vq, rep);
+      const uint32_t rnz = rv1 | rvq;
+      const uint32_t s1 = packed_nz<N>(ph[1] & rv1), snz = packed_nz<N>(ph[1] & rnz);
+      const uint32_t sn1 = packed_nz<N>(ph[1] & ~rv1), s0 = packed_nz<N>(ph[1] & ~rnz);
+      const uint32_t snq = packed_nz<N>(ph[1] & ~rvq);
+      const uint32_t d1f = H & ~sn1, d0f = H & ~snz;
+      newly = packed_compress<N>(d0f | d1f);
+      newv = packed_compress<N>(d1f);
+      nv1 = packed_compress<N>(d1f | (s1 & ~s0));
+      need_coin = packed_compress<N>(H & ~snq);
+    } else {
+      uint32_t hm[2][N];  // heard sets of both rounds: independent of the votes
+#pragma unroll
+      for (int rd = 0; rd < 2; rd++)
+#pragma unroll
+        for (int r = 0; r < N; r++)
+          hm[rd][r] = use_tab ? heard_mask_tab<N>(s_heard, ck[rd][r], s32, r, q) : heard_mask_k<N>(ck[rd][r], s32, r, q);
+      uint32_t v1 = 0, vq = 0;
+#pragma unroll
+      for (int r = 0; r < N; r++) {
+        const uint32_t c1r = __builtin_popcount(hm[0][r] & st), c0r = __builtin_popcount(hm[0][r] & ~st);
+        v1 |= (uint32_t)(c1r >= q) << r;
+        vq |= (uint32_t)(c1r < q && c0r < q) << r;
+      }
+      // the coin word consumed on every phase, after the round-1 tally (a load left unconsumed
+      // let its register be reused, which put a wait for it at the top of the next phase)
+      uint32_t coin_word = coin_w;
+      asm volatile("" : "+v"(coin_word));  // (materialised here: the compiler would sink it into the coin branch)
+      coin_tab_bit = (coin_word >> (s & 31)) & 1u;
+#pragma unroll
+      for (int r = 0; r < N; r++) {
+        const uint32_t c1r = __builtin_popcount(hm[1][r] & v1), cq = __builtin_popcount(hm[1][r] & vq);
+        const uint32_t c0r = q - c1r - cq;
+        const bool d0 = c0r >= fp1, d1 = !d0 && c1r >= fp1;
+        newly |= (uint32_t)(d0 || d1) << r;
+        newv |= (uint32_t)d1 << r;
+        // undecided this phase: 0 if any 0 was heard, else 1 if any 1, else the coin
+        nv1 |= (uint32_t)(d1 || (!d0 && c0r == 0 && c1r > 0)) << r;
+        need_coin |= (uint32_t)(!d0 && !d1 && c0r == 0 && c1r == 0) << r;
+      }
     }
     newly &= ~decided;
     if (newly && !first) first = p;
@@ -3354,7 +3473,7 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
     if (need_coin) {  // one coin per slot and phase, counted whenever a replica needs it
       uint32_t coin;
       if (coin_tabbed) {
-        coin = (coin_w >> (s & 31)) & 1u;
+        coin = coin_tab_bit;
       } else {
         uint32_t blk[16];
         chacha_block<12>(ckey, ((uint64_t)(p - 1) << 40) | (id >> 9), coin_stream, blk);

@@ -5,9 +5,9 @@ issue utilisation, and (pass 2) the instruction mix.
 
 Peak issue rate (MI355X_MICROARCH.md, "Wave scheduling": a SIMD-32 issues a wave64
 VALU instruction over 2 cycles): 4 SIMDs x 256 CUs / 2 = 512 wave-instructions per
-cycle, reached with >= 2 waves per SIMD. Quarter-rate instructions (v_mul_lo_u32,
-v_mul_hi_u32, v_mad_u64_u32: 32-bit multiplies) take 4 issue slots each, so the bound
-for the kernel's own mix is reported beside the plain count when pass 2 has it.
+cycle. Measured on this chip (tools/valu_peak.hip, 8 waves per SIMD of independent
+chains, the same counters): v_xor_b32 / v_add_u32 reach 0.79 of it, v_mul_lo_u32 and
+v_bcnt_u32_b32 0.48 (twice the issue cost of a plain 32-bit op).
 GRBM_GUI_ACTIVE is summed over the 8 XCDs (the guide's DVFS note): active cycles =
 GRBM_GUI_ACTIVE / 8.
 usage: python tools/pmc_c3_summary.py <p1 counter_collection.csv> [<p2 csv>] <out.json>"""
