@@ -101,12 +101,14 @@ struct KvCounters {
   unsigned long long mode;        // per batch: 0 keyed commit, 1 ordered replay, 2 fault, 3 capacity-ranked
   unsigned long long batch_base;  // heap top before the batch (keyed commit offsets)
   unsigned long long cut;         // mode 3: command index of the first create StoreFull refuses
+                                  // (kCutBits: the refused creates are the kEvRefused bitmap)
 };
 
 // Per-block partials of the plan walk. kPLiveDel: DELETEs that hit a live key (the
 // all-succeed replay); none in a batch => the live count only grows (mode 3).
 enum { kPCreated = 0, kPNewSlots, kPOverflow, kPLiveDelta, kPVersion, kPOps, kPNeed, kPLiveDel, kPCount };
 constexpr uint32_t kNoCreate = 0xFFFFFFFFu;
+constexpr unsigned long long kCutBits = ~0ull - 1;
 
 // What the commit writes for one key, decided by the plan (one record per distinct
 // key of a hash run, at the run head's sorted position + the key's rank in the run).
@@ -286,6 +288,14 @@ __device__ __forceinline__ bool eq_fast(const uint8_t* a, const uint8_t* b, uint
 }
 constexpr uint32_t kFastKey = 16, kFastVal = 64;  // decode fast path: key <= 16 B, value region <= 64 B
 
+// Event bitmaps of a batch that may meet StoreFull (BatchView.cbits), one bit per
+// command index, plane p at cbits + p * kv_plane(n): kEvCreate = SETs on a key that is not
+// live in the all-succeed replay, kEvDelete = DELETEs of a live key there, kEvTail = the
+// creates that are their key's last SET / DELETE of the batch, kEvRefused = the creates
+// StoreFull refuses (decide, batches with live-key DELETEs). Decode zeroes the first three.
+enum { kEvCreate = 0, kEvDelete = 1, kEvTail = 2, kEvRefused = 3, kEvPlanes = 4 };
+__host__ __device__ __forceinline__ uint64_t kv_plane(uint64_t n) { return (n + 31) / 32; }
+
 // ---- 1 decode ----------------------------------------------------------------
 constexpr int kSetPart = 3;  // decode partials per block: pending SETs, their worst-case bytes, pending DELETEs
 __global__ __launch_bounds__(kBlock) void kv_decode_kernel(
@@ -375,8 +385,13 @@ __global__ __launch_bounds__(kBlock) void kv_decode_kernel(
   ops[c] = op;
   sort_key[c] = key == kInvalidKey ? invalid_bucket : (uint32_t)hash_bucket(key, bmask);
   done[c] = 0;  // the plan's per-sorted-position marks (multi-key runs), cleared here: no memset launch
-  if (cbits) {  // the create bitmap and reservations (when StoreFull can fire), likewise
-    if ((c & 31u) == 0) cbits[c >> 5] = 0;
+  if (cbits) {  // the event bitmaps and reservations (when StoreFull can fire), likewise
+    if ((c & 31u) == 0) {
+      const uint64_t pl = kv_plane(n);
+      cbits[c >> 5] = 0;
+      cbits[pl + (c >> 5)] = 0;
+      cbits[2 * pl + (c >> 5)] = 0;
+    }
     cbytes[c] = 0;
   }
   if (op.status != kPending) results[c] = (uint8_t)op.status;
@@ -471,8 +486,9 @@ struct BatchView {
   KeyRec* recs;           // per sorted position: plan -> commit records (run head + key rank)
   uint32_t invalid_bucket;  // sort key of the commands that are not applied (sorted last)
   unsigned long long* part;  // [blocks][kPCount]
-  uint32_t* cbits;           // creates by command index (one bit each), NULL when StoreFull cannot fire
-  unsigned long long* cbytes;  // per command: heap bytes its key reserves when it is the key's create
+  uint32_t* cbits;           // event bitmaps by command index, 4 planes of kv_plane(n) words (kEv*),
+                             // NULL when StoreFull cannot fire
+  unsigned long long* cbytes;  // per command: heap bytes its key reserves when it is the key's last create
 };
 
 __device__ __forceinline__ bool same_key(const BatchView& b, const KvOp& x, const KvOp& y) {
@@ -484,7 +500,8 @@ struct KeyOutcome {
   bool live0, live1, wrote_value, any_set;
   uint64_t ver0, ver1;
   uint32_t last_set;     // command index of the final value's SET
-  uint32_t first_create; // command index of the first SET on a non-live key (kNoCreate: none)
+  uint32_t last_create;  // position of the last SET on a non-live key (kNoCreate: none)
+  uint32_t last_mut;     // position of the last SET or DELETE
   uint64_t n_ops, n_version, n_live_del;
 };
 
@@ -492,7 +509,7 @@ __device__ __forceinline__ KeyOutcome key_start(int64_t slot, const KvEntry& e) 
   KeyOutcome o{};
   o.live0 = o.live1 = slot >= 0 && e.version > 0;
   o.ver0 = o.ver1 = o.live0 ? e.version : 0;
-  o.first_create = kNoCreate;
+  o.last_create = o.last_mut = kNoCreate;
   return o;
 }
 
@@ -500,7 +517,8 @@ __device__ __forceinline__ KeyOutcome key_start(int64_t slot, const KvEntry& e) 
 __device__ __forceinline__ uint8_t key_step(KeyOutcome& o, uint32_t kind, uint32_t c, uint32_t notify) {
   uint8_t r;
   if (kind == 0) {                    // SET: update or insert (store.rs:151-163)
-    if (!o.live1 && o.first_create == kNoCreate) o.first_create = c;
+    if (!o.live1) o.last_create = c;
+    o.last_mut = c;
     o.ver1 = o.live1 ? o.ver1 + 1 : 1;
     o.live1 = true;
     o.wrote_value = true;
@@ -510,6 +528,7 @@ __device__ __forceinline__ uint8_t key_step(KeyOutcome& o, uint32_t kind, uint32
     r = RG_KV_SUCCESS;
   } else if (kind == 2) {             // DELETE (store.rs:220-251)
     r = o.live1 ? RG_KV_SUCCESS : RG_KV_NOT_FOUND;
+    o.last_mut = c;
     if (o.live1) {
       o.n_version += notify;
       o.wrote_value = false;
@@ -524,15 +543,29 @@ __device__ __forceinline__ uint8_t key_step(KeyOutcome& o, uint32_t kind, uint32
   return r;
 }
 
+// key_step plus the command's event bits (cmd: its command index; ev: the event planes
+// of a batch that may meet StoreFull, else NULL).
+__device__ __forceinline__ uint8_t key_step_ev(KeyOutcome& o, uint32_t kind, uint32_t pos, uint32_t cmd,
+                                               uint32_t notify, uint32_t* ev, uint64_t plane) {
+  if (ev) {
+    const uint32_t bit = 1u << (cmd & 31u);
+    if (kind == 0 && !o.live1) atomicOr(ev + kEvCreate * plane + (cmd >> 5), bit);
+    else if (kind == 2 && o.live1) atomicOr(ev + kEvDelete * plane + (cmd >> 5), bit);
+  }
+  return key_step(o, kind, pos, notify);
+}
+
 // Folds a replayed key into the block partials and its commit record; returns the
 // heap bytes the commit will take for it (new key bytes + a new value allocation).
 // (vsrc, vlen: the final value's bytes, from the SET the replay recorded in last_set.)
-// (create: the command index of the key's first create, o.first_create translated by
-// the caller; its bit goes to the create bitmap when StoreFull can fire.)
+// (create: the command index of the key's last create, o.last_create translated by the
+// caller; tail: it is also the key's last SET / DELETE. When StoreFull can fire, the
+// key's plan bytes are reserved at the create and a tail create gets its kEvTail bit:
+// refusing it changes nothing else in the batch.)
 __device__ uint64_t plan_key(const KeyOutcome& o, int64_t slot, const KvEntry& e, uint64_t key_off,
-                             uint32_t key_len, uint64_t vsrc, uint32_t vlen, uint64_t hl, uint32_t create,
-                             uint32_t* cbits, unsigned long long* cbytes, unsigned long long (&acc)[kPCount],
-                             KeyRec& r) {
+                             uint32_t key_len, uint64_t vsrc, uint32_t vlen, uint64_t hl, uint32_t create, bool tail,
+                             uint32_t* cbits, uint64_t plane, unsigned long long* cbytes,
+                             unsigned long long (&acc)[kPCount], KeyRec& r) {
   acc[kPLiveDel] += o.n_live_del;
   acc[kPOps] += o.n_ops;
   acc[kPVersion] += o.n_version;
@@ -559,9 +592,9 @@ __device__ uint64_t plan_key(const KeyOutcome& o, int64_t slot, const KvEntry& e
             ((slot >= 0 || new_slot) && (o.any_set || o.live0 != o.live1) ? kRecVersion : 0u);
   r.create = create;
   const uint64_t need = (new_slot ? key_len : 0) + (value && !in_place ? val_class(vlen) : 0);
-  if (cbits && create != kNoCreate) {  // StoreFull reachable: the create's bit and the key's reservation
-    atomicOr(cbits + (create >> 5), 1u << (create & 31u));
+  if (cbits && create != kNoCreate) {  // StoreFull reachable: the key's reservation, the tail bit
     cbytes[create] = need;
+    if (tail) atomicOr(cbits + kEvTail * plane + (create >> 5), 1u << (create & 31u));
   }
   return need;
 }
@@ -638,6 +671,7 @@ __global__ __launch_bounds__(kBlock) void kv_plan_kernel(BatchView b, StoreView 
   unsigned long long acc[kPCount] = {0, 0, 0, 0, 0, 0, 0, 0};
   const uint64_t bbase = (uint64_t)blockIdx.x * kWalkBlockSpan;
   const uint32_t wl = (uint32_t)wave * kWalkSpan;
+  const uint64_t plane = kv_plane(b.n);
   if (b.skey[bbase] == b.invalid_bucket) {  // the sorted tail of commands not applied: nothing to plan
     if (threadIdx.x < kPCount) b.part[(uint64_t)blockIdx.x * kPCount + threadIdx.x] = 0;
     return;
@@ -715,12 +749,13 @@ __global__ __launch_bounds__(kBlock) void kv_plan_kernel(BatchView b, StoreView 
       KvEntry e{};
       const int64_t slot = table_find(st.hashes, st.ent, st.heap, st.mask, hl, b.data + koff, klen, &e);
       KeyOutcome o = key_start(slot, e);
-      for (uint32_t q = l0; q < l; q++)  // last_set records the LDS position here
-        b.results[s_c[q]] = key_step(o, s_inf[q] & 3u, q, st.notify);
+      for (uint32_t q = l0; q < l; q++)  // last_set / last_create record the LDS position here
+        b.results[s_c[q]] = key_step_ev(o, s_inf[q] & 3u, q, s_c[q], st.notify, b.cbits, plane);
       const uint32_t ls = o.last_set;
       KeyRec r;
       need = plan_key(o, slot, e, koff, klen, s_koff[ls] + s_klen[ls] + 8, s_vlen[ls], hl,
-                      o.first_create == kNoCreate ? kNoCreate : s_c[o.first_create], b.cbits, b.cbytes, acc, r);
+                      o.last_create == kNoCreate ? kNoCreate : s_c[o.last_create], o.last_create == o.last_mut,
+                      b.cbits, plane, b.cbytes, acc, r);
       r.flags |= kRecLast;
       b.recs[i] = r;
     } else {       // general: split the bucket run into keys by their bytes
@@ -747,7 +782,7 @@ __global__ __launch_bounds__(kBlock) void kv_plan_kernel(BatchView b, StoreView 
           const KvOp op = b.ops[c];
           if (q != first && !(op.hash == hl && same_key(b, op, lead))) continue;
           b.done[q] = 1;
-          b.results[c] = key_step(o, op.kind, c, st.notify);
+          b.results[c] = key_step_ev(o, op.kind, c, c, st.notify, b.cbits, plane);
         }
         uint64_t vsrc = 0;
         uint32_t vlen = 0;
@@ -756,8 +791,8 @@ __global__ __launch_bounds__(kBlock) void kv_plan_kernel(BatchView b, StoreView 
           vsrc = kv_val_off(v);
           vlen = v.val_len;
         }
-        need += plan_key(o, slot, e, lead.key_off, lead.key_len, vsrc, vlen, hl, o.first_create, b.cbits, b.cbytes,
-                         acc, r);
+        need += plan_key(o, slot, e, lead.key_off, lead.key_len, vsrc, vlen, hl, o.last_create,
+                         o.last_create == o.last_mut, b.cbits, plane, b.cbytes, acc, r);
       }
       if (keys) {
         r.flags |= kRecLast;
@@ -772,10 +807,11 @@ __global__ __launch_bounds__(kBlock) void kv_plan_kernel(BatchView b, StoreView 
 
 __device__ void kv_ordered(const uint8_t* data, const KvOp* ops, uint64_t n, uint8_t* results, StoreView st);
 
-// Mode 3, a key whose create StoreFull refuses (its create's command index >= the cut):
-// from the create on, the key stays absent (store.rs:153-158: the SET fails, no later
-// command of the batch deletes a live key), so its SETs answer StoreFull and its GETs /
-// EXISTS NotFound. Its commands are the bucket run's (one key) or, in a run of several
+// Mode 3, a key whose (last) create StoreFull refuses (its command index >= the cut, or
+// its kEvRefused bit): from the create on, the key stays absent (store.rs:153-158: the
+// SET fails; no later SET or DELETE of the key: without live-key DELETEs the store stays
+// full, with them decide checked that the create is the key's last mutation), so its
+// SETs answer StoreFull and its GETs / EXISTS NotFound. Its commands are the bucket run's (one key) or, in a run of several
 // keys, those with its hash and key bytes. The counters lose what the all-succeed
 // replay counted for it: the live key, the slot of a new key, and per refused SET one
 // operation and (notifications on) one version.
@@ -827,6 +863,12 @@ __global__ __launch_bounds__(kBlock) void kv_commit_kernel(BatchView b, StoreVie
   const uint64_t wbase = (uint64_t)blockIdx.x * kWalkBlockSpan + (uint64_t)wave * kWalkSpan;
   const uint32_t nh = collect_heads(b, wbase, lane, true, s_heads[wave]);
   const unsigned long long cut = mode == 3 ? st.ctr->cut : ~0ull;
+  const uint32_t* evr = b.cbits ? b.cbits + kEvRefused * kv_plane(b.n) : nullptr;
+  auto refused = [&](uint32_t cr) {  // mode 3: StoreFull refuses the key's (last) create
+    if (cr == kNoCreate) return false;
+    if (cut == kCutBits) return ((evr[cr >> 5] >> (cr & 31u)) & 1u) != 0;
+    return cr >= cut;
+  };
   // this lane's heap offset: block base + exclusive prefix of plan sizes over (wave, lane)
   // (mode 3: the sizes of the keys that are not refused, and the workgroup's base from
   // one atomic on the heap top: the decide scan counted the refused keys too)
@@ -835,7 +877,7 @@ __global__ __launch_bounds__(kBlock) void kv_commit_kernel(BatchView b, StoreVie
     for (uint32_t h = lane; h < nh; h += 64)
       for (uint64_t k = wbase + s_heads[wave][h]; k < b.n; k++) {
         const KeyRec r = b.recs[k];
-        if (!(r.create != kNoCreate && r.create >= cut))
+        if (!refused(r.create))
           mine += (r.flags & kRecNew) ? r.key_len + val_class(r.val_len)
                                       : ((r.flags & kRecValue) && !(r.flags & kRecInPlace) ? val_class(r.val_len) : 0);
         if (r.flags & kRecLast) break;
@@ -872,8 +914,11 @@ __global__ __launch_bounds__(kBlock) void kv_commit_kernel(BatchView b, StoreVie
     for (uint64_t k = i; k < b.n && k < i + kMaxRunKeys; k++) {
       const KeyRec r = b.recs[k];
       int64_t s = r.slot;
-      if (r.create != kNoCreate && r.create >= cut) {  // mode 3: StoreFull refuses this key's create
+      if (refused(r.create)) {  // mode 3: StoreFull refuses this key's create
         refuse_key(b, i, r, k == i && (r.flags & kRecLast), st.notify, corr);
+        // a key live before the batch and deleted in it before the refused create ends
+        // absent (the create is its last mutation): its entry's version goes to 0
+        if (s >= 0) st.ent[s].version = 0;
         if (r.flags & kRecLast) break;
         continue;
       }
@@ -969,7 +1014,7 @@ __global__ __launch_bounds__(kDecBlock) void kv_decide_kernel(StoreView st, cons
                                                               uint32_t walk_blocks, const unsigned long long* set_part,
                                                               uint32_t blocks, uint64_t* block_base,
                                                               uint64_t* group_base, unsigned long long* dpart,
-                                                              unsigned long long* arrivals, const uint32_t* cbits,
+                                                              unsigned long long* arrivals, uint32_t* cbits,
                                                               const unsigned long long* cbytes, uint64_t n_cmds) {
   __shared__ unsigned long long red[kDecBlock / 64][kDCount];
   __shared__ uint32_t s_last;
@@ -1063,6 +1108,7 @@ __global__ __launch_bounds__(kDecBlock) void kv_decide_kernel(StoreView st, cons
   }
   __syncthreads();
   __shared__ unsigned long long s_tot[kDCount], s_path, s_cut, s_failed;
+  __shared__ uint32_t s_violate;
   if (tid < kDCount) {
     unsigned long long t = 0;
     for (int w = 0; w < kDecBlock / 64; w++) t += red[w][tid];
@@ -1075,10 +1121,101 @@ __global__ __launch_bounds__(kDecBlock) void kv_decide_kernel(StoreView st, cons
   // keyed commit (0). Reachable: if no DELETE meets a live key, the live count only
   // grows through the batch, so a create succeeds iff fewer than max_keys - live
   // creates precede it in command order: the keyed commit with the creates ranked
-  // (3, the cut below). Otherwise the ordered replay (1).
+  // (3, the cut below). With live-key DELETEs the live count is a clamped walk over the
+  // batch's events (the scan below): still the keyed commit (3, refused creates by
+  // bitmap) when every refused create is its key's last SET / DELETE, else the ordered
+  // replay (1).
   unsigned long long path = 0;
-  if (ov || live0 + c > st.max_keys) path = (!ov && s_tot[kDLiveDel] == 0 && cbits) ? 3 : 1;
-  if (path == 3) {
+  const bool dels = s_tot[kDLiveDel] != 0;
+  if (ov || live0 + c > st.max_keys) path = (!ov && cbits && live0 <= st.max_keys) ? 3 : 1;
+  if (path == 3 && dels) {
+    // live count L over the batch: a create sets L = min(max_keys, L + 1) (refused when
+    // L = max_keys), a live-key DELETE L - 1. Maps x -> min(C, x + D) compose, so each
+    // thread folds its range of words into (C, D), a workgroup scan gives each range its
+    // starting L, and each thread replays its range: the refused creates' bits, their
+    // reserved heap bytes, and whether one of them is not its key's last mutation
+    const long long M = (long long)st.max_keys, kInf = 1ll << 62;
+    const uint64_t pl = kv_plane(n_cmds), W = pl, per_w = (W + kDecBlock - 1) / kDecBlock;
+    const uint64_t w0 = (uint64_t)tid * per_w, w1 = w0 + per_w < W ? w0 + per_w : W;
+    const uint32_t* evc = cbits + kEvCreate * pl;
+    const uint32_t* evd = cbits + kEvDelete * pl;
+    const uint32_t* evt = cbits + kEvTail * pl;
+    uint32_t* evr = cbits + kEvRefused * pl;
+    long long C = kInf, D = 0;
+    for (uint64_t w = w0; w < w1; w++) {
+      const uint32_t cw = evc[w], dw = evd[w];
+      if (!dw) {
+        const long long k = __builtin_popcount(cw);
+        C = C + k < M ? C + k : M;
+        D += k;
+      } else if (!cw) {
+        const long long k = __builtin_popcount(dw);
+        C -= k;
+        D -= k;
+      } else {
+        for (uint32_t x = cw | dw; x; x &= x - 1) {
+          if (cw & x & (~x + 1u)) { C = C + 1 < M ? C + 1 : M; D++; }
+          else { C--; D--; }
+        }
+      }
+    }
+    __shared__ long long s_sc[kDecBlock], s_sd[kDecBlock];
+    s_sc[tid] = C;
+    s_sd[tid] = D;
+    if (tid == 0) s_violate = 0;
+    __syncthreads();
+    for (int o = 1; o < kDecBlock; o <<= 1) {  // inclusive scan: ranges 0..tid composed in order
+      long long pc = 0, pd = 0;
+      const bool has = tid >= o;
+      if (has) { pc = s_sc[tid - o]; pd = s_sd[tid - o]; }
+      __syncthreads();
+      if (has) {
+        const long long cc = s_sc[tid], dd = s_sd[tid];
+        s_sc[tid] = cc < pc + dd ? cc : pc + dd;
+        s_sd[tid] = pd + dd;
+      }
+      __syncthreads();
+    }
+    long long L = (long long)live0;
+    if (tid > 0) {
+      const long long ec = s_sc[tid - 1], ed = s_sd[tid - 1];
+      L = ec < L + ed ? ec : L + ed;
+    }
+    unsigned long long fb = 0;
+    uint32_t bad = 0;
+    for (uint64_t w = w0; w < w1; w++) {
+      const uint32_t cw = evc[w], dw = evd[w];
+      uint32_t rw = 0;
+      if (!dw && L + __builtin_popcount(cw) <= M) {
+        L += __builtin_popcount(cw);
+      } else if (!dw && L >= M) {
+        rw = cw;
+      } else if (!cw) {
+        L -= __builtin_popcount(dw);
+      } else {
+        for (uint32_t x = cw | dw; x; x &= x - 1) {
+          const uint32_t bit = x & (~x + 1u);
+          if (cw & bit) {
+            if (L >= M) rw |= bit;
+            else L++;
+          } else {
+            L--;
+          }
+        }
+      }
+      evr[w] = rw;
+      bad |= rw & ~evt[w];
+      for (uint32_t x = rw; x; x &= x - 1) fb += cbytes[w * 32 + (uint64_t)__builtin_ctz(x)];
+    }
+    if (bad) s_violate = 1;  // (benign race: every writer stores 1)
+    for (int o = 32; o > 0; o >>= 1) fb += __shfl_xor(fb, o, 64);
+    if (lane == 0) red[wave][0] = fb;
+    __syncthreads();
+    if (tid == 0) s_failed = red[0][0] + red[1][0] + red[2][0] + red[3][0];
+    if (s_violate) path = 1;  // a refused key is mutated again: its later SETs depend on the order
+    if (tid == 0) s_cut = kCutBits;
+    __syncthreads();
+  } else if (path == 3) {
     // the cut = command index of the create of rank max_keys - live (0-based) in
     // command order, from the plan's create bitmap: each thread popcounts a contiguous
     // range of words, a workgroup scan finds the range that holds it
@@ -1123,7 +1260,9 @@ __global__ __launch_bounds__(kDecBlock) void kv_decide_kernel(StoreView st, cons
   const unsigned long long ns = s_tot[kDNewSlots], sets = s_tot[kDSets], set_bytes = s_tot[kDSetBytes];
   // mode 3: the accepted creates take at most max_keys - live new slots, and the heap
   // bytes without the refused keys' reservations
-  const unsigned long long slots = path == 3 && ns > free_keys ? free_keys : ns;
+  // (with live-key DELETEs each frees at most one key for a later create)
+  const unsigned long long room3 = dels ? free_keys + s_tot[kDLiveDel] : free_keys;
+  const unsigned long long slots = path == 3 && ns > room3 ? room3 : ns;
   // the ordered replay creates at most max_keys - live keys plus one per DELETE (each
   // frees at most one), so it needs at most that many new slots
   const unsigned long long room = free_keys + s_tot[kDDels];
@@ -1709,7 +1848,7 @@ struct rg_kv {
   uint8_t* done = nullptr;
   unsigned long long* part = nullptr;
   unsigned long long* set_part = nullptr;  // [blocks][2] decode partials: pending SETs, worst-case bytes
-  uint32_t* cbits = nullptr;               // [cap / 32] creates by command index (mode 3)
+  uint32_t* cbits = nullptr;               // [kEvPlanes][cap / 32 + 1] event bitmaps (mode 3)
   unsigned long long* cbytes = nullptr;    // [cap] heap bytes reserved at each create (mode 3)
   // host-side upper bound of the live keys after every enqueued batch (exact after a
   // synchronising call): a batch marks its creates only when it could meet StoreFull
@@ -1776,7 +1915,7 @@ int ensure_scratch(rg_kv* kv, uint64_t n) {
   KV_HIP(kv, hipMalloc(&kv->done, cap));
   KV_HIP(kv, hipMalloc(&kv->part, blocks * kPCount * 8));
   KV_HIP(kv, hipMalloc(&kv->set_part, blocks * kSetPart * 8));
-  KV_HIP(kv, hipMalloc(&kv->cbits, (cap / 32 + 1) * 4));
+  KV_HIP(kv, hipMalloc(&kv->cbits, kEvPlanes * (cap / 32 + 1) * 4));
   KV_HIP(kv, hipMalloc(&kv->cbytes, cap * 8));
   KV_HIP(kv, hipMalloc(&kv->sort_hist, (cap / kL1Chunk + 1) * kRadix * 4));
   KV_HIP(kv, hipMalloc(&kv->bin_lo, (kRadix + 1) * 4));

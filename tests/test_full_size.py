@@ -156,6 +156,69 @@ def test_c4_full_size_store_full(oracle):
         assert got_state["data"] == exp_state["data"]
 
 
+def kv_blobs(kinds, ids, vals):
+    """bincode KVOperation blobs (u32 variant, u64 key length, key, [u64 value length,
+    value]) for keys "k%011d" % id and 8-digit values, built with numpy: (data, offsets)."""
+    n = len(kinds)
+    rows = np.zeros((n, 40), dtype=np.uint8)
+    rows[:, 0] = kinds
+    rows[:, 4] = 12
+    rows[:, 12] = ord("k")
+    pw = 10 ** np.arange(10, -1, -1, dtype=np.int64)
+    rows[:, 13:24] = (ids[:, None] // pw) % 10 + ord("0")
+    rows[:, 24] = 8
+    rows[:, 32:40] = (vals[:, None] // pw[3:]) % 10 + ord("0")
+    lens = np.where(kinds == 0, 40, 24)
+    data = rows[np.arange(40)[None, :] < lens[:, None]]
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum(lens, out=offs[1:])
+    return data, offs
+
+
+def test_c4_full_size_store_full_live_deletes(oracle):
+    """StoreFull with live-key DELETEs at full size (2^22 commands per batch, max_keys
+    3,000,000): batch 1 creates 2^22 distinct keys (the last 1,194,304 refused: the cut);
+    batch 2 interleaves DELETEs (1/4 of the commands, over half of the live keys), creates
+    of fresh keys (each SET once), updates and GETs of the other half: decide's clamped scan over 2^22 events picks the refused
+    creates (path 3, no ordered replay), against the sequential C restatement: every
+    result, the counters and the final store."""
+    torch = torch_cuda()
+    from rabia_amd.kvstore import DeviceKVStore, KVStoreConfig
+    S, mk = 1 << 22, 3_000_000
+    rng = np.random.default_rng(11)
+    res = torch.zeros(S, dtype=torch.uint8, device="cuda")
+    ref = oracle.KVStoreC(max_keys=mk)
+    with DeviceKVStore(KVStoreConfig(max_keys=mk)) as kv:
+        b1 = (np.zeros(S, dtype=np.uint8), np.arange(S, dtype=np.int64), rng.integers(0, 10**8, S))
+        r = rng.random(S)
+        kinds = np.select([r < 0.25, r < 0.55, r < 0.65], [2, 0, 0], 1).astype(np.uint8)
+        # DELETEs hit keys [0, mk / 2), updates / GETs keys [mk / 2, mk) (never deleted: an
+        # update is never a create), fresh keys are SET once: every refused create is its
+        # key's last mutation, so the batch stays on the keyed path
+        ids = np.where(r < 0.25, rng.integers(0, mk // 2, S),
+              np.where(r < 0.55, S + np.arange(S), rng.integers(mk // 2, mk, S)))
+        b2 = (kinds, ids, rng.integers(0, 10**8, S))
+        for want_path, (k, i, v) in ((3, b1), (3, b2)):
+            data, offs = kv_blobs(k, i, v)
+            d_data = torch.from_numpy(data).to("cuda")
+            d_off = torch.from_numpy(offs.view(np.int64)).to("cuda")
+            kv.apply_async(d_data.data_ptr(), d_off.data_ptr(), S, 0, res.data_ptr())
+            kv.sync()
+            stats = kv.stats()
+            assert stats["last_path"] == want_path and stats["ordered_batches"] == 0, stats
+            exp_res = ref.apply(data, offs, np.ones(S, dtype=np.uint8))
+            got = res.cpu().numpy()
+            np.testing.assert_array_equal(got, exp_res)
+            assert (got == 5).any() and (got == 0).any()  # RG_KV_E_FULL and Success
+            rs = ref.stats()
+            assert stats["live_keys"] == rs["live_keys"] and stats["version"] == rs["version"]
+            assert stats["total_operations"] == rs["total_operations"] and stats["flags"] == 0
+            del d_data, d_off
+        got_state, exp_state = kv.get_state(), ref.state()
+        assert got_state["version"] == exp_state["version"]
+        assert got_state["data"] == exp_state["data"]
+
+
 def test_c5_full_size_step(oracle):
     torch = torch_cuda()
     n, S, T = 9, 1 << 26, 1024

@@ -200,13 +200,89 @@ def test_gpu_store_full_capacity_ranked(n, key_space, max_keys, bucket_bits, bat
             _check_state(dev, ref)
         assert R.E_FULL in got
         assert 3 in paths and dev.stats()["ordered_batches"] == 0, paths
-        # a DELETE of a live key in a batch that meets StoreFull: the ordered replay
+        # a DELETE of a live key in a batch that meets StoreFull: the clamped scan (3) when
+        # every refused create is its key's last mutation, else the ordered replay (1)
         victim = next(iter(ref.data))
         blobs = [R.encode_op(R.DELETE, victim)] + no_delete(random_blobs(rng, n, key_space))
         got = [int(x) for x in dev.apply_commands(blobs)]
         assert got == ref.apply_commands(blobs)
         _check_state(dev, ref)
-        assert dev.stats()["last_path"] == 1 and dev.stats()["ordered_batches"] == 1
+        st = dev.stats()
+        assert st["last_path"] in (1, 3) and st["ordered_batches"] == (st["last_path"] == 1)
+
+
+def live_delete_batch(rng, live, n, fresh):
+    """Creates of fresh keys (each SET once: a refused create is its key's last mutation),
+    DELETEs of keys live before the batch, updates of live keys, GETs / EXISTS of both."""
+    out, made = [], []
+    for _ in range(n):
+        r = rng.random()
+        if r < 0.40:
+            k = f"new{next(fresh)}".encode()
+            made.append(k)
+            out.append(R.encode_op(R.SET, k, f"v{rng.randrange(1 << 20)}".encode()))
+        elif r < 0.60 and live:
+            out.append(R.encode_op(R.DELETE, rng.choice(live)))
+        elif r < 0.75 and made:
+            out.append(R.encode_op(rng.choice([R.GET, R.EXISTS]), rng.choice(made)))
+        elif r < 0.85 and live:
+            out.append(R.encode_op(R.SET, rng.choice(live), b"u" + bytes(str(rng.randrange(99)), "ascii")))
+        else:
+            out.append(R.encode_op(R.EXISTS, rng.choice(live) if live else b"none"))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,max_keys,bucket_bits,batches", [(3000, 800, 0, 3), (4000, 1500, 12, 3), (600, 50, 0, 4)])
+def test_gpu_store_full_with_live_deletes(n, max_keys, bucket_bits, batches):
+    """StoreFull reachable in batches that also DELETE live keys: the live count is a
+    clamped walk over the creates and deletes in command order (decide's scan); a create is
+    refused iff it finds the store full. Equal to the in-order restatement (results, store,
+    counters) on the keyed path (3), also with multi-key runs (12-bit buckets) and a live key
+    deleted and re-updated (its update a create, refused or not)."""
+    import itertools
+    rng = random.Random(n + max_keys)
+    fresh = itertools.count()
+    # (deleted keys keep their table slots: a table well above max_keys for the fresh keys)
+    with _store(max_keys=max_keys, max_value_size=64, bucket_bits=bucket_bits, table_slots=1 << 15) as dev:
+        ref = R.KVStoreRef(max_keys=max_keys, max_value_size=64)
+        paths = []
+        for _ in range(batches):
+            blobs = live_delete_batch(rng, list(ref.data), n, fresh)
+            got = [int(x) for x in dev.apply_commands(blobs)]
+            assert got == ref.apply_commands(blobs)
+            _check_state(dev, ref)
+            paths.append(dev.stats()["last_path"])
+        assert R.E_FULL in got and R.OK in got
+        assert 3 in paths, paths
+
+
+@pytest.mark.gpu
+def test_gpu_store_full_live_delete_cases():
+    """Hand-made StoreFull batches with live-key DELETEs: a refused create that is its key's
+    last mutation stays on the keyed path (3), including a key live before the batch,
+    deleted, then re-created and refused (its entry goes to version 0); a refused key SET
+    again after a DELETE freed a slot takes the ordered replay (1)."""
+    def run(dev, ref, cmds):
+        blobs = [R.encode_op(k, key, val) for k, key, val in cmds]
+        got = [int(x) for x in dev.apply_commands(blobs)]
+        assert got == ref.apply_commands(blobs)
+        _check_state(dev, ref)
+        return got, dev.stats()["last_path"]
+
+    S, G, D = R.SET, R.GET, R.DELETE
+    with _store(max_keys=3, max_value_size=64) as dev:
+        ref = R.KVStoreRef(max_keys=3, max_value_size=64)
+        run(dev, ref, [(S, b"a", b"1"), (S, b"b", b"1"), (S, b"c", b"1")])  # full
+        got, path = run(dev, ref, [(S, b"k1", b"x"), (D, b"a", b""), (S, b"k2", b"y"), (G, b"k1", b""),
+                                   (G, b"k2", b""), (S, b"k3", b"z")])
+        assert path == 3 and got == [R.E_FULL, R.OK, R.OK, R.NOT_FOUND, R.OK, R.E_FULL]
+        # b: live, deleted, k4 takes its place, b re-created and refused (its last mutation)
+        got, path = run(dev, ref, [(D, b"b", b""), (S, b"k4", b"w"), (S, b"b", b"2"), (G, b"b", b"")])
+        assert path == 3 and got == [R.OK, R.OK, R.E_FULL, R.NOT_FOUND]
+        # k5 refused, then a DELETE frees a key and k5's second SET succeeds: ordered replay
+        got, path = run(dev, ref, [(S, b"k5", b"1"), (D, b"c", b""), (S, b"k5", b"2"), (G, b"k5", b"")])
+        assert path == 1 and got == [R.E_FULL, R.OK, R.OK, R.OK]
 
 
 @pytest.mark.gpu

@@ -79,7 +79,7 @@ for step in "$@"; do
   case $name in
     tests)
       if [ -n "$arg" ]; then
-        run tests 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$arg"
+        run tests 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${arg//:/ }"
       else
         run tests 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
       fi ;;
