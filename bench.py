@@ -40,7 +40,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402  (imported before the native library: shared HIP runtime)
 
 from rabia_amd import _native as N  # noqa: E402
-from rabia_amd.engine import PhaseEvaluator  # noqa: E402
+from rabia_amd.engine import PhaseEvaluator, record_window_words  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 WINDOW = 1 << 20
@@ -492,7 +492,7 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, comm, bitmaps):
     for i in range(a.sets):
         votes = torch.empty(K * in_words, dtype=torch.int32, device="cuda")
         out = torch.empty(K * out_words, dtype=torch.int32, device="cuda")
-        rec = torch.empty(K * cap, dtype=torch.int64, device="cuda")
+        rec = torch.empty(K * record_window_words(S, cap), dtype=torch.int32, device="cuda")  # draw-record regions
         for k in range(K):
             ev.trace_generate_async(N.RG_TRACE_AGREE90, 1000 + i * K + k, 1 + (i * K + k) * window_slots + start, S,
                                     stride, votes.data_ptr() + 4 * k * in_words, comp.cuda_stream)

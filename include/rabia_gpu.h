@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define RG_ABI_VERSION 5
+#define RG_ABI_VERSION 6  /* 6: 4-B draw records in per-window regions (rg_record_window_words) */
 #define RG_MAX_REPLICAS 16
 #define RG_OUT_PLANES 8
 /* rg_create's scratch reservation (rg_reserve): launches of up to 2^32 slots over up to
@@ -189,9 +189,11 @@ int rg_last_stage_result(rg_ctx* ctx, int stage, rg_step_result* out_host);
  * the engine's draw  rng_next + (VQ slots of shards 0..r-1) + k  — ascending slot
  * order over the whole window, as one evaluator (engine.rs:567-611). Per window:
  *  1. every shard: rg_phase_step_shard_async — evaluates its slots with draws taken
- *     at a provisional position (no cross-GPU wait), writes one 8-B draw record per
- *     VQ slot (records_dev, capacity records_cap; n_slots always suffices) and its
- *     row (rg_step_result): counts, extremes and n_draws of its NON-VQ slots.
+ *     at a provisional position (no cross-GPU wait), writes one 4-B draw record per
+ *     VQ slot into its record region (records_dev: rg_record_window_words(n_slots,
+ *     records_cap) u32 words, a segment table then records_cap records; records_cap =
+ *     n_slots always suffices) and its row (rg_step_result): counts, extremes and
+ *     n_draws of its NON-VQ slots.
  *     Draw-record overflow (n_draws > records_cap: the records past the cap are not
  *     written) is NOT flagged in this row: the step cannot know it before its
  *     statistics fold. The fix-up flags it (flags value 8) in its final row, and the
@@ -214,16 +216,21 @@ int rg_last_stage_result(rg_ctx* ctx, int stage, rg_step_result* out_host);
  * row_dev / result_dev may be NULL: the context then keeps the latest fix-up's and
  * commit's result for rg_last_stage_result (rg_last_result returns phase steps'
  * results only — a fix-up may run on another stream than the next window's step). */
+/* u32 words of one window's draw-record region: the segment table (one word per 2^24
+ * slots + 1, rounded up to 4) followed by records_cap records. A record: bits 0-23 the VQ
+ * slot's offset inside its 2^24-slot segment, bits 24-30 the class / both decisions / the
+ * provisional own vote (rabia_amd/csrc/rg_common.h). */
+uint64_t rg_record_window_words(uint64_t n_slots, uint64_t records_cap);
 int rg_phase_step_shard_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev,
                               uint64_t n_slots, uint64_t stride_words, uint64_t slot_base,
-                              uint64_t max_phase, uint64_t* records_dev, uint64_t records_cap,
+                              uint64_t max_phase, uint32_t* records_dev, uint64_t records_cap,
                               rg_step_result* row_dev, void* stream);
 /* Stage (1) for n_windows consecutive windows of this shard in ONE launch (the shard
  * step's fixed ramp/drain cost is paid once, not per window): window w's shard is
  * [slot_base + w * window_stride, + n_slots), its planes at votes_dev + w *
  * votes_pitch_words / out_dev + w * out_pitch_words (each a buffer in the context
- * layout, stride_words as for one window), its draw records at records_dev + w *
- * records_cap, its row at rows_dev[w] (required). Equivalent to n_windows calls of
+ * layout, stride_words as for one window), its record region at records_dev + w *
+ * rg_record_window_words(n_slots, records_cap), its row at rows_dev[w] (required). Equivalent to n_windows calls of
  * rg_phase_step_shard_async in window order, except that every window takes its
  * provisional draws from the same position and shard_draws does not advance (the
  * fix-up re-draws every VQ slot at its global position, so the fixed outputs, rows
@@ -238,17 +245,18 @@ int rg_phase_step_shard_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* 
 int rg_phase_step_shard_windows_async(rg_ctx* ctx, uint32_t n_windows, const uint32_t* votes_dev,
                                       uint64_t votes_pitch_words, uint32_t* out_dev, uint64_t out_pitch_words,
                                       uint64_t n_slots, uint64_t stride_words, uint64_t slot_base,
-                                      uint64_t window_stride, uint64_t max_phase, uint64_t* records_dev,
+                                      uint64_t window_stride, uint64_t max_phase, uint32_t* records_dev,
                                       uint64_t records_cap, rg_step_result* rows_dev, void* stream);
 int rg_shard_fixup_async(rg_ctx* ctx, uint32_t* out_dev, uint64_t n_slots, uint64_t stride_words,
-                         uint64_t slot_base, uint64_t max_phase, const uint64_t* records_dev,
+                         uint64_t slot_base, uint64_t max_phase, const uint32_t* records_dev,
                          uint64_t records_cap, const rg_step_result* rows_dev, uint32_t shard,
                          uint32_t n_shards, rg_step_result* row_dev, void* stream);
 /* Stages (3) and (4) for n_windows consecutive windows at once (after
  * rg_phase_step_shard_windows_async): rows_dev = every shard's n_windows rows,
  * rank-major [n_shards][n_windows] (one all-gather of each shard's rows); window w's
  * outputs at out_dev + w * out_pitch_words, its slot ids + w * window_stride, its
- * records at records_dev + w * records_cap; rows_out_dev[w] = its final row. The
+ * record region at records_dev + w * rg_record_window_words(n_slots, records_cap);
+ * rows_out_dev[w] = its final row. The
  * commit folds [n_shards][n_windows] final rows window by window (window w =
  * [window_base + w * window_slots, + window_slots)) into results_dev[w]. Equivalent
  * to the per-window calls in window order. window_slots of the commit must equal the
@@ -256,7 +264,7 @@ int rg_shard_fixup_async(rg_ctx* ctx, uint32_t* out_dev, uint64_t n_slots, uint6
  * out_pitch_words obeys the step's pitch rule. */
 int rg_shard_fixup_windows_async(rg_ctx* ctx, uint32_t n_windows, uint32_t* out_dev, uint64_t out_pitch_words,
                                  uint64_t n_slots, uint64_t stride_words, uint64_t slot_base, uint64_t window_stride,
-                                 uint64_t max_phase, const uint64_t* records_dev, uint64_t records_cap,
+                                 uint64_t max_phase, const uint32_t* records_dev, uint64_t records_cap,
                                  const rg_step_result* rows_dev, uint32_t shard, uint32_t n_shards,
                                  rg_step_result* rows_out_dev, void* stream);
 int rg_shard_commit_windows_async(rg_ctx* ctx, uint32_t n_windows, const rg_step_result* rows_dev, uint32_t n_shards,
@@ -303,7 +311,7 @@ int rg_comm_allgather_async(rg_ctx* ctx, const void* send_dev, void* recv_dev, u
  * [ceil(n_slots/32)] words (rg_decision_bitmap_windows_async's payload). */
 int rg_shard_exchange_windows_async(rg_ctx* ctx, uint32_t n_windows, uint32_t* out_dev, uint64_t out_pitch_words,
                                     uint64_t n_slots, uint64_t stride_words, uint64_t slot_base, uint64_t window_base,
-                                    uint64_t window_slots, uint64_t max_phase, const uint64_t* records_dev,
+                                    uint64_t window_slots, uint64_t max_phase, const uint32_t* records_dev,
                                     uint64_t records_cap, const rg_step_result* rows_dev, rg_step_result* results_dev,
                                     uint32_t* bitmaps_all_dev, void* stream);
 /* The same stages (2)-(4), with the decided-slot payload as undecided lists instead of
@@ -320,7 +328,7 @@ int rg_shard_exchange_windows_async(rg_ctx* ctx, uint32_t n_windows, uint32_t* o
 int rg_shard_exchange_decisions_async(rg_ctx* ctx, uint32_t n_windows, uint32_t* out_dev, uint64_t out_pitch_words,
                                       uint64_t n_slots, uint64_t stride_words, uint64_t slot_base,
                                       uint64_t window_base, uint64_t window_slots, uint64_t max_phase,
-                                      const uint64_t* records_dev, uint64_t records_cap,
+                                      const uint32_t* records_dev, uint64_t records_cap,
                                       const rg_step_result* rows_dev, rg_step_result* results_dev,
                                       uint32_t undecided_cap, uint32_t with_v1, uint32_t* decisions_all_dev,
                                       void* stream);

@@ -215,17 +215,25 @@ int or_ref_step(int n, int q, int self_lane, uint64_t seed, uint64_t rng_base,
 /* draw record with the decision under either own vote (engine.rs:540-542,      */
 /* 624-628). The row counts the NON-VQ slots only; n_draws = the VQ slots;     */
 /* rng_next = n_draws (the provisional position from 0); watermark 0.           */
+/* The record region (the device's format, include/rabia_gpu.h                 */
+/* rg_record_window_words): a segment table, table[s] = local draw number of   */
+/* the first VQ slot at or after slot s * 2^24, then the 4-B records (offset    */
+/* inside the segment | info << 24).                                           */
 /* ------------------------------------------------------------------------- */
+uint64_t or_record_table_words(uint64_t S) { return (((S + 0xFFFFFFull) >> 24) + 1 + 3) & ~3ull; }
+
 int or_shard_step(int n, int q, int self_lane, uint64_t slot_base, uint64_t max_phase,
                   const uint8_t* r1, const uint8_t* r2, uint64_t S, uint8_t* o_r1, uint8_t* o_r2own,
-                  uint8_t* o_dec, uint8_t* o_committed, uint8_t* o_value, uint64_t* records,
+                  uint8_t* o_dec, uint8_t* o_committed, uint8_t* o_value, uint32_t* region,
                   uint64_t records_cap, or_result* row) {
   if (n < 1 || n > 16 || q < 1) return -1;
   memset(row, 0, sizeof *row);
   uint64_t k = 0, max_v1p1 = 0, first_und = slot_base + S;
   uint8_t votes2[16];
   const int lane_ok = self_lane >= 0 && self_lane < n;
+  uint32_t* records = region + or_record_table_words(S);
   for (uint64_t s = 0; s < S; s++) {
+    if ((s & 0xFFFFFFull) == 0) region[s >> 24] = (uint32_t)k;
     const uint8_t* x1 = r1 + s * n;
     int c0, c1, cq, present;
     count3(x1, n, &c0, &c1, &cq, &present);
@@ -246,7 +254,7 @@ int or_shard_step(int n, int q, int self_lane, uint64_t slot_base, uint64_t max_
       o_committed[s] = (uint8_t)(d <= OR_V1);
       o_value[s] = (uint8_t)(d == OR_V1);
       const uint32_t info = cls | (d0 << 2) | (d1 << 4) | ((uint32_t)(prov == OR_V1) << 6);
-      if (k < records_cap) records[k] = ((uint64_t)info << 32) | (uint32_t)s;
+      if (k < records_cap) records[k] = ((uint32_t)s & 0xFFFFFFu) | (info << 24);
       k++;
       continue;  /* counted by the fix-up */
     }
@@ -286,17 +294,21 @@ int or_shard_step(int n, int q, int self_lane, uint64_t slot_base, uint64_t max_
  * last_committed_max within max_phase, first_undecided). out_row.rng_next = rng_after
  * (the engine position after this window, every shard's draws); *flags |= 8 when the
  * records did not fit (n_draws > records_cap: the outputs past the cap stay provisional). */
-int or_shard_fixup(uint64_t seed, uint64_t g0, uint64_t slot_base, uint64_t max_phase,
-                   const uint64_t* records, uint64_t records_cap, uint8_t* o_r2own, uint8_t* o_dec,
+int or_shard_fixup(uint64_t seed, uint64_t g0, uint64_t slot_base, uint64_t max_phase, uint64_t S,
+                   const uint32_t* region, uint64_t records_cap, uint8_t* o_r2own, uint8_t* o_dec,
                    uint8_t* o_committed, uint8_t* o_value, const or_result* row, uint64_t rng_after,
                    or_result* out_row, uint64_t* flags) {
   uint32_t key[8];
   or_seed_from_u64(seed, key);
   *out_row = *row;
   const uint64_t nn = row->n_draws < records_cap ? row->n_draws : records_cap;
+  const uint64_t n_chunks = (S + 0xFFFFFFull) >> 24;
+  const uint32_t* records = region + or_record_table_words(S);
   uint64_t max_v1p1 = row->last_committed_max ? row->last_committed_max + 1 : 0;
+  uint64_t c = 0;
   for (uint64_t k = 0; k < nn; k++) {
-    const uint32_t off = (uint32_t)records[k], info = (uint32_t)(records[k] >> 32);
+    while (c + 1 < n_chunks && region[c + 1] <= k) c++;  /* record k's segment */
+    const uint32_t off = (uint32_t)((c << 24) | (records[k] & 0xFFFFFFu)), info = (records[k] >> 24) & 0x7Fu;
     const uint32_t cls = info & 3u;
     const int c1 = cls == 1u, c0 = cls == 2u;  /* only the comparison matters */
     const int own = or_ref_round2_vote_for_question(c0, c1, or_ref_draw(key, g0 + k));

@@ -65,17 +65,19 @@ int or_wmvc_step(int n, int q, int fp1, int self_lane, uint64_t coin_seed,
 
 /* --- sharded REF: one engine over a window split into shards ---------------- */
 /* The product's protocol (include/rabia_gpu.h "Sharded REF"): stage 1
- * evaluates a shard with a provisional own vote for every VQ slot and leaves one draw
- * record per VQ slot (slot offset | info << 32: info bits 0-1 c1-vs-c0 class (0 tie,
- * 1 c1 > c0, 2 c1 < c0), 2-3 the decision under own V0, 4-5 under own V1, 6 the
- * provisional own vote) and a row of its non-VQ slots; stage 3 re-draws every VQ slot
- * at its global stream position g0 + k and patches the outputs and the row. */
+ * evaluates a shard with a provisional own vote for every VQ slot and leaves one 4-B draw
+ * record per VQ slot in a record region (a segment table of the first record of every
+ * 2^24-slot segment, then the records: offset inside the segment | info << 24, info bits 0-1
+ * c1-vs-c0 class (0 tie, 1 c1 > c0, 2 c1 < c0), 2-3 the decision under own V0, 4-5 under
+ * own V1, 6 the provisional own vote) and a row of its non-VQ slots; stage 3 re-draws
+ * every VQ slot at its global stream position g0 + k and patches the outputs and the row. */
+uint64_t or_record_table_words(uint64_t S);
 int or_shard_step(int n, int q, int self_lane, uint64_t slot_base, uint64_t max_phase,
                   const uint8_t* r1, const uint8_t* r2, uint64_t S, uint8_t* o_r1, uint8_t* o_r2own,
-                  uint8_t* o_dec, uint8_t* o_committed, uint8_t* o_value, uint64_t* records,
+                  uint8_t* o_dec, uint8_t* o_committed, uint8_t* o_value, uint32_t* region,
                   uint64_t records_cap, or_result* row);
-int or_shard_fixup(uint64_t seed, uint64_t g0, uint64_t slot_base, uint64_t max_phase,
-                   const uint64_t* records, uint64_t records_cap, uint8_t* o_r2own, uint8_t* o_dec,
+int or_shard_fixup(uint64_t seed, uint64_t g0, uint64_t slot_base, uint64_t max_phase, uint64_t S,
+                   const uint32_t* region, uint64_t records_cap, uint8_t* o_r2own, uint8_t* o_dec,
                    uint8_t* o_committed, uint8_t* o_value, const or_result* row, uint64_t rng_after,
                    or_result* out_row, uint64_t* flags);
 

@@ -85,6 +85,7 @@ _SIGS = {
     "rg_set_state": (ctypes.c_int, [vp, ctypes.POINTER(RgEngineState)]),
     "rg_get_state": (ctypes.c_int, [vp, ctypes.POINTER(RgEngineState)]),
     "rg_phase_step_async": (ctypes.c_int, [vp, vp, vp, u64, u64, u64, u64, u64, vp, vp]),
+    "rg_record_window_words": (u64, [u64, u64]),
     "rg_phase_step": (ctypes.c_int, [vp, vp, vp, u64, u64, u64, u64, u64, ctypes.POINTER(RgStepResult)]),
     "rg_phase_step_shard_async": (ctypes.c_int, [vp, vp, vp, u64, u64, u64, u64, vp, u64, vp, vp]),
     "rg_phase_step_shard_windows_async": (ctypes.c_int, [vp, u32, vp, u64, vp, u64, u64, u64, u64, u64, u64, vp, u64,

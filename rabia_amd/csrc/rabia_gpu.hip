@@ -293,6 +293,10 @@ extern "C" {
 
 int rg_abi_version(void) { return RG_ABI_VERSION; }
 
+uint64_t rg_record_window_words(uint64_t n_slots, uint64_t records_cap) {
+  return rec_table_words(n_slots) + records_cap;
+}
+
 int rg_device_count(int* out) {
   if (!out) return fail(nullptr, RG_EINVAL, "rg_device_count: null out");
   int n = 0;
@@ -461,7 +465,7 @@ struct WinArgs {
 
 static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, uint64_t n_slots, uint64_t stride_words,
               uint64_t slot_base, uint64_t phase, uint64_t max_phase, rg_step_result* result_dev, void* stream,
-              bool shard, uint64_t* records_dev, uint64_t records_cap, WinArgs win = WinArgs()) {
+              bool shard, uint32_t* records_dev, uint64_t records_cap, WinArgs win = WinArgs()) {
   if (!ctx) return fail(nullptr, RG_EINVAL, "rg_phase_step: null context");
   if (shard && ctx->cfg.mode != RG_MODE_REF)
     return fail(ctx, RG_EINVAL, "rg_phase_step_shard: REF mode only (WMVC coins are shard-invariant already)");
@@ -569,8 +573,10 @@ static int step_impl(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, 
   p.dbg = nullptr;
   p.in_bytes = need_in * 4;
   p.out_bytes = need_out * 4;
-  p.vq_rec = reinterpret_cast<unsigned long long*>(records_dev);
+  p.vq_rec = records_dev;
   p.vq_cap = records_cap;
+  p.rec_tw = (uint32_t)rec_table_words(n_slots);
+  p.rec_pitch = p.rec_tw + records_cap;
   p.n_win = win.n;
   p.win_in_pitch = win.in_pitch;
   p.win_out_pitch = win.out_pitch;
@@ -623,7 +629,7 @@ int rg_phase_step_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_de
 }
 
 int rg_phase_step_shard_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* out_dev, uint64_t n_slots,
-                              uint64_t stride_words, uint64_t slot_base, uint64_t max_phase, uint64_t* records_dev,
+                              uint64_t stride_words, uint64_t slot_base, uint64_t max_phase, uint32_t* records_dev,
                               uint64_t records_cap, rg_step_result* row_dev, void* stream) {
   return step_impl(ctx, votes_dev, out_dev, n_slots, stride_words, slot_base, 1, max_phase, row_dev, stream, true,
                    records_dev, records_cap);
@@ -632,7 +638,7 @@ int rg_phase_step_shard_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* 
 int rg_phase_step_shard_windows_async(rg_ctx* ctx, uint32_t n_windows, const uint32_t* votes_dev,
                                       uint64_t votes_pitch_words, uint32_t* out_dev, uint64_t out_pitch_words,
                                       uint64_t n_slots, uint64_t stride_words, uint64_t slot_base,
-                                      uint64_t window_stride, uint64_t max_phase, uint64_t* records_dev,
+                                      uint64_t window_stride, uint64_t max_phase, uint32_t* records_dev,
                                       uint64_t records_cap, rg_step_result* rows_dev, void* stream) {
   if (!ctx) return fail(nullptr, RG_EINVAL, "rg_phase_step_shard_windows: null context");
   if (n_windows < 1 || n_windows > 65535) return fail(ctx, RG_EINVAL, "rg_phase_step_shard_windows: 1..65535 windows");
@@ -655,7 +661,7 @@ int rg_phase_step_shard_windows_async(rg_ctx* ctx, uint32_t n_windows, const uin
 
 static int fixup_impl(rg_ctx* ctx, uint32_t n_win, uint32_t* out_dev, uint64_t out_pitch, uint64_t n_slots,
                       uint64_t stride_words, uint64_t slot_base, uint64_t id_stride, uint64_t max_phase,
-                      const uint64_t* records_dev, uint64_t records_cap, const rg_step_result* rows_dev,
+                      const uint32_t* records_dev, uint64_t records_cap, const rg_step_result* rows_dev,
                       uint32_t shard, uint32_t n_shards, rg_step_result* rows_out_dev, void* stream,
                       hipEvent_t patched = nullptr) {
   if (!ctx) return fail(nullptr, RG_EINVAL, "rg_shard_fixup: null context");
@@ -686,7 +692,7 @@ static int fixup_impl(rg_ctx* ctx, uint32_t n_win, uint32_t* out_dev, uint64_t o
     return beyond_reservation(ctx, "rg_shard_fixup");
   hipStream_t s = pick_stream(ctx, stream);
   FixParams f;
-  f.rec = reinterpret_cast<const unsigned long long*>(records_dev);
+  f.rec = records_dev;
   f.rows = reinterpret_cast<const DevResult*>(rows_dev);
   f.shard = shard;
   f.n_shards = n_shards;
@@ -702,6 +708,10 @@ static int fixup_impl(rg_ctx* ctx, uint32_t n_win, uint32_t* out_dev, uint64_t o
   f.n_win = n_win;
   f.out_pitch = out_pitch;
   f.id_stride = id_stride;
+  f.n_slots = n_slots;
+  f.n_words = n_words;
+  f.rec_tw = (uint32_t)rec_table_words(n_slots);
+  f.rec_pitch = f.rec_tw + records_cap;
   hipLaunchKernelGGL(shard_fixup_kernel, dim3(n_part, n_win), dim3(256), 0, s, f);
   // (the exchange forks the decision lists off here: the outputs are final, the rows not yet)
   if (patched) RG_HIP(ctx, hipEventRecord(patched, s));
@@ -712,7 +722,7 @@ static int fixup_impl(rg_ctx* ctx, uint32_t n_win, uint32_t* out_dev, uint64_t o
 }
 
 int rg_shard_fixup_async(rg_ctx* ctx, uint32_t* out_dev, uint64_t n_slots, uint64_t stride_words,
-                         uint64_t slot_base, uint64_t max_phase, const uint64_t* records_dev,
+                         uint64_t slot_base, uint64_t max_phase, const uint32_t* records_dev,
                          uint64_t records_cap, const rg_step_result* rows_dev, uint32_t shard,
                          uint32_t n_shards, rg_step_result* row_dev, void* stream) {
   return fixup_impl(ctx, 1, out_dev, 0, n_slots, stride_words, slot_base, n_slots, max_phase, records_dev, records_cap,
@@ -721,7 +731,7 @@ int rg_shard_fixup_async(rg_ctx* ctx, uint32_t* out_dev, uint64_t n_slots, uint6
 
 int rg_shard_fixup_fork(rg_ctx* ctx, uint32_t n_windows, uint32_t* out_dev, uint64_t out_pitch_words, uint64_t n_slots,
                         uint64_t stride_words, uint64_t slot_base, uint64_t window_stride, uint64_t max_phase,
-                        const uint64_t* records_dev, uint64_t records_cap, const rg_step_result* rows_dev,
+                        const uint32_t* records_dev, uint64_t records_cap, const rg_step_result* rows_dev,
                         uint32_t shard, uint32_t n_shards, rg_step_result* rows_out_dev, void* stream,
                         hipEvent_t patched) {
   return fixup_impl(ctx, n_windows, out_dev, out_pitch_words, n_slots, stride_words, slot_base, window_stride,
@@ -730,7 +740,7 @@ int rg_shard_fixup_fork(rg_ctx* ctx, uint32_t n_windows, uint32_t* out_dev, uint
 
 int rg_shard_fixup_windows_async(rg_ctx* ctx, uint32_t n_windows, uint32_t* out_dev, uint64_t out_pitch_words,
                                  uint64_t n_slots, uint64_t stride_words, uint64_t slot_base, uint64_t window_stride,
-                                 uint64_t max_phase, const uint64_t* records_dev, uint64_t records_cap,
+                                 uint64_t max_phase, const uint32_t* records_dev, uint64_t records_cap,
                                  const rg_step_result* rows_dev, uint32_t shard, uint32_t n_shards,
                                  rg_step_result* rows_out_dev, void* stream) {
   return fixup_impl(ctx, n_windows, out_dev, out_pitch_words, n_slots, stride_words, slot_base, window_stride,

@@ -181,7 +181,7 @@ int gather(rg_ctx* ctx, const void* send, void* recv, uint64_t bytes, hipStream_
 // folded window by window into the engine state and results_dev[K].
 int exchange_rows(rg_ctx* ctx, uint32_t n_windows, uint32_t* out_dev, uint64_t out_pitch_words, uint64_t n_slots,
                   uint64_t stride_words, uint64_t slot_base, uint64_t window_base, uint64_t window_slots,
-                  uint64_t max_phase, const uint64_t* records_dev, uint64_t records_cap, const rg_step_result* rows_dev,
+                  uint64_t max_phase, const uint32_t* records_dev, uint64_t records_cap, const rg_step_result* rows_dev,
                   rg_step_result* results_dev, uint64_t und_chk, hipStream_t s, hipEvent_t patched = nullptr) {
   RgComm* c = ctx->comm;
   const uint64_t row_bytes = (uint64_t)n_windows * sizeof(DevResult);
@@ -291,7 +291,7 @@ int rg_comm_allgather_async(rg_ctx* ctx, const void* send_dev, void* recv_dev, u
 
 int rg_shard_exchange_windows_async(rg_ctx* ctx, uint32_t n_windows, uint32_t* out_dev, uint64_t out_pitch_words,
                                     uint64_t n_slots, uint64_t stride_words, uint64_t slot_base, uint64_t window_base,
-                                    uint64_t window_slots, uint64_t max_phase, const uint64_t* records_dev,
+                                    uint64_t window_slots, uint64_t max_phase, const uint32_t* records_dev,
                                     uint64_t records_cap, const rg_step_result* rows_dev, rg_step_result* results_dev,
                                     uint32_t* bitmaps_all_dev, void* stream) {
   if (int rc = need_comm(ctx, "rg_shard_exchange_windows")) return rc;
@@ -319,7 +319,7 @@ int rg_shard_exchange_windows_async(rg_ctx* ctx, uint32_t n_windows, uint32_t* o
 int rg_shard_exchange_decisions_async(rg_ctx* ctx, uint32_t n_windows, uint32_t* out_dev, uint64_t out_pitch_words,
                                       uint64_t n_slots, uint64_t stride_words, uint64_t slot_base,
                                       uint64_t window_base, uint64_t window_slots, uint64_t max_phase,
-                                      const uint64_t* records_dev, uint64_t records_cap,
+                                      const uint32_t* records_dev, uint64_t records_cap,
                                       const rg_step_result* rows_dev, rg_step_result* results_dev,
                                       uint32_t undecided_cap, uint32_t with_v1, uint32_t* decisions_all_dev,
                                       void* stream) {

@@ -118,12 +118,24 @@ struct DevState {
   unsigned long long shard_draws;
 };
 
-// Sharded REF draw record, one per VQ slot of a shard step, indexed by the slot's
-// local draw number: slot offset (low 32 bits) | info << 32 with
+// Sharded REF draw record (4 B), one per VQ slot of a shard step, indexed by the slot's
+// local draw number: bits 0-23 the slot's offset inside its record segment (2^24 slots =
+// 2^19 words of the window), bits 24-30 info:
 //   info bits 0-1 (c1 vs c0 over R1: 0 tie, 1 c1 > c0, 2 c1 < c0),
 //   bits 2-3 decision code if the own round-2 vote is V0, bits 4-5 if it is V1,
-//   bit 6 the own vote the provisional draw gave.
+//   bit 6 the provisional own vote (the likelier outcome of the draw).
+// A window's record region (include/rabia_gpu.h rg_record_window_words) is the segment
+// table, then the records: table[s] = local draw number of segment s's first VQ slot
+// (written by the thread whose words start segment s), so segment s's records are
+// [table[s], table[s + 1]). Round 5's records were 8 B (a 32-bit window offset).
 constexpr uint32_t kRecGt = 1u, kRecLt = 2u;
+constexpr uint32_t kRecChunkShift = 24, kRecChunkWords = 1u << (kRecChunkShift - 5);  // a segment: 2^24 slots
+constexpr uint32_t kRecNone = 0xFFFFFFFFu;  // (bit 31 is 0 in every record)
+RG_HD uint64_t rec_chunks(uint64_t n_slots) { return (n_slots + (1ull << kRecChunkShift) - 1) >> kRecChunkShift; }
+RG_HD uint64_t rec_table_words(uint64_t n_slots) { return (rec_chunks(n_slots) + 1 + 3) & ~3ull; }
+RG_HD uint32_t rec_make(uint32_t off, uint32_t info) {
+  return (off & ((1u << kRecChunkShift) - 1u)) | (info << kRecChunkShift);
+}
 
 struct DevResult {  // layout-identical to rg_step_result
   unsigned long long n_slots, n_decided, n_v1, n_pending_r1, n_draws;

@@ -78,7 +78,7 @@ extern "C" int rg_shard_commit_impl(rg_ctx* ctx, uint32_t n_windows, const rg_st
 // between the re-draw kernel (the outputs final) and the finish kernel (the final rows)
 extern "C" int rg_shard_fixup_fork(rg_ctx* ctx, uint32_t n_windows, uint32_t* out_dev, uint64_t out_pitch_words,
                                    uint64_t n_slots, uint64_t stride_words, uint64_t slot_base,
-                                   uint64_t window_stride, uint64_t max_phase, const uint64_t* records_dev,
+                                   uint64_t window_stride, uint64_t max_phase, const uint32_t* records_dev,
                                    uint64_t records_cap, const rg_step_result* rows_dev, uint32_t shard,
                                    uint32_t n_shards, rg_step_result* rows_out_dev, void* stream,
                                    hipEvent_t patched);

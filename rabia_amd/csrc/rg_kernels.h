@@ -52,11 +52,13 @@ struct StepParams {
                                   //  1 skip the look-back wait, 2 skip finish_tile, 4 stamps
   unsigned long long* dbg;        // [n_tiles][8] s_memrealtime stamps when diag & 4
   uint64_t in_bytes, out_bytes;   // the plane buffers' extents
-  unsigned long long* vq_rec;     // sharded REF: draw records [vq_cap] (rg_common.h)
-  uint64_t vq_cap;
+  uint32_t* vq_rec;               // sharded REF: the window's record region (rg_common.h): chunk
+  uint64_t vq_cap;                //   table [rec_tw words], then [vq_cap] draw records
+  uint64_t rec_pitch;             //   words per window region (rg_record_window_words)
+  uint32_t rec_tw;                //   chunk-table words
   // Sharded REF over n_win windows in one launch (grid.y = window; tiled kernel): window
   // w reads votes + w * win_in_pitch, writes out + w * win_out_pitch, its shard's slot
-  // ids start at slot_base + w * win_id_stride, its records at vq_rec + w * vq_cap, its
+  // ids start at slot_base + w * win_id_stride, its record region at vq_rec + w * rec_pitch, its
   // row at result_user[w]; its look-back chain and statistics granules are its own
   // (lookback / stats + w * n_tiles tiles). n_win = 1: one window, as before.
   uint32_t n_win;
@@ -776,7 +778,7 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p_arg) {
       p.slot_base += w * p.win_id_stride;
       p.lookback += (uint64_t)w * p.n_tiles;
       p.stats += (uint64_t)w * p.n_tiles * kStatGranules;
-      p.vq_rec += w * p.vq_cap;
+      p.vq_rec += w * p.rec_pitch;
       p.result_user += w;
       if (w + 1 != p.n_win) p.result = nullptr;  // the context's result: the last window's row
     }
@@ -928,6 +930,9 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p_arg) {
   // one word at a time; only the decision masks stay live for the stores
   uint32_t dlo[W], dhi[W];
   unsigned long long kr = k_first - k_base;  // SHARD: local draw number of this thread's first VQ slot
+  if constexpr (SHARD) {  // the record segment this thread's words start: its first record
+    if ((w0 & (kRecChunkWords - 1)) == 0 && active) p.vq_rec[w0 / kRecChunkWords] = (uint32_t)kr;
+  }
 #pragma unroll
   for (int i = 0; i < W; i++) {
     const uint32_t sel = own_lo[i] & r1vq[i];  // VQ slots whose draw gave V1
@@ -945,7 +950,7 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p_arg) {
         const uint32_t cls = ((gtm >> b) & 1u) ? kRecGt : (((ltm >> b) & 1u) ? kRecLt : 0u);
         const uint32_t info = cls | (d_v0 << 2) | (d_v1 << 4) | (own << 6);
         const uint32_t off = (uint32_t)(32u * (w0 + i) + b);
-        if (kr < p.vq_cap) p.vq_rec[kr] = ((unsigned long long)info << 32) | off;
+        if (kr < p.vq_cap) p.vq_rec[p.rec_tw + kr] = rec_make(off, info);
         kr++;
       }
     }
@@ -1526,8 +1531,14 @@ __global__ __launch_bounds__(BLOCK, OCC) RG_LAG_REGS void ref_lag_kernel(StepPar
       // per VQ slot (index = local draw number, ascending slot order): offset, class,
       // the decision under each own vote, the provisional own vote. No ChaCha12 pass and
       // no barrier in the sharded step.
+      uint32_t* const vq_reg = p.vq_rec + (MW ? (uint64_t)park_l.w * p.rec_pitch : 0ull);
+      {  // the record segment this thread's words start: its first record
+        const uint32_t pw = park_l.c * kTW + (uint32_t)tid * W;
+        if ((pw & (kRecChunkWords - 1)) == 0 && pw < p.n_words)
+          vq_reg[pw / kRecChunkWords] = (uint32_t)(k_tile + park_thr - k_base);
+      }
       if (park_total) {
-        unsigned long long* const vq_rec = p.vq_rec + (MW ? (uint64_t)park_l.w * p.vq_cap : 0ull);
+        uint32_t* const vq_rec = vq_reg + p.rec_tw;
         unsigned long long k = k_tile + park_thr;
 #pragma unroll
         for (int i = 0; i < W; i++) {
@@ -1548,7 +1559,7 @@ __global__ __launch_bounds__(BLOCK, OCC) RG_LAG_REGS void ref_lag_kernel(StepPar
             const uint32_t info = cls | (d4 << 2) | ((uint32_t)x0 << 6);
             const unsigned long long kr = k - k_base;
             const uint32_t off = 32u * (park_l.c * kTW + (uint32_t)tid * W + i) + b;  // window-relative
-            if (kr < p.vq_cap) vq_rec[kr] = ((unsigned long long)info << 32) | off;
+            if (kr < p.vq_cap) vq_rec[kr] = rec_make(off, info);
             k++;
           }
         }
@@ -2035,7 +2046,7 @@ __device__ __forceinline__ void fold_partials(const unsigned long long* acc, uin
 }
 
 struct FixParams {
-  const unsigned long long* rec;  // [vq_cap] draw records of this shard's step
+  const uint32_t* rec;            // the step's record region (chunk table, then [vq_cap] records)
   const DevResult* rows;          // [n_shards] step rows of every shard, rank order
   uint32_t shard, n_shards;
   DevState* state;
@@ -2049,10 +2060,13 @@ struct FixParams {
   unsigned long long* acc;
   uint32_t n_part;
   // n_win windows (grid.y): window w's outputs at out + w * out_pitch, slot ids + w *
-  // id_stride, records + w * vq_cap; rows [n_shards][n_win] (rank-major, as an
+  // id_stride, record region + w * rec_pitch; rows [n_shards][n_win] (rank-major, as an
   // all-gather of every shard's n_win rows lays them out)
   uint32_t n_win;
   uint64_t out_pitch, id_stride;
+  uint64_t n_slots, n_words;      // per window
+  uint64_t rec_pitch;             // words per window record region
+  uint32_t rec_tw;                // chunk-table words
 };
 
 // Sum of one 64-bit value per thread over a 256-thread workgroup, returned to every
@@ -2089,8 +2103,14 @@ __device__ __forceinline__ unsigned long long fix_first_draw(const FixParams& f,
 // XOR-patches the own-vote bits that change, one atomic per changed word of its run
 // (records are in slot order: a block's changes fall in a few neighbouring words), and
 // the rare decision changes (the own vote decides the round-2 count). Every lane works
-// on a block of its own, so no lane idles on a partial pass and no LDS is needed; the
-// statistics are one partial per workgroup.
+// on a block of its own, so no lane idles on a partial pass; the statistics are one
+// partial per workgroup. Records are 4 B with segment-relative offsets (rg_common.h):
+// the workgroup stages the window's segment table in LDS and each thread finds its first
+// record's segment by binary search there, then walks forward.
+// (Round 6 also tried a fix-up that writes plane 2 whole, one workgroup per 2^15-slot
+// chunk, so the step could skip its plane-2 store: fewer bytes on paper, but its per-chunk
+// barriers kept it resident beside the whole next step kernel: 0.780 vs 0.732 ms per
+// C2 step, profiles/r06/c2_sharded_chunk_fixup_kernel_stats.csv. Not kept.)
 #ifndef RG_FIX_GRID
 #define RG_FIX_GRID 2048
 #endif
@@ -2103,17 +2123,23 @@ constexpr uint32_t kFixGrid = RG_FIX_GRID;  // fix-up workgroups at most, all wi
 // the exchange chain waited a whole step kernel (round 5: the finish kernel's 266 us).
 // So: the exchange kernels at <= 64 VGPRs (8 waves per SIMD, the hardware's maximum, is
 // the lowest budget the compiler takes), and the lag kernel at <= 224 (RG_LAG_REGS).
+constexpr uint32_t kRecSegMax = 264;  // segment-table words staged in LDS (windows < 2^32 slots)
 static __global__ __launch_bounds__(256, 8) void shard_fixup_kernel(FixParams f) {
   __shared__ unsigned long long sred[4];
+  __shared__ uint32_t s_seg[kRecSegMax];
   const uint32_t win = blockIdx.y;
   const unsigned long long n = f.rows[(uint64_t)f.shard * f.n_win + win].n_draws;
   const unsigned long long g0 = fix_first_draw(f, win, sred);  // global position of local draw 0
   if (win) {  // this window's outputs, slot ids, records
     f.out += win * f.out_pitch;
     f.slot_base += win * f.id_stride;
-    f.rec += win * f.vq_cap;
+    f.rec += win * f.rec_pitch;
   }
   const unsigned long long nn = n < f.vq_cap ? n : f.vq_cap;
+  const uint32_t n_seg = (uint32_t)rec_chunks(f.n_slots);
+  for (uint32_t i = threadIdx.x; i < n_seg; i += 256) s_seg[i] = f.rec[i];
+  __syncthreads();
+  const uint32_t* recs = f.rec + f.rec_tw;
   // per-thread statistics in 32 bits (window-relative offsets: max V1 offset + 1, min
   // undecided offset), widened for the workgroup fold
   uint32_t dec = 0, v1 = 0, mx = 0, mn = ~0u;
@@ -2126,24 +2152,41 @@ static __global__ __launch_bounds__(256, 8) void shard_fixup_kernel(FixParams f)
     const long long k0 = (long long)(b << 3) - (long long)g0;  // local index of the block's first draw
     // the block first, then the records: the ChaCha state and the 8 records are never live
     // together, so the kernel fits the 64 VGPRs it may take beside the next step's lag kernel
+    // the segment of the block's first record: the last segment whose first record <= it
+    uint32_t seg = 0;
+    {
+      const uint32_t kf = k0 > 0 ? (uint32_t)k0 : 0u;
+      uint32_t lo = 0, hi = n_seg;  // s_seg[lo] <= kf (s_seg[0] = 0)
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_seg[mid] <= kf) lo = mid; else hi = mid;
+      }
+      seg = lo;
+    }
+    uint32_t seg_end = seg + 1 < n_seg ? s_seg[seg + 1] : ~0u;  // first record of the next segment
     uint32_t x[16];
     chacha_block<12>(f.key, b, 0, x);
     uint32_t cur_w = ~0u, cur_m = 0;  // the run's word being patched and its XOR mask
     const bool whole = k0 >= 0 && (unsigned long long)k0 + 8 <= nn;  // all but the ends
 #pragma unroll
-    for (int h = 0; h < 2; h++) {  // the 8 records in two halves (register budget)
-      unsigned long long rr[4];
+    for (int h = 0; h < 4; h++) {  // the 8 records in quarters (register budget)
+      uint32_t rr[2];
 #pragma unroll
-      for (int jj = 0; jj < 4; jj++) {
-        const long long k = k0 + 4 * h + jj;
-        rr[jj] = (whole || (k >= 0 && (unsigned long long)k < nn)) ? f.rec[k] : ~0ull;
+      for (int jj = 0; jj < 2; jj++) {
+        const long long k = k0 + 2 * h + jj;
+        rr[jj] = (whole || (k >= 0 && (unsigned long long)k < nn)) ? recs[k] : kRecNone;
       }
 #pragma unroll
-      for (int jj = 0; jj < 4; jj++) {
-        const int j = 4 * h + jj;
-        const unsigned long long r = rr[jj];
-        if (r == ~0ull) continue;
-        const uint32_t off = (uint32_t)r, info = (uint32_t)(r >> 32);
+      for (int jj = 0; jj < 2; jj++) {
+        const int j = 2 * h + jj;
+        const uint32_t r = rr[jj];
+        if (r == kRecNone) continue;
+        const uint32_t kk = (uint32_t)(k0 + j);
+        while (kk >= seg_end) {  // (records ascend: the walk only moves up; rare)
+          seg++;
+          seg_end = seg + 1 < n_seg ? s_seg[seg + 1] : ~0u;
+        }
+        const uint32_t off = (seg << kRecChunkShift) | (r & ((1u << kRecChunkShift) - 1u)), info = r >> kRecChunkShift;
         const unsigned long long u = (unsigned long long)x[2 * j] | ((unsigned long long)x[2 * j + 1] << 32);
         const uint32_t cls = info & 3u;
         const uint32_t own = cls == kRecGt ? (u < kP90) : (cls == kRecLt ? (u >= kP90) : (u < kP80));

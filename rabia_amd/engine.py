@@ -52,6 +52,13 @@ class ClusterConfig:
         return len(self.all_nodes)
 
 
+def record_window_words(n_slots: int, records_cap: int) -> int:
+    """u32 words of one window's draw-record region of the sharded step (include/rabia_gpu.h
+    rg_record_window_words): the segment table (one word per 2^24 slots + 1, rounded up to
+    4), then records_cap 4-B records."""
+    return ((((n_slots + 0xFFFFFF) >> 24) + 1 + 3) & ~3) + records_cap
+
+
 def plane_stride(n_slots: int) -> int:
     return ((n_slots + 127) // 128) * 4
 
@@ -292,7 +299,8 @@ class PhaseEvaluator:
                                        slot_base, window_stride, records_ptr, records_cap, rows_ptr, max_phase=0,
                                        stream=0):
         """Stage 1 for n_windows consecutive windows of this shard in one launch (pitches
-        in 32-bit words; window w's records at records_ptr + 8 * w * records_cap, its row
+        in 32-bit words; window w's record region at records_ptr + 4 * w * record_window_words(n_slots,
+        records_cap), its row
         at rows_ptr + 80 * w)."""
         N.check(self.lib.rg_phase_step_shard_windows_async(self.ctx, n_windows, votes_ptr, votes_pitch, out_ptr,
                                                            out_pitch, n_slots, stride, slot_base, window_stride,

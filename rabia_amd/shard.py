@@ -257,7 +257,10 @@ class ShardedRefStep:
         self.shared_gpu = shared_gpu
         self.rccl = rccl
         self.cap = int(n_slots_cap)
-        self.records = torch.empty(max(self.cap, 1), dtype=torch.int64, device="cuda")
+        from .engine import record_window_words
+        # the shard's draw-record region (chunk table + 4-B records) for shards of up to cap slots
+        self.records = torch.empty(record_window_words(max(self.cap, 1), max(self.cap, 1)), dtype=torch.int32,
+                                   device="cuda")
         self.row = torch.zeros(10, dtype=torch.int64, device="cuda")
         self.fixed = torch.zeros(10, dtype=torch.int64, device="cuda")
         self.result = torch.zeros(10, dtype=torch.int64, device="cuda")

@@ -74,10 +74,10 @@ def load():
     lib.or_kv_apply_partitioned.argtypes = [ctypes.c_uint32, i, u64, u64, i, u8p, u64p, u64, u8p, u8p, u64p]
     lib.or_kv_dump.argtypes = [ctypes.c_void_p, u64p, u8p, u64p, u8p, u32p]
     lib.or_unpack_planes.argtypes = [u32p, i, u64, u64, u8p]
-    lib.or_shard_step.argtypes = [i, i, i, u64, u64, u8p, u8p, u64, u8p, u8p, u8p, u8p, u8p, u64p, u64,
+    lib.or_shard_step.argtypes = [i, i, i, u64, u64, u8p, u8p, u64, u8p, u8p, u8p, u8p, u8p, u32p, u64,
                                   ctypes.POINTER(OrResult)]
-    lib.or_shard_fixup.argtypes = [u64, u64, u64, u64, u64p, u64, u8p, u8p, u8p, u8p, ctypes.POINTER(OrResult), u64,
-                                   ctypes.POINTER(OrResult), u64p]
+    lib.or_shard_fixup.argtypes = [u64, u64, u64, u64, u64, u32p, u64, u8p, u8p, u8p, u8p, ctypes.POINTER(OrResult),
+                                   u64, ctypes.POINTER(OrResult), u64p]
     _lib = lib
     return lib
 
@@ -107,32 +107,38 @@ def ref_step(n, q, self_lane, seed, rng_base, slot_base, r1, r2, max_phase=0, lc
     return dict(zip(["r1", "r2own", "dec", "committed", "value"], outs)), res.as_dict()
 
 
+def record_window_words(S, cap):
+    """u32 words of one window's record region (include/rabia_gpu.h rg_record_window_words)."""
+    return ((((S + 0xFFFFFF) >> 24) + 1 + 3) & ~3) + cap
+
+
 def shard_step(n, q, self_lane, slot_base, r1, r2, max_phase=0, records_cap=None):
-    """Stage 1 of the sharded pipeline (or_shard_step): provisional outputs, draw records,
-    the row of the shard's non-VQ slots."""
+    """Stage 1 of the sharded pipeline (or_shard_step): provisional outputs, the record
+    region (segment table + 4-B draw records, np.uint32), the row of the shard's non-VQ slots."""
     lib = load()
     S = r1.shape[0]
     outs = [np.zeros(S, np.uint8) for _ in range(5)]
     cap = S if records_cap is None else records_cap
-    recs = np.zeros(max(cap, 1), np.uint64)
+    region = np.zeros(record_window_words(S, cap), np.uint32)
     row = OrResult()
     rc = lib.or_shard_step(n, q, self_lane, slot_base, max_phase, _p(np.ascontiguousarray(r1), u8p),
-                           _p(np.ascontiguousarray(r2), u8p), S, *[_p(o, u8p) for o in outs], _p(recs, u64p), cap,
+                           _p(np.ascontiguousarray(r2), u8p), S, *[_p(o, u8p) for o in outs], _p(region, u32p), cap,
                            ctypes.byref(row))
     assert rc == 0
-    return dict(zip(["r1", "r2own", "dec", "committed", "value"], outs)), recs[:min(row.n_draws, cap)], row.as_dict()
+    return dict(zip(["r1", "r2own", "dec", "committed", "value"], outs)), region, row.as_dict()
 
 
-def shard_fixup(seed, g0, slot_base, outs, records, row, rng_after, max_phase=0, records_cap=None):
-    """Stage 3 (or_shard_fixup): re-draw the shard's VQ slots at global positions g0 + k;
-    patches `outs` in place; returns (final row, flags)."""
+def shard_fixup(seed, g0, slot_base, outs, region, row, rng_after, max_phase=0, records_cap=None):
+    """Stage 3 (or_shard_fixup): re-draw the shard's VQ slots at global positions g0 + k
+    from its record region; patches `outs` in place; returns (final row, flags)."""
     lib = load()
+    S = len(outs["r2own"])
     rin = OrResult(**{k: int(row[k]) for k in RES_KEYS})
     rout = OrResult()
     flags = np.zeros(1, np.uint64)
-    recs = np.ascontiguousarray(records, np.uint64)
-    cap = len(recs) if records_cap is None else records_cap
-    lib.or_shard_fixup(seed, g0, slot_base, max_phase, _p(recs if recs.size else np.zeros(1, np.uint64), u64p), cap,
+    reg = np.ascontiguousarray(region, np.uint32)
+    cap = len(reg) - (record_window_words(S, 0)) if records_cap is None else records_cap
+    lib.or_shard_fixup(seed, g0, slot_base, max_phase, S, _p(reg, u32p), cap,
                        *[_p(outs[k], u8p) for k in ("r2own", "dec", "committed", "value")], ctypes.byref(rin),
                        rng_after, ctypes.byref(rout), _p(flags, u64p))
     return rout.as_dict(), int(flags[0])

@@ -16,7 +16,7 @@ def test_header_symbols_exported():
     for s in syms:
         assert hasattr(lib, s), f"librabia_gpu.so does not export {s}"
         assert s in N._SIGS, f"binding lacks a signature for {s}"
-    assert lib.rg_abi_version() == 5
+    assert lib.rg_abi_version() == 6
 
 
 def test_reservation_entry_points_error_path():
@@ -126,3 +126,15 @@ def test_tiled_layout_roundtrip(P, nw, T):
         for p_ in (0, P - 1):
             assert tiled[(w // T) * P * T + p_ * T + w % T] == planar[p_, w]
     np.testing.assert_array_equal(from_tiled(tiled, P, nw, T, stride), planar)
+
+
+def test_record_window_words_matches_host_helpers():
+    """The record-region size the library computes (rg_record_window_words, a pure function:
+    no device call) equals the Python mirror and the oracle's table size + capacity."""
+    from rabia_amd import _native as N
+    from rabia_amd.engine import record_window_words
+    import oracle_lib
+    lib = N.load()
+    for S, cap in [(1, 1), ((1 << 24) - 1, 5), (1 << 24, 0), ((1 << 24) + 1, 100), (1 << 30, 1 << 27), ((1 << 32) - 1, 7)]:
+        assert lib.rg_record_window_words(S, cap) == record_window_words(S, cap) == oracle_lib.record_window_words(S, cap)
+        assert (record_window_words(S, cap) - cap) % 4 == 0  # records start 16-B aligned

@@ -167,7 +167,7 @@ def _ref_worker(rank, world, port, q):
 @pytest.mark.parametrize("world", [2, 3])
 def test_ref_shards_one_stream_gloo(oracle, world):
     """gloo world 2 and 3, the product's shard protocol (provisional likely-outcome votes,
-    8-B draw records, re-draw at global positions, K-window commit) == one engine
+    4-B draw records with a segment table, re-draw at global positions, K-window commit) == one engine
     (oracle.ref_step) over every window of both steps: outputs, results, engine position."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -229,7 +229,7 @@ def test_shard_protocol_equals_one_engine(oracle, n, world, K, W, kind):
             sl = slice(start, start + cnt)
             outs[r][w], recs[r][w], rows[r][w] = oracle.shard_step(n, q, lane, 1 + w * W + start, r1[sl], r2[sl],
                                                                    max_phase=max_phase)
-            assert rows[r][w]["n_draws"] == len(recs[r][w])
+            assert len(recs[r][w]) == oracle.record_window_words(cnt, cnt)  # segment table + records
     n_draws = [[rows[r][w]["n_draws"] for w in range(K)] for r in range(world)]
     fixed = [[None] * K for _ in range(world)]
     for r, (start, cnt) in enumerate(parts):
@@ -261,6 +261,6 @@ def test_shard_fixup_flags_record_overflow(oracle):
     n, W = 5, 4000
     r1, r2, _ = oracle.trace(0, n, 3, 1, W)
     out, rec, row = oracle.shard_step(n, 3, 2, 1, r1, r2, records_cap=10)
-    assert row["n_draws"] > 10 and len(rec) == 10
+    assert row["n_draws"] > 10 and len(rec) == oracle.record_window_words(W, 10)
     fixed, flags = oracle.shard_fixup(42, 0, 1, out, rec, row, row["n_draws"], records_cap=10)
     assert flags == 8

@@ -18,7 +18,7 @@ import pytest
 
 from rabia_amd import _native as N
 from rabia_amd import shard
-from rabia_amd.engine import PhaseEvaluator, decode_outputs, plane_stride
+from rabia_amd.engine import PhaseEvaluator, decode_outputs, plane_stride, record_window_words
 
 pytestmark = pytest.mark.gpu
 
@@ -59,8 +59,9 @@ def run_sharded(n, world, window_sizes, votes, out, stride, seed=42, self_lane=N
         recs, plan = [], []
         for S in window_sizes:
             for r in range(world):
-                c = cap if cap is not None else max(shard.shard_range(S, world, r, align=aligned)[1], 1)
-                recs.append(torch.zeros(max(c, 1), dtype=torch.int64, device="cuda"))
+                cnt_r = max(shard.shard_range(S, world, r, align=aligned)[1], 1)
+                c = cap if cap is not None else cnt_r
+                recs.append(torch.zeros(record_window_words(cnt_r, max(c, 1)), dtype=torch.int32, device="cuda"))
         # torch fills on its own stream; the contexts' streams do not wait for it
         torch.cuda.synchronize()
         base, off = 1, 0
@@ -134,7 +135,8 @@ def run_sharded_windows(n, world, K, S, votes, out, stride, seed=42, self_lane=N
         fixed = torch.zeros((K, world, 10), dtype=torch.int64, device="cuda")
         result = torch.zeros((K, world, 10), dtype=torch.int64, device="cuda")
         parts = [shard.shard_range(S, world, r, align=128) for r in range(world)]
-        recs = [torch.zeros(K * max(cnt, 1), dtype=torch.int64, device="cuda") for _, cnt in parts]
+        recs = [torch.zeros(K * record_window_words(max(cnt, 1), max(cnt, 1)), dtype=torch.int32, device="cuda")
+                for _, cnt in parts]
         rows_r = [torch.zeros((K, 10), dtype=torch.int64, device="cuda") for _ in range(world)]
         torch.cuda.synchronize()
         for r, (start, cnt) in enumerate(parts):
@@ -169,7 +171,8 @@ def run_sharded_windows(n, world, K, S, votes, out, stride, seed=42, self_lane=N
             for r, (start, cnt) in enumerate(parts):
                 w0 = (off + start) // 32
                 ctxs[r].shard_fixup_async(out.data_ptr() + 4 * w0, cnt, stride, base + start,
-                                          recs[r].data_ptr() + 8 * w * cnt, cnt, g.data_ptr(), r, world,
+                                          recs[r].data_ptr() + 4 * w * record_window_words(cnt, cnt), cnt,
+                                          g.data_ptr(), r, world,
                                           fixed[w, r].data_ptr(), max_phase=max_phase)
             torch.cuda.synchronize()
             fg = fixed[w].contiguous()
@@ -446,7 +449,8 @@ def test_pipelined_two_streams_equals_one_engine():
     fixed = torch.zeros((steps, world, K, 10), **i64)
     g_fixed = torch.zeros((steps, world, world, K, 10), **i64)
     result = torch.zeros((steps, world, K, 10), **i64)
-    recs = [[torch.zeros(K * cnt, **i64) for _, cnt in parts] for _ in range(steps)]
+    recs = [[torch.zeros(K * record_window_words(cnt, cnt), dtype=torch.int32, device="cuda") for _, cnt in parts]
+            for _ in range(steps)]
     ctxs = [PhaseEvaluator(n, self_lane=2, seed=42) for _ in range(world)]
     comp = [torch.cuda.Stream() for _ in range(world)]
     fix = [torch.cuda.Stream() for _ in range(world)]
@@ -708,18 +712,20 @@ def test_async_calls_refuse_past_reservation():
 @pytest.mark.parametrize("n,K,S,kind,force_lag", [(5, 3, 300_032, 1, True), (9, 2, 262_144, 0, True),
                                                    (7, 1, 100_000, 2, False), (3, 2, 65_536, 1, False)])
 def test_shard_step_records_equal_oracle(oracle, n, K, S, kind, force_lag):
-    """Stage 1 itself against the oracle's restatement (or_shard_step): the device's draw
-    records (slot offset, c1-vs-c0 class, the decision under each own vote, the
-    provisional vote) and its row of the non-VQ slots, bit for bit. The lag kernel's
-    provisional vote is the likelier outcome, as the oracle's; the tiled kernel draws at
-    the provisional position instead (bit 6 then differs: the fix-up re-draws either)."""
+    """Stage 1 itself against the oracle's restatement (or_shard_step): the device's record
+    region (the segment table; per VQ slot the offset in its segment, c1-vs-c0 class, the
+    decision under each own vote, the provisional vote) and its row of the non-VQ slots,
+    bit for bit. The lag kernel's provisional vote is the likelier outcome, as the oracle's;
+    the tiled kernel draws at the provisional position instead (bit 30 then differs: the
+    fix-up re-draws either)."""
     torch = torch_cuda()
     votes, stride, total = make_votes(n, [S] * K, kind, seed=61)
     Sp = ((S + 127) // 128) * 128
     i64 = dict(dtype=torch.int64, device="cuda")
     out = torch.zeros(8 * stride, dtype=torch.int32, device="cuda")
     rows = torch.zeros((K, 10), **i64)
-    rec = torch.zeros(K * S, **i64)
+    rww = record_window_words(S, S)
+    rec = torch.zeros(K * rww, dtype=torch.int32, device="cuda")
     mp = K * S // 2
     torch.cuda.synchronize()
     with PhaseEvaluator(n, self_lane=n // 2, seed=42) as ev:
@@ -731,17 +737,20 @@ def test_shard_step_records_equal_oracle(oracle, n, K, S, kind, force_lag):
         la = ev.last_launch()
     assert la["kernel"] == ("lag" if force_lag else "tiled"), la
     got_rows = rows_of(rows)
-    recs = rec.cpu().numpy().view(np.uint64).reshape(K, S)
+    regs = rec.cpu().numpy().view(np.uint32).reshape(K, rww)
     planes = out.view(8, stride).cpu().numpy().view(np.uint32)
+    n_chunks = (S + 0xFFFFFF) >> 24
+    tw = rww - S
     for w in range(K):
         base = 1 + w * S
         r1, r2, _ = oracle.trace(kind, n, 61, base, S)
-        exp, erec, erow = oracle.shard_step(n, n // 2 + 1, n // 2, base, r1, r2, max_phase=mp)
+        exp, ereg, erow = oracle.shard_step(n, n // 2 + 1, n // 2, base, r1, r2, max_phase=mp)
         for k in ("n_slots", "n_decided", "n_v1", "n_pending_r1", "n_draws", "last_committed_max", "first_undecided"):
             assert got_rows[w][k] == erow[k], (w, k)
-        g = recs[w, :erow["n_draws"]]
-        mask = np.uint64(0xFFFFFFFFFFFFFFFF if force_lag else ~(1 << 38) & 0xFFFFFFFFFFFFFFFF)
-        np.testing.assert_array_equal(g & mask, erec.astype(np.uint64) & mask, err_msg=f"window {w} records")
+        np.testing.assert_array_equal(regs[w, :n_chunks], ereg[:n_chunks], err_msg=f"window {w} segment table")
+        nd = erow["n_draws"]
+        mask = np.uint32(0xFFFFFFFF if force_lag else ~(1 << 30) & 0xFFFFFFFF)
+        np.testing.assert_array_equal(regs[w, tw:tw + nd] & mask, ereg[tw:tw + nd] & mask, err_msg=f"window {w} records")
         if force_lag:  # the provisional outputs too
             w0 = (w * Sp) // 32
             dec = decode_outputs(planes[:, w0:w0 + (S + 31) // 32], S)
