@@ -2124,6 +2124,9 @@ constexpr uint32_t kFixGrid = RG_FIX_GRID;  // fix-up workgroups at most, all wi
 // So: the exchange kernels at <= 64 VGPRs (8 waves per SIMD, the hardware's maximum, is
 // the lowest budget the compiler takes), and the lag kernel at <= 224 (RG_LAG_REGS).
 constexpr uint32_t kRecSegMax = 264;  // segment-table words staged in LDS (windows < 2^32 slots)
+#ifndef RG_FIX_RECS
+#define RG_FIX_RECS 2
+#endif
 static __global__ __launch_bounds__(256, 8) void shard_fixup_kernel(FixParams f) {
   __shared__ unsigned long long sred[4];
   __shared__ uint32_t s_seg[kRecSegMax];
@@ -2168,17 +2171,18 @@ static __global__ __launch_bounds__(256, 8) void shard_fixup_kernel(FixParams f)
     chacha_block<12>(f.key, b, 0, x);
     uint32_t cur_w = ~0u, cur_m = 0;  // the run's word being patched and its XOR mask
     const bool whole = k0 >= 0 && (unsigned long long)k0 + 8 <= nn;  // all but the ends
+    constexpr int kFR = RG_FIX_RECS;  // records per batch (register budget)
 #pragma unroll
-    for (int h = 0; h < 4; h++) {  // the 8 records in quarters (register budget)
-      uint32_t rr[2];
+    for (int h = 0; h < 8 / kFR; h++) {
+      uint32_t rr[kFR];
 #pragma unroll
-      for (int jj = 0; jj < 2; jj++) {
-        const long long k = k0 + 2 * h + jj;
+      for (int jj = 0; jj < kFR; jj++) {
+        const long long k = k0 + kFR * h + jj;
         rr[jj] = (whole || (k >= 0 && (unsigned long long)k < nn)) ? recs[k] : kRecNone;
       }
 #pragma unroll
-      for (int jj = 0; jj < 2; jj++) {
-        const int j = 2 * h + jj;
+      for (int jj = 0; jj < kFR; jj++) {
+        const int j = kFR * h + jj;
         const uint32_t r = rr[jj];
         if (r == kRecNone) continue;
         const uint32_t kk = (uint32_t)(k0 + j);
