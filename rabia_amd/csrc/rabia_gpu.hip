@@ -1076,6 +1076,7 @@ static int cluster_run(rg_ctx* ctx, const uint32_t* states_dev, uint64_t stride_
   if (stride_words < (n_slots + 31) / 32) return fail(ctx, RG_EINVAL, "rg_wmvc_cluster: stride too small");
   if (max_phases < 1 || max_phases > 255) return fail(ctx, RG_EINVAL, "rg_wmvc_cluster: max_phases must be 1..255");
   if (slot_base + n_slots > (1ull << 49)) return fail(ctx, RG_EINVAL, "rg_wmvc_cluster: slot ids must be < 2^49");
+  if (n_slots >= (1ull << 32)) return fail(ctx, RG_EINVAL, "rg_wmvc_cluster: n_slots must be < 2^32 per call");
   RG_HIP(ctx, hipSetDevice(ctx->cfg.device));
   // one slot per lane to start with, at most 2048 workgroups, unless that leaves a
   // workgroup more than kClusterChunk slots (its initial states are staged in LDS)

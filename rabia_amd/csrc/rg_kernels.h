@@ -3403,6 +3403,11 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
   bool active = false;
   uint64_t s = 0, id = 0;
   uint32_t s32 = 0, st = 0, decided = 0, decv = 0, p = 0, first = 0, coins = 0;
+  // 32-bit running offsets (n_slots < 2^32, so the coin table has < 2^30 words): the coin
+  // word of the current phase, the slot's phase-1 coin word, the phase's key row in s_ck
+  // (one add per phase instead of 64-bit address arithmetic and a multiply)
+  const uint32_t nw32 = (uint32_t)n_words;
+  uint32_t c_off = 0, c_w1 = 0, k_off = 0;
   for (;;) {
     const unsigned long long idle = __ballot(!active);
     if (idle) {
@@ -3423,6 +3428,8 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
 #pragma unroll
           for (int r = 0; r < N; r++) st |= ((s_st[r][wl] >> (s & 31)) & 1u) << r;
           decided = decv = first = coins = 0;
+          c_w1 = c_off = (uint32_t)(s >> 5);
+          k_off = 0;
           p = 1;
           active = true;
         }
@@ -3436,13 +3443,13 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
     // in flight, so the compiler put a vmcnt(0) wait at the top of every phase, which also
     // waited for the previous phase's info store; phase 1's row stands in for later phases)
     const bool coin_tabbed = p <= coin_phases;
-    const uint32_t coin_w = coin_tab[(coin_tabbed ? (uint64_t)(p - 1) * n_words : 0ull) + s / 32];
+    const uint32_t coin_w = coin_tab[coin_tabbed ? c_off : c_w1];
     uint32_t ck[2][N];
     if (p <= kKeyPhases) {
 #pragma unroll
       for (int rd = 0; rd < 2; rd++)
 #pragma unroll
-        for (int r = 0; r < N; r++) ck[rd][r] = s_ck[p - 1][rd][r];
+        for (int r = 0; r < N; r++) ck[rd][r] = (&s_ck[0][0][0])[k_off + rd * N + r];
     } else {
 #pragma unroll
       for (int rd = 0; rd < 2; rd++)
@@ -3459,8 +3466,18 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
       for (int rd = 0; rd < 2; rd++)
 #pragma unroll
         for (int r = 0; r < N; r++) {
-          const uint32_t h = fmix32(ck[rd][r] ^ s32);
-          ph[rd] |= s_raw[((uint32_t)r << Raw::nb) + ((h >> Raw::lo) & ((1u << Raw::nb) - 1u))];
+          // fmix32 without its last step: h = x ^ (x >> 16), and only h's bits [lo, lo + nb)
+          // are read, so the byte offset of the table entry is taken from x directly
+          uint32_t x = ck[rd][r] ^ s32;
+          x ^= x >> 16;
+          x *= 0x85EBCA6Bu;
+          x ^= x >> 13;
+          x *= 0xC2B2AE35u;
+          uint32_t a = 0;
+          if constexpr (Raw::nb > 0)
+            a = ((x >> (Raw::lo - 2)) ^ (x >> (Raw::lo + 14))) & (((1u << Raw::nb) - 1u) << 2);
+          ph[rd] |= *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(s_raw) +
+                                                       ((uint32_t)r << (Raw::nb + 2)) + a);
         }
       // round 1: v1 = all heard voted 1, vq = heard both values
       const uint32_t rs = __umul24(st, rep);
@@ -3534,7 +3551,7 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
     if (all || p >= max_phases) {
       const uint32_t phases = all ? p : 0u;
       const uint32_t dec = all ? ((decv == 0 || decv == kAll) ? (decv & 1u) : kCodeVQ) : kCodeNone;
-      info[s] = dec | (phases << 8) | (first << 16) | (coins << 24);
+      info[(uint32_t)s] = dec | (phases << 8) | (first << 16) | (coins << 24);
       if (bm_dec && dec <= kCodeV1) {
         const uint32_t wl = (uint32_t)(s / 32 - w0), bit = 1u << (s & 31);
         atomicOr(&s_bd[wl], bit);
@@ -3550,6 +3567,8 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
       active = false;
     } else {
       p++;
+      c_off += nw32;
+      k_off += 2 * N;
     }
   }
   __shared__ unsigned long long red[4][kClusterStats];
