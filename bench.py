@@ -112,6 +112,9 @@ def parse():
     ap.add_argument("--sets", type=int, default=3)
     ap.add_argument("--launch-events", action="store_true",
                     help="an event pair around every timed launch (costs the stream 6-10 us per step)")
+    ap.add_argument("--launch-sample", type=int, default=16,
+                    help="sharded pipeline: an event pair around every n-th timed step kernel (its kernel "
+                         "time; each pair costs the stream 6-10 us)")
     ap.add_argument("--tile-words", type=int, default=1024,
                     help="slot-tiled plane layout (include/rabia_gpu.h); 0 = planar")
     ap.add_argument("--cpu-threads", type=int, default=0,
@@ -636,7 +639,7 @@ def run_sharded(a, n, S, window_slots, world, rank, dist, comm, bitmaps):
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
-    evs = launch_events(a, every=4)  # the step kernel alone, sampled: the step time holds the exchange too
+    evs = launch_events(a, every=max(1, a.launch_sample))  # the step kernel alone, sampled (the step time holds the exchange too)
     t_begin, t_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t_begin.record(comp)
     host_wait[0] = 0.0
