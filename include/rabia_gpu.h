@@ -231,8 +231,9 @@ int rg_phase_step_shard_async(rg_ctx* ctx, const uint32_t* votes_dev, uint32_t* 
  * votes_pitch_words / out_dev + w * out_pitch_words (each a buffer in the context
  * layout, stride_words as for one window), its record region at records_dev + w *
  * rg_record_window_words(n_slots, records_cap), its row at rows_dev[w] (required).
- * Equivalent to n_windows calls of rg_phase_step_shard_async in window order, except that every window takes its
- * provisional draws from the same position and shard_draws does not advance (the
+ * Equivalent to n_windows calls of rg_phase_step_shard_async in window order, except
+ * that every window takes its provisional draws from the same position and
+ * shard_draws does not advance (the
  * fix-up re-draws every VQ slot at its global position, so the fixed outputs, rows
  * and engine state are the same). Stages (2)-(4) then run per window as above, with
  * that window's out buffer, records and rows. The context's last result is the last
