@@ -12,6 +12,8 @@
 // same pass by a decoupled look-back over tiles in blockIdx order.
 #pragma once
 
+#include <type_traits>
+
 #include "rg_common.h"
 
 namespace rg {
@@ -3350,9 +3352,10 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
   constexpr uint32_t kAll = (1u << N) - 1u;
   constexpr uint32_t kKeyPhases = 32;  // cluster_key table: phases 1..32 (later phases compute theirs)
   constexpr uint32_t kStageWords = kClusterChunk / 32 + 1;
-  __shared__ unsigned long long s_next;
+  __shared__ uint32_t s_next;  // the chunk's next slot (n_slots < 2^32)
   __shared__ uint32_t s_ck[kKeyPhases][2][N];
-  __shared__ uint32_t s_st[N][kStageWords];  // the chunk's initial-state words
+  using StT = typename std::conditional<(N <= 8), uint8_t, uint16_t>::type;
+  __shared__ StT s_stb[kClusterChunk];  // the chunk's initial states, N bits per slot
   __shared__ uint32_t s_bd[kStageWords], s_b1[kStageWords];  // the chunk's decided / V1 bitmap words
   constexpr uint32_t kTabCap = heard_tab_size<N>((uint32_t)N / 2 + 1) ? heard_tab_size<N>((uint32_t)N / 2 + 1) : 1;
   __shared__ uint16_t s_heard[kTabCap];     // heard sets at the majority quorum (heard_mask_tab)
@@ -3364,7 +3367,7 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
   const uint64_t c0 = (uint64_t)blockIdx.x * chunk;
   const uint64_t c1 = c0 + chunk < n_slots ? c0 + chunk : n_slots;
   const uint64_t w0 = c0 / 32;
-  if (threadIdx.x == 0) s_next = c0;
+  if (threadIdx.x == 0) s_next = (uint32_t)c0;
   for (uint32_t e = threadIdx.x; e < kKeyPhases * 2 * N; e += blockDim.x) {
     const uint32_t ph = e / (2 * N), rd = (e / N) % 2, rr = e % N;
     s_ck[ph][rd][rr] = (uint32_t)cluster_key(dseed, ph + 1, rd + 1, (int)rr);
@@ -3391,9 +3394,26 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
     for (uint32_t e = threadIdx.x; e < tab_n; e += blockDim.x) s_heard[e] = (uint16_t)heard_tab_entry<N>(e, q);
   }
   const uint32_t nw = c1 > c0 ? (uint32_t)((c1 - 1) / 32 - w0 + 1) : 0u;  // <= kStageWords (chunk <= kClusterChunk)
-  for (uint32_t e = threadIdx.x; e < N * nw; e += blockDim.x) {
-    const uint32_t r = e / nw, w = e % nw;
-    s_st[r][w] = states[(uint64_t)r * stride + w0 + w];
+  // the state words transposed to one element per slot (a refill reads one byte / short
+  // instead of N words and N bit extractions); the host makes c0 a multiple of 32, so
+  // slot c0 + i is element i
+  for (uint32_t w = threadIdx.x; w < nw; w += blockDim.x) {
+    uint32_t x[N];
+#pragma unroll
+    for (int r = 0; r < N; r++) x[r] = states[(uint64_t)r * stride + w0 + w];
+    constexpr int kPer = 4 / (int)sizeof(StT);  // slots per 32-bit store
+#pragma unroll
+    for (int q4 = 0; q4 < 32 / kPer; q4++) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int j = 0; j < kPer; j++) {
+        uint32_t e = 0;
+#pragma unroll
+        for (int r = 0; r < N; r++) e |= ((x[r] >> (kPer * q4 + j)) & 1u) << r;
+        v |= e << (8 * (int)sizeof(StT) * j);
+      }
+      if (32 * w + kPer * q4 < kClusterChunk) reinterpret_cast<uint32_t*>(s_stb)[(32 / kPer) * w + q4] = v;
+    }
   }
   if (bm_dec)
     for (uint32_t w = threadIdx.x; w < nw; w += blockDim.x) s_bd[w] = s_b1[w] = 0;
@@ -3401,7 +3421,8 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
   const int lane = threadIdx.x & 63;
   uint32_t acc[kClusterStats] = {0, 0, 0, 0, 0, 0, 0, 0};  // per lane: <= chunk slots, sums < 2^32
   bool active = false;
-  uint64_t s = 0, id = 0;
+  uint32_t s = 0;  // the lane's slot (window-relative)
+  uint64_t id = 0;
   uint32_t s32 = 0, st = 0, decided = 0, decv = 0, p = 0, first = 0, coins = 0;
   // 32-bit running offsets (n_slots < 2^32, so the coin table has < 2^30 words): the coin
   // word of the current phase, the slot's phase-1 coin word, the phase's key row in s_ck
@@ -3413,22 +3434,19 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
     if (idle) {
       const uint32_t cnt = (uint32_t)__builtin_popcountll(idle);
       const int leader = __builtin_ctzll(idle);
-      unsigned long long base = 0;
-      if (lane == leader) base = atomicAdd(&s_next, (unsigned long long)cnt);
+      uint32_t base = 0;
+      if (lane == leader) base = atomicAdd(&s_next, cnt);
       base = __shfl(base, leader, 64);
       if (!active) {
         const uint32_t rank = (uint32_t)__builtin_popcountll(idle & ((1ull << lane) - 1ull));
-        const uint64_t ns = base + rank;
-        if (ns < c1) {
+        const uint32_t ns = base + rank;
+        if (ns < (uint32_t)c1) {
           s = ns;
           id = slot_base + s;
           s32 = slot_fold32(id);
-          st = 0;
-          const uint32_t wl = (uint32_t)(s / 32 - w0);
-#pragma unroll
-          for (int r = 0; r < N; r++) st |= ((s_st[r][wl] >> (s & 31)) & 1u) << r;
+          st = s_stb[s - (uint32_t)c0];
           decided = decv = first = coins = 0;
-          c_w1 = c_off = (uint32_t)(s >> 5);
+          c_w1 = c_off = s >> 5;
           k_off = 0;
           p = 1;
           active = true;
@@ -3551,9 +3569,9 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
     if (all || p >= max_phases) {
       const uint32_t phases = all ? p : 0u;
       const uint32_t dec = all ? ((decv == 0 || decv == kAll) ? (decv & 1u) : kCodeVQ) : kCodeNone;
-      info[(uint32_t)s] = dec | (phases << 8) | (first << 16) | (coins << 24);
+      info[s] = dec | (phases << 8) | (first << 16) | (coins << 24);
       if (bm_dec && dec <= kCodeV1) {
-        const uint32_t wl = (uint32_t)(s / 32 - w0), bit = 1u << (s & 31);
+        const uint32_t wl = s / 32 - (uint32_t)w0, bit = 1u << (s & 31);
         atomicOr(&s_bd[wl], bit);
         if (dec == kCodeV1) atomicOr(&s_b1[wl], bit);
       }
