@@ -656,7 +656,11 @@ __device__ __forceinline__ void lds_wave_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-__global__ __launch_bounds__(kBlock) void kv_plan_kernel(BatchView b, StoreView st) {
+// Waves per SIMD the plan is compiled for (its VGPR budget; LDS allows 10).
+#ifndef RG_KV_PLAN_WAVES
+#define RG_KV_PLAN_WAVES 5  // 4 (103 VGPRs): apply 545.2 / 546.0 us, 5 (83, no spill): 538.7 / 538.6, 6 (80 + spills): 545.1 / 544.4 (profiles/r06/c4_plan_occ_ab.json)
+#endif
+__global__ __launch_bounds__(kBlock, RG_KV_PLAN_WAVES) void kv_plan_kernel(BatchView b, StoreView st) {
   __shared__ uint32_t s_c[kWalkBlockSpan];
   __shared__ uint8_t s_inf[kWalkBlockSpan];
   __shared__ uint16_t s_heads[kBlock / 64][kWalkSpan];
@@ -845,7 +849,10 @@ __device__ void refuse_key(const BatchView& b, uint64_t i, const KeyRec& r, bool
 // replay (one thread); mode 2, the refusal (every pending command gets
 // RG_KV_E_CAPACITY, grid-stride). Mode 3 is mode 0 with the keys whose create is
 // refused left out (refuse_key).
-__global__ __launch_bounds__(kBlock) void kv_commit_kernel(BatchView b, StoreView st) {
+#ifndef RG_KV_COMMIT_WAVES
+#define RG_KV_COMMIT_WAVES 5  // 86 VGPRs; 6 (80 + spills): no gain (539.9 / 541.0 us with the plan at 5)
+#endif
+__global__ __launch_bounds__(kBlock, RG_KV_COMMIT_WAVES) void kv_commit_kernel(BatchView b, StoreView st) {
   __shared__ uint16_t s_heads[kBlock / 64][kWalkSpan];
   __shared__ unsigned long long s_wsum[kBlock / 64];
   const unsigned long long mode = st.ctr->mode;  // uniform over the grid
