@@ -53,16 +53,17 @@ def bytes_per_slot_ref(n: int) -> float:
     return (4 * n + 8) / 8.0
 
 
-C3_COIN_TABLE_PHASES = 8  # rabia_gpu.hip cluster_run: kCoinTablePhases (RG_COIN_TABLE_PHASES)
+C3_COIN_TABLE_PHASES = 8  # rabia_gpu.hip cluster_run: kCoinTablePhases (RG_COIN_TABLE_PHASES), held in LDS per workgroup
 
 
 def c3_bytes_per_slot(n: int, mean_phases: float) -> float:
     """Bytes per slot of the call the C3 step makes, rg_wmvc_cluster_bitmaps_async (the
     decided / V1 bitmaps built inside the cluster kernel, no second pass over the info
-    words): n initial-state bits read, the u32 info word written, 2 bitmap bits written,
-    the coin table's bits written (one per slot per table phase) and read (about one per
-    phase the slot runs)."""
-    return n / 8 + 4 + 2 / 8 + C3_COIN_TABLE_PHASES / 8 + mean_phases / 8
+    words): n initial-state bits read, the u32 info word written, 2 bitmap bits written.
+    The common-coin bits of the first C3_COIN_TABLE_PHASES phases are computed into LDS by
+    each workgroup (round 6; before, a coin-table launch wrote them to HBM and the kernel
+    read them back), so they move no HBM bytes."""
+    return n / 8 + 4 + 2 / 8
 
 
 # SQ_INSTS_VALU / (512 x GRBM_GUI_ACTIVE / 8) that independent v_xor_b32 / v_add_u32 chains reach
@@ -91,7 +92,7 @@ def c3_roofline(r, bytes_slot):
                    counter_file="profiles/pmc_c3.json", measured_int_issue_ceiling=C3_INT_ISSUE_CEILING,
                    frac_of_measured_ceiling=pmc["valu_issue_util"] / C3_INT_ISSUE_CEILING,
                    note="achieved = the cluster kernel's VALU wave-instructions over the rg_wmvc_cluster_bitmaps_async call's "
-                        "time (coin table + cluster kernel with the bitmaps + statistics fold: a lower bound for the kernel); "
+                        "time (cluster kernel with its LDS coin table and the bitmaps + statistics fold: a lower bound for the kernel); "
                         "counter_issue_util = SQ_INSTS_VALU / (512 x GRBM_GUI_ACTIVE/8 cycles) of the cluster kernel "
                         "alone, at the clock the chip actually ran (DVFS); mix_per_slot in the counter file; "
                         "measured_int_issue_ceiling = the same ratio for independent 32-bit integer ALU chains at 8 waves "
@@ -748,7 +749,7 @@ def run_c3(a, world, rank, dist, comm):
         step(t)
     torch.cuda.synchronize()
     barrier()
-    # the cluster call (coin table, cluster kernel with the bitmaps, statistics fold): at world 1
+    # the cluster call (cluster kernel with the bitmaps, statistics fold): at world 1
     # it is the whole step (span / K); with the all-gathers in the step, every 2nd call bracketed
     evs = launch_events(a, every=2 if world > 1 else 0)
     t_begin, t_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -125,20 +125,20 @@ struct Disp {
   }
   static void cluster_lc(uint32_t grid, hipStream_t s, const uint32_t* st, uint64_t stride, uint64_t n_slots,
                          uint64_t base, uint32_t q, uint32_t fp1, Key key, uint64_t cs, uint64_t dseed,
-                         uint32_t maxp, uint32_t* info, unsigned long long* part, const uint32_t* coins,
-                         uint32_t coin_phases, uint64_t chunk, uint32_t* bm_dec, uint32_t* bm_v1) {
+                         uint32_t maxp, uint32_t* info, unsigned long long* part, uint32_t coin_phases,
+                         uint64_t chunk, uint32_t* bm_dec, uint32_t* bm_v1) {
     constexpr bool kPackable = N <= 5 && N % 2 == 1;  // N fields of N bits; q = fp1 = N / 2 + 1 by default
     if (kPackable && q == (uint32_t)(N / 2 + 1) && fp1 == q) {  // subset tests instead of popcounts
       if constexpr (kPackable)
         hipLaunchKernelGGL((wmvc_cluster_lc_kernel<N, N / 2 + 1, true>), dim3(grid), dim3(256), 0, s, st, stride,
-                           n_slots, base, q, fp1, key, cs, dseed, maxp, info, part, coins, coin_phases, chunk, bm_dec,
+                           n_slots, base, q, fp1, key, cs, dseed, maxp, info, part, coin_phases, chunk, bm_dec,
                            bm_v1);
     } else if (q == (uint32_t)(N / 2 + 1))  // the majority quorum: the straight-line instantiation
       hipLaunchKernelGGL((wmvc_cluster_lc_kernel<N, N / 2 + 1>), dim3(grid), dim3(256), 0, s, st, stride, n_slots,
-                         base, q, fp1, key, cs, dseed, maxp, info, part, coins, coin_phases, chunk, bm_dec, bm_v1);
+                         base, q, fp1, key, cs, dseed, maxp, info, part, coin_phases, chunk, bm_dec, bm_v1);
     else
       hipLaunchKernelGGL((wmvc_cluster_lc_kernel<N, 0>), dim3(grid), dim3(256), 0, s, st, stride, n_slots, base, q,
-                         fp1, key, cs, dseed, maxp, info, part, coins, coin_phases, chunk, bm_dec, bm_v1);
+                         fp1, key, cs, dseed, maxp, info, part, coin_phases, chunk, bm_dec, bm_v1);
   }
 };
 
@@ -158,7 +158,7 @@ const StepLaunch kWmvcLaunch[17] = RG_TABLE(wmvc);
 const DigestLaunch kDigestLaunch[17] = RG_TABLE(digest);
 using ClusterLcLaunch = void (*)(uint32_t, hipStream_t, const uint32_t*, uint64_t, uint64_t, uint64_t, uint32_t,
                                  uint32_t, Key, uint64_t, uint64_t, uint32_t, uint32_t*, unsigned long long*,
-                                 const uint32_t*, uint32_t, uint64_t, uint32_t*, uint32_t*);
+                                 uint32_t, uint64_t, uint32_t*, uint32_t*);
 const ClusterLcLaunch kClusterLcLaunch[17] = RG_TABLE(cluster_lc);
 
 hipStream_t pick_stream(rg_ctx* ctx, void* stream) {
@@ -410,7 +410,6 @@ int rg_destroy(rg_ctx* ctx) {
   (void)hipFree(ctx->r1v_cells);
   (void)hipFree(ctx->r1v_blocks);
   (void)hipFree(ctx->r1v_base);
-  (void)hipFree(ctx->cluster_coins);
   (void)hipFree(ctx->cluster_part);
   (void)hipFree(ctx->cluster_stats);
   (void)hipFree(ctx->fix_acc);
@@ -1096,32 +1095,20 @@ static int cluster_run(rg_ctx* ctx, const uint32_t* states_dev, uint64_t stride_
   }
   if (!ctx->cluster_stats) RG_HIP(ctx, hipMalloc(&ctx->cluster_stats, kClusterStats * 8));
   hipStream_t s = pick_stream(ctx, stream);
-  // coin bits of the first phases precomputed (one ChaCha12 block per 512 slots and
-  // phase instead of one per lane and phase); later phases (rare) compute inline
+  // coin bits of the first phases from per-workgroup LDS tables (one ChaCha12 block per
+  // 512 slots and phase instead of one per lane and phase); later phases (rare) compute inline
 #ifndef RG_COIN_TABLE_PHASES
 #define RG_COIN_TABLE_PHASES 8
 #endif
-  constexpr uint32_t kCoinTablePhases = RG_COIN_TABLE_PHASES;  // 16: 0.498 ms per C3 step, 8: 0.465-0.468, 4: 0.475-0.478 (profiles/r05/c3_ab.json)
+  static_assert(RG_COIN_TABLE_PHASES <= kClusterCoinPhases, "the cluster kernel's LDS coin table holds kClusterCoinPhases");
+  constexpr uint32_t kCoinTablePhases = RG_COIN_TABLE_PHASES;
   const uint32_t coin_phases = max_phases < kCoinTablePhases ? max_phases : kCoinTablePhases;
-  const uint64_t n_words = (n_slots + 31) / 32;
-  if (coin_phases * n_words > ctx->cluster_coins_cap) {
-    RG_HIP(ctx, hipDeviceSynchronize());
-    (void)hipFree(ctx->cluster_coins);
-    ctx->cluster_coins = nullptr;
-    ctx->cluster_coins_cap = 0;
-    RG_HIP(ctx, hipMalloc(&ctx->cluster_coins, coin_phases * n_words * 4));
-    ctx->cluster_coins_cap = coin_phases * n_words;
-  }
-  const uint64_t coin_wgs = ((n_words + 15) / 16 + kCoinGroupsPerWg - 1) / kCoinGroupsPerWg;
-  hipLaunchKernelGGL(coin_table_kernel, dim3((uint32_t)coin_wgs, coin_phases), dim3(kCoinBlock), 0, s, ctx->coin_key,
-                     ctx->coin_stream, slot_base, n_slots, coin_phases, ctx->cluster_coins);
   // whole bitmap words per workgroup (<= kClusterChunk still: grid >= n_slots / kClusterChunk
   // and kClusterChunk is a multiple of 32); trailing workgroups may get an empty chunk
   const uint64_t chunk = ((n_slots + grid - 1) / grid + 31) / 32 * 32;
   kClusterLcLaunch[ctx->cfg.n_replicas](grid, s, states_dev, stride_words, n_slots, slot_base, ctx->q, ctx->fp1,
                                         ctx->coin_key, ctx->coin_stream, delivery_seed, max_phases, info_dev,
-                                        ctx->cluster_part, ctx->cluster_coins, coin_phases, chunk, decided_dev,
-                                        v1_dev);
+                                        ctx->cluster_part, coin_phases, chunk, decided_dev, v1_dev);
   unsigned long long* dst = stats_dev ? reinterpret_cast<unsigned long long*>(stats_dev) : ctx->cluster_stats;
   hipLaunchKernelGGL(cluster_stats_kernel, dim3(1), dim3(kStatsBlock), 0, s, ctx->cluster_part, grid, dst);
   RG_HIP(ctx, hipGetLastError());

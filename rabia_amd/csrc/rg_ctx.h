@@ -36,8 +36,6 @@ struct rg_ctx {
   uint32_t* r1v_blocks = nullptr;  // per-block draw counts / offsets
   uint64_t r1v_blocks_cap = 0;
   unsigned long long* r1v_base = nullptr;
-  uint32_t* cluster_coins = nullptr;            // [phases][n_words] common-coin table
-  uint64_t cluster_coins_cap = 0;               // words
   unsigned long long* cluster_part = nullptr;  // [blocks][kClusterStats]
   uint64_t cluster_part_cap = 0;                // blocks
   unsigned long long* cluster_stats = nullptr;  // [kClusterStats]

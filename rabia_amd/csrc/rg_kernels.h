@@ -3227,50 +3227,19 @@ __device__ __forceinline__ uint32_t heard_mask_tab(const uint16_t* tab, uint32_t
 
 constexpr int kClusterStats = 8;  // all_decided, v1, sum_phases, max_phases, sum_coin_phases, sum_first, slots, -
 
-// Common-coin table for the cluster kernel: coin bits of phases 1..P for the
-// window's slots, [P][n_words] (the same bits as coin_kernel). A 512-slot group's 16
-// words start sh = slot_base mod 512 bits into one ChaCha12 block and end in the next,
-// the same sh for every group. One workgroup per (phase, 255 groups): each thread
-// computes ONE block into LDS (256 blocks: the 255 groups' and the one after), then
-// the workgroup writes the 255 x 16 words coalesced, each a funnel shift of two LDS
-// words. 8 phases of 2^24 slots: 13.5 µs (one lane quad per block, chacha_block_quad
-// in 1,024-thread workgroups: 15.3 µs); 30 µs with one thread per group computing both
-// of its blocks (2x the ChaCha work, and a run-time register select that put them in
-// scratch memory).
-constexpr uint32_t kCoinBlock = 256;  // one ChaCha block per thread
-constexpr uint32_t kCoinGroupsPerWg = kCoinBlock - 1;
-static __global__ __launch_bounds__(kCoinBlock) void coin_table_kernel(Key key, uint64_t stream, uint64_t slot_base,
-                                                                       uint64_t n_slots, uint32_t phases,
-                                                                       uint32_t* tab) {
-  __shared__ uint32_t s_blk[kCoinBlock][17];  // +1: conflict-free column reads
-  const uint64_t n_words = (n_slots + 31) / 32, n_groups = (n_words + 15) / 16;
-  const uint64_t phase = blockIdx.y + 1, g0 = (uint64_t)blockIdx.x * kCoinGroupsPerWg;
-  const uint32_t sh = (uint32_t)(slot_base & 511u), ws = sh >> 5, bo = sh & 31u;  // grid-uniform
-  const uint64_t blk0 = (slot_base >> 9) + g0;  // the first group's first block
-  const uint32_t t = threadIdx.x;
-  {
-    uint32_t b[16];
-    chacha_block<12>(key, ((phase - 1) << 40) | (blk0 + t), stream, b);
-#pragma unroll
-    for (int k = 0; k < 16; k++) s_blk[t][k] = b[k];
-  }
-  __syncthreads();
-  const uint64_t wbase = g0 * 16, row = (phase - 1) * n_words;
-  const uint64_t ng = n_groups - g0 < kCoinGroupsPerWg ? n_groups - g0 : kCoinGroupsPerWg;
-  const uint32_t nw = (uint32_t)(wbase + ng * 16 <= n_words ? ng * 16 : n_words - wbase);
-  for (uint32_t w = t; w < nw; w += kCoinBlock) {
-    // bits [sh + 32k, sh + 32k + 32) of the group's two blocks
-    const uint32_t gl = w >> 4, i = ws + (w & 15u);  // i + 1 <= 31
-    const uint32_t lo = i < 16 ? s_blk[gl][i] : s_blk[gl + 1][i - 16];
-    const uint32_t hi = i + 1 < 16 ? s_blk[gl][i + 1] : s_blk[gl + 1][i - 15];
-    tab[row + wbase + w] = __builtin_amdgcn_alignbit(hi, lo, bo) & valid_mask(wbase + w, n_words, n_slots);
-  }
-}
+// Common-coin table of the cluster kernel: each workgroup computes the ChaCha12 blocks
+// of phases 1..P that its chunk's slots read (one block per 512 slots and phase: at most
+// kClusterChunk / 512 + 1 blocks per phase) into LDS in its prologue, so the coins of
+// those phases are LDS reads (later phases, rare, compute theirs inline). Round 6: this
+// replaced coin_table_kernel, a launch ahead of the cluster kernel that wrote the table
+// ([P][n_words]) to global memory (14 µs at 8 phases x 2^24 slots, four times its ChaCha
+// issue time; the in-kernel blocks add ~4 µs of issue to a VALU-bound kernel).
+constexpr uint32_t kClusterCoinPhases = 8;  // 16: 0.498 ms per C3 step, 8: 0.465-0.468, 4: 0.475-0.478 (profiles/r05/c3_ab.json)
 
 // Lane-compacted cluster kernel: each workgroup owns a contiguous chunk of slots;
 // a lane whose slot terminated takes the next slot of the chunk (wave-aggregated
 // LDS counter), so a wave never idles on its slowest slot (phases per slot vary
-// 1..max). Coins come from coin_table_kernel for phases <= coin_phases. The chunk's
+// 1..max). Coins of phases <= coin_phases come from the chunk's LDS table. The chunk's
 // initial-state words are staged in LDS first (<= kClusterChunk slots: the host sizes
 // the grid for it), so a refill reads LDS instead of waiting on global loads.
 // bm_dec / bm_v1 (both or neither): the decided / V1 bitmaps of the run, built in LDS
@@ -3341,13 +3310,13 @@ static_assert(packed_compress_exact<1>() && packed_compress_exact<3>() && packed
               "packed_compress gathers every flag pattern");
 
 constexpr uint32_t kClusterChunk = 8192;
+constexpr uint32_t kClusterCoinBlocks = kClusterChunk / 512 + 1;  // blocks a chunk's slots span, per phase
 template <int N, int Q, bool PK = false>
 __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* states, uint64_t stride,
                                                               uint64_t n_slots, uint64_t slot_base, uint32_t q_rt,
                                                               uint32_t fp1, Key ckey, uint64_t coin_stream,
                                                               uint64_t dseed, uint32_t max_phases, uint32_t* info,
-                                                              unsigned long long* partials, const uint32_t* coin_tab,
-                                                              uint32_t coin_phases, uint64_t chunk, uint32_t* bm_dec,
+                                                              unsigned long long* partials, uint32_t coin_phases, uint64_t chunk, uint32_t* bm_dec,
                                                               uint32_t* bm_v1) {
   constexpr uint32_t kAll = (1u << N) - 1u;
   constexpr uint32_t kKeyPhases = 32;  // cluster_key table: phases 1..32 (later phases compute theirs)
@@ -3360,10 +3329,10 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
   constexpr uint32_t kTabCap = heard_tab_size<N>((uint32_t)N / 2 + 1) ? heard_tab_size<N>((uint32_t)N / 2 + 1) : 1;
   __shared__ uint16_t s_heard[kTabCap];     // heard sets at the majority quorum (heard_mask_tab)
   __shared__ uint32_t s_raw[PK ? ClusterRaw<N, (Q ? Q : 1)>::size : 1];  // PK: raw-bits heard table, pre-shifted
+  __shared__ uint32_t s_coin[kClusterCoinPhases * kClusterCoinBlocks * 16];  // coin blocks [phase][block][word]
   const uint32_t q = Q ? (uint32_t)Q : q_rt;
   const uint32_t tab_n = heard_tab_size<N>(q);
   const bool use_tab = tab_n != 0 && tab_n <= kTabCap;  // (uniform; a constant when Q is)
-  const uint64_t n_words = (n_slots + 31) / 32;
   const uint64_t c0 = (uint64_t)blockIdx.x * chunk;
   const uint64_t c1 = c0 + chunk < n_slots ? c0 + chunk : n_slots;
   const uint64_t w0 = c0 / 32;
@@ -3394,6 +3363,22 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
     for (uint32_t e = threadIdx.x; e < tab_n; e += blockDim.x) s_heard[e] = (uint16_t)heard_tab_entry<N>(e, q);
   }
   const uint32_t nw = c1 > c0 ? (uint32_t)((c1 - 1) / 32 - w0 + 1) : 0u;  // <= kStageWords (chunk <= kClusterChunk)
+  // the coin blocks of phases 1..coin_phases over the chunk's ids (coin_kernel's bits:
+  // phase p, id -> block ((p - 1) << 40) | (id >> 9), word (id >> 5) & 15, bit id & 31)
+  const uint64_t cb0 = (slot_base + c0) >> 9;
+  const uint32_t n_cb = c1 > c0 ? (uint32_t)(((slot_base + c1 - 1) >> 9) - cb0 + 1) : 0u;  // <= kClusterCoinBlocks
+  for (uint32_t e = threadIdx.x; e < coin_phases * n_cb; e += blockDim.x) {
+    const uint32_t ph = e / n_cb, j = e - ph * n_cb;
+    uint32_t x[16];
+    chacha_block<12>(ckey, ((uint64_t)ph << 40) | (cb0 + j), coin_stream, x);
+    u32x4* dst = reinterpret_cast<u32x4*>(s_coin + (ph * kClusterCoinBlocks + j) * 16);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      u32x4 v;
+      v.x = x[4 * k]; v.y = x[4 * k + 1]; v.z = x[4 * k + 2]; v.w = x[4 * k + 3];
+      dst[k] = v;
+    }
+  }
   // the state words transposed to one element per slot (a refill reads one byte / short
   // instead of N words and N bit extractions); the host makes c0 a multiple of 32, so
   // slot c0 + i is element i
@@ -3424,10 +3409,9 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
   uint32_t s = 0;  // the lane's slot (window-relative)
   uint64_t id = 0;
   uint32_t s32 = 0, st = 0, decided = 0, decv = 0, p = 0, first = 0, coins = 0;
-  // 32-bit running offsets (n_slots < 2^32, so the coin table has < 2^30 words): the coin
-  // word of the current phase, the slot's phase-1 coin word, the phase's key row in s_ck
-  // (one add per phase instead of 64-bit address arithmetic and a multiply)
-  const uint32_t nw32 = (uint32_t)n_words;
+  // running offsets: the LDS coin word of the current phase, the slot's phase-1 coin word,
+  // the phase's key row in s_ck (one add per phase instead of address arithmetic)
+  constexpr uint32_t kCoinRow = kClusterCoinBlocks * 16;
   uint32_t c_off = 0, c_w1 = 0, k_off = 0;
   for (;;) {
     const unsigned long long idle = __ballot(!active);
@@ -3446,7 +3430,7 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
           s32 = slot_fold32(id);
           st = s_stb[s - (uint32_t)c0];
           decided = decv = first = coins = 0;
-          c_w1 = c_off = s >> 5;
+          c_w1 = c_off = (uint32_t)((id >> 5) - (cb0 << 4));
           k_off = 0;
           p = 1;
           active = true;
@@ -3456,12 +3440,10 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
     if (!__ballot(active)) break;
     if (!active) continue;
     // ---- one phase of every replica of slot s (same rules as wmvc_cluster_kernel)
-    // the coin word of this phase, loaded ahead (its latency hides behind the heard sets)
-    // (unconditional: a conditional load meant a register zeroed with a load into it still
-    // in flight, so the compiler put a vmcnt(0) wait at the top of every phase, which also
-    // waited for the previous phase's info store; phase 1's row stands in for later phases)
+    // the coin word of this phase, read ahead (its latency hides behind the heard sets;
+    // unconditional, phase 1's row standing in for later phases)
     const bool coin_tabbed = p <= coin_phases;
-    const uint32_t coin_w = coin_tab[coin_tabbed ? c_off : c_w1];
+    const uint32_t coin_w = s_coin[coin_tabbed ? c_off : c_w1];
     uint32_t ck[2][N];
     if (p <= kKeyPhases) {
 #pragma unroll
@@ -3503,7 +3485,7 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
       const uint32_t v1 = packed_compress<N>(H & ~some0), vq = packed_compress<N>(some1 & some0);
       uint32_t coin_word = coin_w;  // consumed here, as in the unpacked body below
       asm volatile("" : "+v"(coin_word));
-      coin_tab_bit = (coin_word >> (s & 31)) & 1u;
+      coin_tab_bit = (coin_word >> ((uint32_t)id & 31u)) & 1u;
       // round 2 (fp1 = q): d0 = none of V1 / VQ heard, d1 = only V1 heard; undecided:
       // 1 if only V1 / VQ heard and some V1, the coin if only VQ heard
       const uint32_t rv1 = __umul24(v1, rep), rvq = __umul24(vq, rep);
@@ -3534,7 +3516,7 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
       // let its register be reused, which put a wait for it at the top of the next phase)
       uint32_t coin_word = coin_w;
       asm volatile("" : "+v"(coin_word));  // (materialised here: the compiler would sink it into the coin branch)
-      coin_tab_bit = (coin_word >> (s & 31)) & 1u;
+      coin_tab_bit = (coin_word >> ((uint32_t)id & 31u)) & 1u;
 #pragma unroll
       for (int r = 0; r < N; r++) {
         const uint32_t c1r = __builtin_popcount(hm[1][r] & v1), cq = __builtin_popcount(hm[1][r] & vq);
@@ -3585,7 +3567,7 @@ __global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* st
       active = false;
     } else {
       p++;
-      c_off += nw32;
+      c_off += kCoinRow;
       k_off += 2 * N;
     }
   }

@@ -414,9 +414,9 @@ def test_wmvc_cluster_fused_bitmaps(S):
 
 @pytest.mark.parametrize("slot_base", [512, 1 + 32 * 7, 1000, (1 << 40) + 300, 479])
 def test_wmvc_cluster_slot_base_offsets(oracle, slot_base):
-    """The coin table's word shift (slot_base mod 512: whole words and a bit offset,
-    both, or none) against the CPU restatement, n = 5, and past the 8 tabled phases
-    (inline coins) for a few slots."""
+    """The coin table's block alignment (slot_base mod 512: a chunk's slots start inside
+    an LDS coin block at a whole-word and a bit offset, both, or none) against the CPU
+    restatement, n = 5, and past the 8 tabled phases (inline coins) for a few slots."""
     torch = torch_cuda()
     n, S = 5, 300_001
     q, fp1 = n // 2 + 1, (n - 1) // 2 + 1
