@@ -3312,7 +3312,10 @@ static_assert(packed_compress_exact<1>() && packed_compress_exact<3>() && packed
 constexpr uint32_t kClusterChunk = 8192;
 constexpr uint32_t kClusterCoinBlocks = kClusterChunk / 512 + 1;  // blocks a chunk's slots span, per phase
 template <int N, int Q, bool PK = false>
-__global__ __launch_bounds__(256) void wmvc_cluster_lc_kernel(const uint32_t* states, uint64_t stride,
+#ifndef RG_CLUSTER_WAVES
+#define RG_CLUSTER_WAVES 6  // waves per SIMD asked of n <= 6 (larger n: spills); n = 5 packed: 83 -> 80 VGPRs, 5 -> 6 waves per SIMD: 0.2724 / 0.2732 / 0.2723 -> 0.2683 / 0.2695 / 0.2686 ms per C3 step (profiles/r06/c3_occ_ab.json)
+#endif
+__global__ __launch_bounds__(256, (N <= 6 ? RG_CLUSTER_WAVES : 1)) void wmvc_cluster_lc_kernel(const uint32_t* states, uint64_t stride,
                                                               uint64_t n_slots, uint64_t slot_base, uint32_t q_rt,
                                                               uint32_t fp1, Key ckey, uint64_t coin_stream,
                                                               uint64_t dseed, uint32_t max_phases, uint32_t* info,
