@@ -539,7 +539,8 @@ __device__ __forceinline__ void block_reduce_totals(unsigned long long (&v)[7], 
 }
 
 template <int FIN>
-__device__ __forceinline__ void step_commit(const StepParams& p, Record* rec, const unsigned long long (&v)[7]);
+__device__ __forceinline__ void step_commit(const StepParams& p, const unsigned long long (&v)[7], const DevState& s,
+                                            unsigned long long err);
 
 // Publish this tile's statistics; the tile with the last index folds every
 // tile's granules, advances the device engine state and writes the step result.
@@ -602,7 +603,9 @@ __device__ __forceinline__ void finish_tile(const StepParams& p, Record* rec, Ti
   block_reduce_totals<BLOCK>(v, lane, wave);
   stamp(p, tile, 5, tid);
   if (tid != 0) return;
-  step_commit<FIN>(p, rec, v);
+  // (loading the state ahead of the granule polls and the error word beside the block fold
+  // measured 0.5-0.8 us slower on the 2^20 sweep, profiles/r06/sweep_quad_ab.json)
+  step_commit<FIN>(p, v, *p.state, atomicAdd(&rec->error.v, 0ull));
 }
 
 // The launch's totals (dec v1 pend draws max(id+1) min(id) fault) -> step result and
@@ -610,9 +613,11 @@ __device__ __forceinline__ void finish_tile(const StepParams& p, Record* rec, Ti
 // writes only the DevState fields it owns: the sharded step may run on one stream
 // while the fix-up and commit of an earlier window (rng_next, last_committed,
 // commit_watermark, steps) run on another.
+// s: the engine state as the launch found it; err0: the launch record's error word.
 template <int FIN>
-__device__ __forceinline__ void step_commit(const StepParams& p, Record* rec, const unsigned long long (&v)[7]) {
-  const unsigned long long err = atomicAdd(&rec->error.v, 0ull) | v[6];
+__device__ __forceinline__ void step_commit(const StepParams& p, const unsigned long long (&v)[7], const DevState& s,
+                                            unsigned long long err0) {
+  const unsigned long long err = err0 | v[6];
   DevResult r;
   r.n_slots = p.n_slots;
   r.n_decided = v[0];
@@ -630,7 +635,7 @@ __device__ __forceinline__ void step_commit(const StepParams& p, Record* rec, co
     // leaves shard_draws alone: the fix-up re-draws every VQ slot at its global position)
     r.last_committed_max = v[4] ? v[4] - 1 : 0;
     r.first_undecided = fu;
-    r.rng_next = p.state->shard_draws + r.n_draws;
+    r.rng_next = s.shard_draws + r.n_draws;
     r.commit_watermark = 0;
     r.flags = err;
     if (p.n_win <= 1) p.state->shard_draws = r.rng_next;
@@ -638,7 +643,6 @@ __device__ __forceinline__ void step_commit(const StepParams& p, Record* rec, co
     if (p.result_user) *p.result_user = r;
     return;
   }
-  DevState s = *p.state;
   unsigned long long lc = s.last_committed;          // commit_phase: monotonic max,
   if (v[4] && v[4] - 1 > lc) lc = v[4] - 1;          // state.rs:77-99
   unsigned long long wm = s.commit_watermark;
@@ -769,6 +773,51 @@ __device__ __forceinline__ void r2_decision_ab(const uint32_t (&lo)[N][W], const
 // The R2 loads go out after the round-1 tally (the R1 registers are dead by then),
 // so the kernel fits 4 waves per SIMD: two 512-thread tiles resident per CU, one
 // tile's look-back overlapping the other's loads.
+// ChaCha block computed by the 4 lanes of a quad (rand_chacha 0.3.1 layout, as
+// chacha_block): lane q holds column q (words q, 4+q, 8+q, 12+q), so a column round
+// is one quarter round per lane; for a diagonal round lane q takes rows b, c, d from
+// lanes q+1, q+2, q+3 of its quad (DPP quad permutes) and hands them back after it.
+// A quarter of the dependent-instruction chain of one lane per block. Every lane of
+// a quad must be active.
+__device__ __forceinline__ uint32_t quad_rot(uint32_t v, int by) {  // lane q <- lane (q + by) & 3
+  if (by == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x39, 0xF, 0xF, false);
+  if (by == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x93, 0xF, 0xF, false);
+}
+template <int ROUNDS>
+__device__ __forceinline__ void chacha_block_quad(const Key& key, uint64_t counter, uint64_t stream, int q,
+                                                  uint32_t (&o)[4]) {
+  // the key words as wave-uniform values first: selecting among struct fields by a
+  // lane index otherwise becomes a per-lane load from the kernel arguments (a vector
+  // memory load whose wait covers every plane load in flight)
+  uint32_t k[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) k[i] = __builtin_amdgcn_readfirstlane(key.k[i]);
+  const uint32_t a0 = q == 0 ? 0x61707865u : (q == 1 ? 0x3320646eu : (q == 2 ? 0x79622d32u : 0x6b206574u));
+  const uint32_t b0 = q == 0 ? k[0] : (q == 1 ? k[1] : (q == 2 ? k[2] : k[3]));
+  const uint32_t c0 = q == 0 ? k[4] : (q == 1 ? k[5] : (q == 2 ? k[6] : k[7]));
+  const uint32_t d0 = q == 0 ? (uint32_t)counter
+                             : (q == 1 ? (uint32_t)(counter >> 32) : (q == 2 ? (uint32_t)stream : (uint32_t)(stream >> 32)));
+  uint32_t a = a0, b = b0, c = c0, d = d0;
+#define RG_QR1()                                  \
+  a += b; d = rotl32(d ^ a, 16);                  \
+  c += d; b = rotl32(b ^ c, 12);                  \
+  a += b; d = rotl32(d ^ a, 8);                   \
+  c += d; b = rotl32(b ^ c, 7);
+#pragma unroll
+  for (int r = 0; r < ROUNDS; r += 2) {
+    RG_QR1()
+    b = quad_rot(b, 1); c = quad_rot(c, 2); d = quad_rot(d, 3);
+    RG_QR1()
+    b = quad_rot(b, 3); c = quad_rot(c, 2); d = quad_rot(d, 1);
+  }
+#undef RG_QR1
+  o[0] = a + a0; o[1] = b + b0; o[2] = c + c0; o[3] = d + d0;
+}
+
+#ifndef RG_STEP_QUAD
+#define RG_STEP_QUAD 1
+#endif
 template <int N, int W, int BLOCK, bool SHARD>
 __global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p_arg) {
   StepParams p = p_arg;
@@ -896,11 +945,26 @@ __global__ __launch_bounds__(BLOCK, 4) void ref_step_kernel(StepParams p_arg) {
     mq[i] = r1vq[i];
   }
   if (tile_total) {
-    constexpr int kRows = BLOCK < 128 ? BLOCK : 128;
+    // RG_STEP_QUAD: block r by the lanes 4r .. 4r + 3 (chacha_block_quad: a quarter of one
+    // lane's dependent chain), else one block per thread. The draws sit on the launch's
+    // critical path after the look-back; a small tile has few of them (a 4,096-slot tile of
+    // the 2^20 sweep: ~5 blocks), so the chain's latency, not the issue, is what counts.
+    constexpr int kRows = RG_STEP_QUAD ? BLOCK / 4 : (BLOCK < 128 ? BLOCK : 128);
     __shared__ uint32_t s_blk[kRows][17];  // +1 word: conflict-free rows
     const unsigned long long b_first = k_tile >> 3, b_last = (k_tile + tile_total - 1) >> 3;
     for (unsigned long long cb = b_first; cb <= b_last; cb += kRows) {
-      if (tid < kRows && cb + tid <= b_last) {
+      if constexpr (RG_STEP_QUAD != 0) {
+        const uint32_t r = (uint32_t)tid >> 2;  // (quad-uniform condition)
+        if (cb + r <= b_last) {
+          uint32_t o[4];
+          chacha_block_quad<12>(p.key, cb + r, 0, tid & 3, o);
+          const int q = tid & 3;
+          s_blk[r][q] = o[0];
+          s_blk[r][4 + q] = o[1];
+          s_blk[r][8 + q] = o[2];
+          s_blk[r][12 + q] = o[3];
+        }
+      } else if (tid < kRows && cb + tid <= b_last) {
         uint32_t x[16];
         chacha_block<12>(p.key, cb + tid, 0, x);
 #pragma unroll
@@ -1135,48 +1199,6 @@ __device__ __forceinline__ void lds_st(uint32_t* s, const uint32_t (&v)[W]) {
   } else {
     s[0] = v[0];
   }
-}
-
-// ChaCha block computed by the 4 lanes of a quad (rand_chacha 0.3.1 layout, as
-// chacha_block): lane q holds column q (words q, 4+q, 8+q, 12+q), so a column round
-// is one quarter round per lane; for a diagonal round lane q takes rows b, c, d from
-// lanes q+1, q+2, q+3 of its quad (DPP quad permutes) and hands them back after it.
-// A quarter of the dependent-instruction chain of one lane per block. Every lane of
-// a quad must be active.
-__device__ __forceinline__ uint32_t quad_rot(uint32_t v, int by) {  // lane q <- lane (q + by) & 3
-  if (by == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x39, 0xF, 0xF, false);
-  if (by == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x93, 0xF, 0xF, false);
-}
-template <int ROUNDS>
-__device__ __forceinline__ void chacha_block_quad(const Key& key, uint64_t counter, uint64_t stream, int q,
-                                                  uint32_t (&o)[4]) {
-  // the key words as wave-uniform values first: selecting among struct fields by a
-  // lane index otherwise becomes a per-lane load from the kernel arguments (a vector
-  // memory load whose wait covers every plane load in flight)
-  uint32_t k[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) k[i] = __builtin_amdgcn_readfirstlane(key.k[i]);
-  const uint32_t a0 = q == 0 ? 0x61707865u : (q == 1 ? 0x3320646eu : (q == 2 ? 0x79622d32u : 0x6b206574u));
-  const uint32_t b0 = q == 0 ? k[0] : (q == 1 ? k[1] : (q == 2 ? k[2] : k[3]));
-  const uint32_t c0 = q == 0 ? k[4] : (q == 1 ? k[5] : (q == 2 ? k[6] : k[7]));
-  const uint32_t d0 = q == 0 ? (uint32_t)counter
-                             : (q == 1 ? (uint32_t)(counter >> 32) : (q == 2 ? (uint32_t)stream : (uint32_t)(stream >> 32)));
-  uint32_t a = a0, b = b0, c = c0, d = d0;
-#define RG_QR1()                                  \
-  a += b; d = rotl32(d ^ a, 16);                  \
-  c += d; b = rotl32(b ^ c, 12);                  \
-  a += b; d = rotl32(d ^ a, 8);                   \
-  c += d; b = rotl32(b ^ c, 7);
-#pragma unroll
-  for (int r = 0; r < ROUNDS; r += 2) {
-    RG_QR1()
-    b = quad_rot(b, 1); c = quad_rot(c, 2); d = quad_rot(d, 3);
-    RG_QR1()
-    b = quad_rot(b, 3); c = quad_rot(c, 2); d = quad_rot(d, 1);
-  }
-#undef RG_QR1
-  o[0] = a + a0; o[1] = b + b0; o[2] = c + c0; o[3] = d + d0;
 }
 
 // Plane access of the lag kernel through buffer resources: the tile's uniform base in
@@ -1991,7 +2013,7 @@ __global__ __launch_bounds__(BLOCK, OCC) RG_LAG_REGS void ref_lag_kernel(StepPar
   atomic_store_agent(&nxt->error.v, 0ull);
   atomic_store_agent(&nxt->ticket.v, 0ull);
   atomic_store_agent(&nxt->done.v, 0ull);
-  step_commit<SHARD ? kFinShard : kFinRef>(p, rec, v);
+  step_commit<SHARD ? kFinShard : kFinRef>(p, v, *p.state, atomicAdd(&rec->error.v, 0ull));
 }
 
 // ============================================================================

@@ -97,7 +97,7 @@ for step in "$@"; do
     stamps) run stamps 300 python tools/lag_stamps.py ;;
     stamps_shard) STAMP_SHARD=1 run stamps_shard 300 python tools/lag_stamps.py ;;
     shard_probe) run shard_probe 300 python tools/shard_step_probe.py ;;
-    latency) run latency 300 python tools/latency_1m.py ;;
+    latency) run "latency$sfx" 300 python tools/latency_1m.py ;;
     warm) run "warm$sfx" 300 env ${arg:+PROBE_ZERO=1} python tools/warm_probe.py ;;
     driver) run "driver$sfx" 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
     gloo2) run gloo2 300 python bench.py --gpus 2 --backend gloo --steps 5 --warmup 2 --no-cpu-baseline ;;
