@@ -544,7 +544,10 @@ __device__ __forceinline__ void step_commit(const StepParams& p, const unsigned 
 
 // Publish this tile's statistics; the tile with the last index folds every
 // tile's granules, advances the device engine state and writes the step result.
-template <int FIN, int BLOCK, int W, int kBatch = 8>  // kBatch: tiles per thread with loads in flight together
+#ifndef RG_FOLD_PREFETCH
+#define RG_FOLD_PREFETCH 1
+#endif
+template <int FIN, int BLOCK, int W, int kBatch = 4>  // kBatch: tiles per thread with loads in flight together (4: the prefetched state fits without spills)
 __device__ __forceinline__ void finish_tile(const StepParams& p, Record* rec, TileStats ts,
                                             uint32_t tile, int tid, int lane, int wave) {
   constexpr uint64_t kTileSlots = (uint64_t)BLOCK * W * 32;
@@ -558,6 +561,13 @@ __device__ __forceinline__ void finish_tile(const StepParams& p, Record* rec, Ti
     atomic_store_agent(g + 1, tag | ((unsigned long long)mn << 34) | ((unsigned long long)b.max_off1 << 17) | b.draws);
   }
   if (tile != p.n_tiles - 1) return;
+#if RG_FOLD_PREFETCH
+  // the engine state for step_commit, loaded by every thread ahead of the granule polls (a
+  // load under `if (tid == 0)` is waited for at once; unconditional, its round trip hides
+  // behind the polls). The state changes only in this launch's step_commit and in earlier,
+  // stream-ordered launches.
+  const DevState st = *p.state;
+#endif
 
   unsigned long long v[7] = {0, 0, 0, 0, 0, ~0ull, 0};  // dec v1 pend draws max(id+1) min(id) fault
   constexpr unsigned long long kTagMask = ~0ull << 51;
@@ -600,12 +610,20 @@ __device__ __forceinline__ void finish_tile(const StepParams& p, Record* rec, Ti
       if (mn != kStatNone && tb + mn < v[5]) v[5] = tb + mn;
     }
   }
+#if RG_FOLD_PREFETCH
+  // every tile's granules are in, so are the error bits it raised before publishing them:
+  // the error word's read goes out now, from every thread (one line per wave), beside the
+  // block fold
+  const unsigned long long err = atomic_load_agent(&rec->error.v);
+#endif
   block_reduce_totals<BLOCK>(v, lane, wave);
   stamp(p, tile, 5, tid);
   if (tid != 0) return;
-  // (loading the state ahead of the granule polls and the error word beside the block fold
-  // measured 0.5-0.8 us slower on the 2^20 sweep, profiles/r06/sweep_quad_ab.json)
+#if RG_FOLD_PREFETCH
+  step_commit<FIN>(p, v, st, err);
+#else
   step_commit<FIN>(p, v, *p.state, atomicAdd(&rec->error.v, 0ull));
+#endif
 }
 
 // The launch's totals (dec v1 pend draws max(id+1) min(id) fault) -> step result and
